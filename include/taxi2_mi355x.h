@@ -1,0 +1,135 @@
+/*
+ * taxi2_mi355x.h -- C ABI of the MI355X all-pairs genetic-distance engine.
+ *
+ * Drop-in boundary for the TaxI2 versusAll / versusReference hot path.  Today the
+ * reference crosses into native code once per pair and per metric, with the GIL held:
+ *
+ *   Biopython (C)  PairwiseAligner(**Scores).align(x, y)[0]
+ *                  src/itaxotools/taxi2/align.py:75, 151-157   (via versus_all.py:527-533,
+ *                  versus_reference.py:100-106)
+ *   calc (Rust)    seq_distances_p / _p_gaps / _jukes_cantor / _kimura2p (str, str) -> f64
+ *                  src/itaxotools/taxi2/distances.py:323, 331, 339, 347
+ *                  (via versus_all.py:546-552, versus_reference.py:119-129)
+ *
+ * This library replaces both with batched entry points: one call covers a block of
+ * pairs, aligns them (when requested) and evaluates every requested metric for both
+ * ordered orientations on the GPU.  Every entry point is plain C: pointers and sizes,
+ * no torch or HIP types.  Bind it from Python with ctypes (taxi2_amd/_native.py), which
+ * releases the GIL for the duration of each call.
+ *
+ * Conventions
+ *   - Return value: 0 on success, < 0 on error; taxi2_last_error() describes the last
+ *     error of that context.  Nothing aborts the process.
+ *   - Undefined distances (0/0, log of <= 0 -- the cases the reference maps to None at
+ *     distances.py:291-292) are written as NaN or +/-inf; the host wrapper maps both to None.
+ *   - Ownership: the caller owns every host buffer it passes (inputs and outputs); the
+ *     context owns all device memory.  *_dev entry points take device pointers that the
+ *     caller allocated on the context's device, plus an optional hipStream_t (void*).
+ *   - Threading: one context per device; calls on one context are serialized by the
+ *     caller (the Python layer holds one context per process / GPU).
+ */
+#ifndef TAXI2_MI355X_H
+#define TAXI2_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct taxi2_ctx taxi2_ctx;
+
+/* align.py:17-35 Scores, same field order as Scores.defaults. */
+typedef struct {
+    int32_t match_score;
+    int32_t mismatch_score;
+    int32_t internal_open_gap_score;
+    int32_t internal_extend_gap_score;
+    int32_t end_open_gap_score;
+    int32_t end_extend_gap_score;
+} taxi2_scores;
+
+/* distances.py:319-348 metric labels p, p-gaps, jc, k2p. */
+enum {
+    TAXI2_METRIC_P = 0,
+    TAXI2_METRIC_P_GAPS = 1,
+    TAXI2_METRIC_JC = 2,
+    TAXI2_METRIC_K2P = 3
+};
+
+/* Sequence set modes.
+ *   PREALIGNED: params.pairs.align == False (versus_all.py:522-533): strings are compared
+ *               column by column as given (case-insensitive ACGT, '-' gaps).
+ *   ALIGN:      params.pairs.align == True: strings are the normalized sequences
+ *               (sequences.py:20-25, done by the caller) and every pair is globally
+ *               aligned first (Gotoh; NW when every open == extend). */
+enum { TAXI2_MODE_PREALIGNED = 0, TAXI2_MODE_ALIGN = 1 };
+
+/* ---- context ----------------------------------------------------------------------- */
+int taxi2_device_count(void);
+int taxi2_ctx_create(int device, taxi2_ctx** out);
+void taxi2_ctx_destroy(taxi2_ctx* ctx);
+const char* taxi2_last_error(const taxi2_ctx* ctx);
+/* Replaces nothing in the reference; reports the build (kernel variants, arch). */
+const char* taxi2_version(void);
+
+/* ---- sequence sets ------------------------------------------------------------------ *
+ * Replaces the per-pair str -> Rust/C conversion of each call: the set is uploaded once
+ * (raw bytes, offsets[n+1]) and packed on the GPU (per-sequence length / first / last
+ * ACGT index; 2-bit + validity + gap bit-planes in PREALIGNED mode). */
+int taxi2_set_create(taxi2_ctx* ctx, const uint8_t* bytes, const int64_t* offsets, int64_t n,
+                     int mode, int* set_id);
+int taxi2_set_destroy(taxi2_ctx* ctx, int set_id);
+int taxi2_set_info(taxi2_ctx* ctx, int set_id, int64_t* n, int32_t* max_len, int* mode);
+
+/* ---- versusAll block (versus_all.py:746-752: fromProduct -> align -> calculate) ------ *
+ * Unordered pairs with linear index k in [k0, k0 + count) of the row-major upper triangle
+ * of `set` (a < b; k = a*(2N-a-1)/2 + (b-a-1)).
+ *   ALIGN:      out[count][2][nmetrics]: [k][0][m] = metric m of (a, b) (target a, query b),
+ *               [k][1][m] = metric m of (b, a).  scores_out[count] (nullable) = the optimal
+ *               global alignment score.
+ *   PREALIGNED: out[count][nmetrics] (the p/p-gaps/jc/k2p counters are symmetric, so one
+ *               value serves both ordered pairs); scores_out must be NULL.
+ * The diagonal rule of versus_all.py:549 (x == y -> None) is the caller's business. */
+int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
+                    const int32_t* metrics, int nmetrics, double* out, int32_t* scores_out);
+
+/* Same with device-resident outputs (d_out / d_scores on the context's device); `stream`
+ * is a hipStream_t or NULL for the context's own stream.  Asynchronous. */
+int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count,
+                        const taxi2_scores* sc, const int32_t* metrics, int nmetrics,
+                        double* d_out, int32_t* d_scores, void* stream);
+
+/* ---- rectangle (versus_reference.py:225-229, decontaminate.py:336-371 shape) ---------- *
+ * Pairs (q, r) for q in [q0, q1) of set_q and every r of set_r, row-major:
+ *   out[(q - q0) * R + r][nmetrics] -- orientation (query, reference) only.
+ * scores_out[(q - q0) * R + r] (nullable, ALIGN only). */
+int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1,
+                     const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* out,
+                     int32_t* scores_out);
+
+/* ---- explicit pair list (align.py:50-51 align_pairs, distances.py:297 calculate) ------- *
+ * Pairs (xs[k] of set_x, ys[k] of set_y): out[count][2][nmetrics] in ALIGN mode
+ * ([k][0] = (x, y), [k][1] = (y, x)), out[count][nmetrics] in PREALIGNED mode. */
+int taxi2_list_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
+                     int64_t count, const taxi2_scores* sc, const int32_t* metrics, int nmetrics,
+                     double* out, int32_t* scores_out);
+
+/* ---- versusReference closest (versus_reference.py:184-188 get_minimum_distances) ------ *
+ * For each query q in [q0, q1): the reference index with the smallest `scale * primary`
+ * metric (NaN/inf skipped, first minimum wins, -0.0 == +0.0; scale = 100 reproduces the
+ * percentage_multiply adjustment that versus_reference.py:232 applies before min()), the
+ * unscaled value, and -- for that pair only -- every metric in `metrics`
+ * (versus_reference.py:124-129).  idx_out[q - q0] = -1 when all values are undefined (the
+ * reference raises ValueError from min() there).
+ *   idx_out[nq], d_out[nq], extra_out[nq][nmetrics] (nullable),
+ *   primary_out[nq][R] (nullable: the full primary matrix for the linear/matrix writers). */
+int taxi2_closest(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1,
+                  const taxi2_scores* sc, int32_t primary, double scale, const int32_t* metrics,
+                  int nmetrics, int64_t* idx_out, double* d_out, double* extra_out,
+                  double* primary_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TAXI2_MI355X_H */

@@ -1,0 +1,389 @@
+"""ctypes binding to ``libtaxi2_mi355x.so`` (the C ABI declared in ``include/taxi2_mi355x.h``).
+
+This is the only way the product reaches the GPU.  There is no CPU fallback: if the library
+is missing or no GPU is visible, constructing an :class:`Engine` raises
+:class:`NativeError`.  ctypes releases the GIL for every call.
+
+Replaces the reference's per-pair native crossings (``align.py:75,152`` Biopython C,
+``distances.py:323-347`` Rust ``calc.seq_distances_*``) with batched calls.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+from typing import Iterable, Sequence as Seq
+
+import numpy as np
+
+LIB_DIR = Path(__file__).resolve().parent / "_lib"
+LIB_PATH = LIB_DIR / "libtaxi2_mi355x.so"
+HEADER_PATH = Path(__file__).resolve().parent.parent / "include" / "taxi2_mi355x.h"
+
+# Every symbol include/taxi2_mi355x.h declares.
+EXPORTS = (
+    "taxi2_device_count",
+    "taxi2_ctx_create",
+    "taxi2_ctx_destroy",
+    "taxi2_last_error",
+    "taxi2_version",
+    "taxi2_set_create",
+    "taxi2_set_destroy",
+    "taxi2_set_info",
+    "taxi2_all_pairs",
+    "taxi2_all_pairs_dev",
+    "taxi2_rect_pairs",
+    "taxi2_list_pairs",
+    "taxi2_closest",
+)
+
+MODE_PREALIGNED = 0
+MODE_ALIGN = 1
+
+METRIC_CODES = {"p": 0, "p-gaps": 1, "jc": 2, "k2p": 3}
+MAX_METRICS = 8
+
+
+class NativeError(RuntimeError):
+    """The MI355X engine is unavailable or reported an error."""
+
+
+class CScores(ctypes.Structure):
+    _fields_ = [
+        ("match_score", ctypes.c_int32),
+        ("mismatch_score", ctypes.c_int32),
+        ("internal_open_gap_score", ctypes.c_int32),
+        ("internal_extend_gap_score", ctypes.c_int32),
+        ("end_open_gap_score", ctypes.c_int32),
+        ("end_extend_gap_score", ctypes.c_int32),
+    ]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_INT = ctypes.c_int
+
+_SIGNATURES = {
+    "taxi2_device_count": (_INT, []),
+    "taxi2_ctx_create": (_INT, [_INT, ctypes.POINTER(_P)]),
+    "taxi2_ctx_destroy": (None, [_P]),
+    "taxi2_last_error": (ctypes.c_char_p, [_P]),
+    "taxi2_version": (ctypes.c_char_p, []),
+    "taxi2_set_create": (_INT, [_P, _P, _P, _I64, _INT, ctypes.POINTER(_INT)]),
+    "taxi2_set_destroy": (_INT, [_P, _INT]),
+    "taxi2_set_info": (_INT, [_P, _INT, ctypes.POINTER(_I64), ctypes.POINTER(_I32), ctypes.POINTER(_INT)]),
+    "taxi2_all_pairs": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
+    "taxi2_all_pairs_dev": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
+    "taxi2_rect_pairs": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
+    "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
+    "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
+                             _P, _INT, _P, _P, _P, _P]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library() -> ctypes.CDLL:
+    """Load the in-tree engine library (raises NativeError when it is absent)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            raise NativeError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(or `make -C taxi2_amd/csrc`).  There is no CPU fallback."
+            )
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name in EXPORTS:
+            fn = getattr(lib, name)  # AttributeError = missing export
+            res, args = _SIGNATURES[name]
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def device_count() -> int:
+    return int(load_library().taxi2_device_count())
+
+
+def version() -> str:
+    return load_library().taxi2_version().decode()
+
+
+def to_cscores(scores) -> CScores:
+    """``align.Scores`` / mapping / 6-tuple -> C struct (field order = Scores.defaults)."""
+    if scores is None:
+        vals = (1, -1, -8, -1, -1, -1)
+    elif isinstance(scores, dict):
+        vals = tuple(
+            scores[k]
+            for k in (
+                "match_score",
+                "mismatch_score",
+                "internal_open_gap_score",
+                "internal_extend_gap_score",
+                "end_open_gap_score",
+                "end_extend_gap_score",
+            )
+        )
+    else:
+        vals = tuple(scores)
+    ints = []
+    for v in vals:
+        if int(v) != v:
+            raise ValueError(f"alignment scores must be integers (got {v!r})")
+        ints.append(int(v))
+    return CScores(*ints)
+
+
+def metric_codes(metrics: Iterable) -> np.ndarray:
+    codes = []
+    for m in metrics:
+        label = m if isinstance(m, str) else str(m)
+        if label not in METRIC_CODES:
+            raise NativeError(f"metric {label!r} is not computed by the MI355X engine")
+        codes.append(METRIC_CODES[label])
+    if not 1 <= len(codes) <= MAX_METRICS:
+        raise NativeError(f"between 1 and {MAX_METRICS} metrics per call")
+    return np.asarray(codes, dtype=np.int32)
+
+
+def encode_sequences(seqs: Seq[str], *, strict: bool) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate sequences as bytes + int64 offsets.
+
+    Characters are handled as latin-1 bytes.  In align mode (``strict``) a character outside
+    latin-1 raises ValueError instead of silently changing which letters compare equal.
+    """
+    errors = "strict" if strict else "replace"
+    enc = [s.encode("latin-1", errors=errors) for s in seqs]
+    offs = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        offs[1:] = np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc)))
+    buf = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8)
+    return buf, offs
+
+
+class SeqSet:
+    """A sequence set resident in HBM (freed with the engine or by ``free``)."""
+
+    def __init__(self, engine: "Engine", set_id: int, n: int, max_len: int, mode: int):
+        self.engine = engine
+        self.id = set_id
+        self.n = n
+        self.max_len = max_len
+        self.mode = mode
+
+    @property
+    def aligned(self) -> bool:
+        return self.mode == MODE_ALIGN
+
+    def free(self) -> None:
+        if self.id >= 0:
+            self.engine._lib.taxi2_set_destroy(self.engine._ctx, self.id)
+            self.id = -1
+
+
+class Engine:
+    """One engine context per GPU (one process per GPU for multi-GPU runs)."""
+
+    _default: dict[int, "Engine"] = {}
+
+    def __init__(self, device: int | None = None):
+        lib = load_library()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        n = lib.taxi2_device_count()
+        if n <= 0:
+            raise NativeError("no HIP device visible; the MI355X engine has no CPU fallback")
+        ctx = _P()
+        rc = lib.taxi2_ctx_create(int(device), ctypes.byref(ctx))
+        if rc != 0:
+            raise NativeError(f"taxi2_ctx_create(device={device}) failed with {rc}")
+        self._lib = lib
+        self._ctx = ctx
+        self.device = int(device)
+        self._lock = threading.Lock()
+
+    @classmethod
+    def default(cls, device: int | None = None) -> "Engine":
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        eng = cls._default.get(device)
+        if eng is None:
+            eng = cls._default[device] = cls(device)
+        return eng
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.taxi2_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            msg = self._lib.taxi2_last_error(self._ctx)
+            raise NativeError(f"{what}: {msg.decode() if msg else rc}")
+
+    # ------------------------------------------------------------------ sets
+    def upload(self, seqs: Seq[str], *, align: bool) -> SeqSet:
+        buf, offs = encode_sequences(seqs, strict=align)
+        return self.upload_packed(buf, offs, align=align)
+
+    def upload_packed(self, buf: np.ndarray, offs: np.ndarray, *, align: bool) -> SeqSet:
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        n = len(offs) - 1
+        sid = _INT()
+        mode = MODE_ALIGN if align else MODE_PREALIGNED
+        with self._lock:
+            self._check(
+                self._lib.taxi2_set_create(self._ctx, buf.ctypes.data, offs.ctypes.data, n, mode, ctypes.byref(sid)),
+                "taxi2_set_create",
+            )
+            nn, ml, md = _I64(), _I32(), _INT()
+            self._check(
+                self._lib.taxi2_set_info(self._ctx, sid.value, ctypes.byref(nn), ctypes.byref(ml), ctypes.byref(md)),
+                "taxi2_set_info",
+            )
+        return SeqSet(self, sid.value, nn.value, ml.value, md.value)
+
+    # ------------------------------------------------------------------ pair blocks
+    def all_pairs(self, s: SeqSet, k0: int, count: int, metrics, scores=None, *, with_scores=False):
+        """Upper-triangle block of ``s``.  ALIGN: (count, 2, M) [(a,b), (b,a)]; else (count, M)."""
+        codes = metric_codes(metrics)
+        shape = (count, 2, len(codes)) if s.aligned else (count, len(codes))
+        out = np.empty(shape, dtype=np.float64)
+        sc_out = np.empty(count, dtype=np.int32) if (with_scores and s.aligned) else None
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_all_pairs(
+                    self._ctx, s.id, int(k0), int(count), ctypes.byref(cs), codes.ctypes.data, len(codes),
+                    out.ctypes.data, sc_out.ctypes.data if sc_out is not None else None,
+                ),
+                "taxi2_all_pairs",
+            )
+        return (out, sc_out) if with_scores else out
+
+    def all_pairs_dev(self, s: SeqSet, k0: int, count: int, metrics, out_ptr: int, scores=None,
+                      scores_ptr: int | None = None, stream: int | None = None) -> None:
+        """Asynchronous device-output variant (pointers from e.g. torch tensors on this GPU)."""
+        codes = metric_codes(metrics)
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_all_pairs_dev(
+                    self._ctx, s.id, int(k0), int(count), ctypes.byref(cs), codes.ctypes.data, len(codes),
+                    ctypes.c_void_p(out_ptr), ctypes.c_void_p(scores_ptr) if scores_ptr else None,
+                    ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_all_pairs_dev",
+            )
+
+    def rect_pairs(self, q: SeqSet, r: SeqSet, q0: int, q1: int, metrics, scores=None, *, with_scores=False):
+        """(q1-q0)*R pairs (query, reference), row-major: (nq*R, M)."""
+        codes = metric_codes(metrics)
+        count = (q1 - q0) * r.n
+        out = np.empty((count, len(codes)), dtype=np.float64)
+        sc_out = np.empty(count, dtype=np.int32) if (with_scores and q.aligned) else None
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_rect_pairs(
+                    self._ctx, q.id, r.id, int(q0), int(q1), ctypes.byref(cs), codes.ctypes.data, len(codes),
+                    out.ctypes.data, sc_out.ctypes.data if sc_out is not None else None,
+                ),
+                "taxi2_rect_pairs",
+            )
+        return (out, sc_out) if with_scores else out
+
+    def list_pairs(self, x: SeqSet, y: SeqSet, xs, ys, metrics, scores=None, *, with_scores=False):
+        """Explicit pairs.  ALIGN: (count, 2, M) [(x,y), (y,x)]; else (count, M)."""
+        codes = metric_codes(metrics)
+        xs = np.ascontiguousarray(xs, dtype=np.int64)
+        ys = np.ascontiguousarray(ys, dtype=np.int64)
+        if xs.shape != ys.shape:
+            raise ValueError("xs and ys must have the same length")
+        count = len(xs)
+        shape = (count, 2, len(codes)) if x.aligned else (count, len(codes))
+        out = np.empty(shape, dtype=np.float64)
+        sc_out = np.empty(count, dtype=np.int32) if (with_scores and x.aligned) else None
+        cs = to_cscores(scores)
+        if count:
+            with self._lock:
+                self._check(
+                    self._lib.taxi2_list_pairs(
+                        self._ctx, x.id, y.id, xs.ctypes.data, ys.ctypes.data, count, ctypes.byref(cs),
+                        codes.ctypes.data, len(codes), out.ctypes.data,
+                        sc_out.ctypes.data if sc_out is not None else None,
+                    ),
+                    "taxi2_list_pairs",
+                )
+        return (out, sc_out) if with_scores else out
+
+    def closest(self, q: SeqSet, r: SeqSet, q0: int, q1: int, primary, extras=(), scores=None, *,
+                scale: float = 1.0, want_matrix: bool = False):
+        """Per query: (idx[nq], d[nq], extras[nq, E] or None, matrix[nq, R] or None)."""
+        pcode = int(metric_codes([primary])[0])
+        nq = q1 - q0
+        idx = np.empty(nq, dtype=np.int64)
+        d = np.empty(nq, dtype=np.float64)
+        ecodes = metric_codes(extras) if len(extras) else None
+        ex = np.empty((nq, len(ecodes)), dtype=np.float64) if ecodes is not None else None
+        mat = np.empty((nq, r.n), dtype=np.float64) if want_matrix else None
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_closest(
+                    self._ctx, q.id, r.id, int(q0), int(q1), ctypes.byref(cs), pcode, float(scale),
+                    ecodes.ctypes.data if ecodes is not None else None, len(ecodes) if ecodes is not None else 0,
+                    idx.ctypes.data, d.ctypes.data, ex.ctypes.data if ex is not None else None,
+                    mat.ctypes.data if mat is not None else None,
+                ),
+                "taxi2_closest",
+            )
+        return idx, d, ex, mat
+
+
+def tri_index(a: np.ndarray, b: np.ndarray, n: int) -> np.ndarray:
+    """Linear upper-triangle index of pairs a < b (row-major), as the C ABI numbers them."""
+    a = np.asarray(a, dtype=np.int64)
+    b = np.asarray(b, dtype=np.int64)
+    return a * (2 * n - a - 1) // 2 + (b - a - 1)
+
+
+def tri_pairs(n: int, k0: int = 0, count: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+    """Inverse of :func:`tri_index` for k in [k0, k0+count)."""
+    total = n * (n - 1) // 2
+    if count is None:
+        count = total - k0
+    k = np.arange(k0, k0 + count, dtype=np.int64)
+    n2 = 2.0 * n - 1.0
+    a = np.floor((n2 - np.sqrt(np.maximum(n2 * n2 - 8.0 * k, 0.0))) / 2).astype(np.int64)
+    a = np.clip(a, 0, max(n - 2, 0))
+    start = a * (2 * n - a - 1) // 2
+    over = start > k
+    while np.any(over):
+        a[over] -= 1
+        start = a * (2 * n - a - 1) // 2
+        over = start > k
+    nxt = (a + 1) * (2 * n - a - 2) // 2
+    under = (nxt <= k) & (a + 1 <= n - 2)
+    while np.any(under):
+        a[under] += 1
+        start = a * (2 * n - a - 1) // 2
+        nxt = (a + 1) * (2 * n - a - 2) // 2
+        under = (nxt <= k) & (a + 1 <= n - 2)
+    b = a + 1 + (k - start)
+    return a, b

@@ -1,0 +1,531 @@
+// C ABI implementation (include/taxi2_mi355x.h): contexts, device-resident sequence sets,
+// kernel-variant selection and chunked launches.  Single translation unit: every kernel
+// template is instantiated here for gfx950.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/taxi2_mi355x.h"
+#include "align_kernel.hpp"
+#include "common.hpp"
+#include "pack_kernels.hpp"
+#include "prealigned_kernel.hpp"
+
+using namespace taxi2;
+
+namespace {
+
+struct DevSet {
+    bool live = false;
+    int mode = 0;
+    int64_t n = 0;
+    int32_t max_len = 0;
+    int64_t nbytes = 0;
+    int64_t nwords = 0;
+    uint8_t* bytes = nullptr;
+    int64_t* offs = nullptr;
+    int4* meta = nullptr;
+    uint4* planes = nullptr;
+};
+
+}  // namespace
+
+struct taxi2_ctx {
+    int device = 0;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<DevSet> sets;
+    // reusable device staging
+    void* d_out = nullptr;
+    size_t d_out_bytes = 0;
+    void* d_aux = nullptr;
+    size_t d_aux_bytes = 0;
+};
+
+namespace {
+
+int fail(taxi2_ctx* ctx, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return -1;
+}
+
+#define HIP_TRY(ctx, expr)                                                                    \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(ctx, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+int ensure(taxi2_ctx* ctx, void** p, size_t* cap, size_t need) {
+    if (*cap >= need) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t want = std::max(need, (size_t)1 << 20);
+    HIP_TRY(ctx, hipMalloc(p, want));
+    *cap = want;
+    return 0;
+}
+
+DevSet* get_set(taxi2_ctx* ctx, int id) {
+    if (id < 0 || id >= (int)ctx->sets.size() || !ctx->sets[id].live) return nullptr;
+    return &ctx->sets[id];
+}
+
+SetView view(const DevSet& s) { return SetView{s.bytes, s.offs, s.meta, s.planes, s.n}; }
+
+int check_metrics(taxi2_ctx* ctx, const int32_t* metrics, int nm, MetricSpec& ms) {
+    if (nm < 1 || nm > MAX_METRICS) return fail(ctx, "nmetrics must be in [1, %d]", MAX_METRICS);
+    ms.n = nm;
+    for (int m = 0; m < nm; ++m) {
+        if (metrics[m] < TAXI2_METRIC_P || metrics[m] > TAXI2_METRIC_K2P)
+            return fail(ctx, "unknown metric code %d", metrics[m]);
+        ms.code[m] = metrics[m];
+    }
+    return 0;
+}
+
+KScores kscores(const taxi2_scores* s) {
+    return KScores{s->match_score, s->mismatch_score, s->internal_open_gap_score,
+                   s->internal_extend_gap_score, s->end_open_gap_score, s->end_extend_gap_score};
+}
+
+bool is_linear(const KScores& k) { return k.io == k.ie && k.eo == k.ee; }
+
+// ---------------------------------------------------------------- align variant table
+struct Variant {
+    int K, W;
+    bool linear, def;
+    const void* fn;
+    void (*launch)(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec,
+                   int, int, double*, int32_t*);
+};
+
+template <int K, int W, bool LIN, bool DEF>
+void launch_align(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView y, PairSrc ps,
+                  KScores sc, MetricSpec ms, int xcap, int om, double* out, int32_t* so) {
+    hipLaunchKernelGGL((k_align<K, W, LIN, DEF>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so);
+}
+
+#define T2_VARIANT(K, W, LIN, DEF) \
+    Variant{K, W, LIN, DEF, (const void*)&k_align<K, W, LIN, DEF>, &launch_align<K, W, LIN, DEF>}
+
+// Ordered by column capacity (64 * K * W); the first one that fits the longest sequence wins.
+// DEF = the default TaxI2 scores (align.py:20-27) as compile-time constants.
+const Variant kGotohDef[] = {
+    T2_VARIANT(4, 1, false, true), T2_VARIANT(6, 1, false, true), T2_VARIANT(8, 1, false, true),
+    T2_VARIANT(6, 2, false, true), T2_VARIANT(8, 2, false, true), T2_VARIANT(6, 4, false, true),
+    T2_VARIANT(8, 4, false, true), T2_VARIANT(8, 8, false, true),
+};
+const Variant kGotoh[] = {
+    T2_VARIANT(4, 1, false, false), T2_VARIANT(6, 1, false, false), T2_VARIANT(8, 1, false, false),
+    T2_VARIANT(6, 2, false, false), T2_VARIANT(8, 2, false, false), T2_VARIANT(6, 4, false, false),
+    T2_VARIANT(8, 4, false, false), T2_VARIANT(8, 8, false, false),
+};
+const Variant kLinear[] = {
+    T2_VARIANT(4, 1, true, false), T2_VARIANT(8, 1, true, false), T2_VARIANT(8, 2, true, false),
+    T2_VARIANT(8, 4, true, false), T2_VARIANT(8, 8, true, false),
+};
+
+bool is_default(const KScores& k) {
+    return k.ma == 1 && k.mi == -1 && k.io == -8 && k.ie == -1 && k.eo == -1 && k.ee == -1;
+}
+
+const Variant* pick_variant(const KScores& k, int max_len) {
+    const Variant* tab;
+    int n;
+    if (is_linear(k)) {
+        tab = kLinear;
+        n = (int)(sizeof kLinear / sizeof kLinear[0]);
+    } else if (is_default(k)) {
+        tab = kGotohDef;
+        n = (int)(sizeof kGotohDef / sizeof kGotohDef[0]);
+    } else {
+        tab = kGotoh;
+        n = (int)(sizeof kGotoh / sizeof kGotoh[0]);
+    }
+    for (int i = 0; i < n; ++i)
+        if (64 * tab[i].K * tab[i].W >= max_len) return &tab[i];
+    return nullptr;
+}
+
+size_t align_lds_bytes(const Variant& v, int xcap) {
+    return ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(v.W - 1) * RING * sizeof(RingEntry);
+}
+
+int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
+                       const taxi2_scores* sc, const MetricSpec& ms, int out_mode, double* d_out,
+                       int32_t* d_scores, hipStream_t st) {
+    const KScores k = kscores(sc);
+    const int max_len = std::max(X.max_len, Y.max_len);
+    if (max_len > 4095) return fail(ctx, "sequence length %d exceeds the aligner's limit of 4095", max_len);
+    const Variant* v = pick_variant(k, max_len);
+    if (!v) return fail(ctx, "sequence length %d exceeds the aligner's column capacity", max_len);
+    // int DP range check: every finite score stays far above NEG_INF
+    const long long mag = std::max({std::llabs(k.ma), std::llabs(k.mi), std::llabs(k.io),
+                                    std::llabs(k.ie), std::llabs(k.eo), std::llabs(k.ee)});
+    if (mag * (2LL * max_len + 2) >= (1LL << 27))
+        return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
+    const int xcap = std::max(max_len, 1);
+    const size_t lds = align_lds_bytes(*v, xcap);
+    if (lds > 160 * 1024) return fail(ctx, "LDS requirement %zu exceeds 160 KiB", lds);
+    if (lds > 64 * 1024)
+        HIP_TRY(ctx, hipFuncSetAttribute(v->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int64_t grid = std::min<int64_t>(ps.count, (int64_t)1 << 30);
+    if (grid <= 0) return 0;
+    v->launch(dim3((unsigned)grid), dim3(64 * v->W), lds, st, view(X), view(Y), ps, k, ms, xcap,
+              out_mode, d_out, d_scores);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
+                      const MetricSpec& ms, double* d_out, hipStream_t st) {
+    if (ps.count <= 0) return 0;
+    const int64_t blocks = std::min<int64_t>((ps.count + 255) / 256, (int64_t)ctx->num_cus * 64);
+    hipLaunchKernelGGL(k_prealigned, dim3((unsigned)blocks), dim3(256), 0, st, view(X), view(Y), ps,
+                       ms, d_out);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+// Generic chunked driver: pairs [0, count) described by `base` (k0 advanced per chunk),
+// device results copied back into host `out` (+ `scores_out`).
+int run_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, PairSrc base, const taxi2_scores* sc,
+              const MetricSpec& ms, int out_mode, double* out, int32_t* scores_out) {
+    const bool align = X.mode == TAXI2_MODE_ALIGN;
+    const int per_pair = (align && out_mode == OUT_BOTH) ? 2 * ms.n : ms.n;
+    const int64_t chunk_cap = std::max<int64_t>(1, ((int64_t)256 << 20) / (8 * per_pair + 4));
+    for (int64_t done = 0; done < base.count; done += chunk_cap) {
+        const int64_t n = std::min(chunk_cap, base.count - done);
+        if (ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)n * per_pair * 8)) return -1;
+        int32_t* d_sc = nullptr;
+        if (scores_out) {
+            if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)n * 4)) return -1;
+            d_sc = (int32_t*)ctx->d_aux;
+        }
+        PairSrc ps = base;
+        ps.k0 = base.k0 + done;
+        ps.count = n;
+        int rc = align ? launch_align_pairs(ctx, X, Y, ps, sc, ms, out_mode, (double*)ctx->d_out, d_sc,
+                                            ctx->stream)
+                       : launch_prealigned(ctx, X, Y, ps, ms, (double*)ctx->d_out, ctx->stream);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipMemcpyAsync(out + done * per_pair, ctx->d_out, (size_t)n * per_pair * 8,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        if (scores_out)
+            HIP_TRY(ctx, hipMemcpyAsync(scores_out + done, d_sc, (size_t)n * 4, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* taxi2_version(void) {
+    return "taxi2_mi355x 0.1 (gfx950; Gotoh K{4,6,8}xW{1,2,4,8} / NW K{4,8}xW{1,2,4,8}; "
+           "bit-plane pre-aligned counter)";
+}
+
+int taxi2_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int taxi2_ctx_create(int device, taxi2_ctx** out) {
+    if (!out) return -1;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return -2;
+    if (device < 0 || device >= n) return -3;
+    if (hipSetDevice(device) != hipSuccess) return -4;
+    taxi2_ctx* ctx = new taxi2_ctx();
+    ctx->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        delete ctx;
+        return -5;
+    }
+    ctx->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return -6;
+    }
+    *out = ctx;
+    return 0;
+}
+
+void taxi2_ctx_destroy(taxi2_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (int i = 0; i < (int)ctx->sets.size(); ++i) taxi2_set_destroy(ctx, i);
+    if (ctx->d_out) (void)hipFree(ctx->d_out);
+    if (ctx->d_aux) (void)hipFree(ctx->d_aux);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* taxi2_last_error(const taxi2_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int taxi2_set_create(taxi2_ctx* ctx, const uint8_t* bytes, const int64_t* offsets, int64_t n,
+                     int mode, int* set_id) {
+    if (!ctx || !offsets || !set_id || n < 0) return fail(ctx, "invalid arguments to taxi2_set_create");
+    if (mode != TAXI2_MODE_PREALIGNED && mode != TAXI2_MODE_ALIGN) return fail(ctx, "bad mode %d", mode);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    DevSet s;
+    s.mode = mode;
+    s.n = n;
+    s.nbytes = offsets[n] - offsets[0];
+    int32_t maxlen = 0;
+    std::vector<int64_t> woffs(mode == TAXI2_MODE_PREALIGNED ? n : 0);
+    std::vector<int64_t> offs0(n + 1);
+    int64_t nwords = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = offsets[i + 1] - offsets[i];
+        if (len < 0) return fail(ctx, "offsets must be non-decreasing");
+        if (len > (1 << 20)) return fail(ctx, "sequence %lld longer than 1 MiB", (long long)i);
+        maxlen = std::max<int32_t>(maxlen, (int32_t)len);
+        if (mode == TAXI2_MODE_PREALIGNED) {
+            woffs[i] = nwords;
+            nwords += (len + 31) / 32;
+        }
+    }
+    for (int64_t i = 0; i <= n; ++i) offs0[i] = offsets[i] - offsets[0];
+    if (nwords > INT32_MAX) return fail(ctx, "set too large");
+    s.max_len = maxlen;
+    s.nwords = nwords;
+    HIP_TRY(ctx, hipMalloc(&s.bytes, std::max<int64_t>(s.nbytes, 16)));
+    HIP_TRY(ctx, hipMalloc(&s.offs, (n + 1) * sizeof(int64_t)));
+    HIP_TRY(ctx, hipMalloc(&s.meta, std::max<int64_t>(n, 1) * sizeof(int4)));
+    if (s.nbytes)
+        HIP_TRY(ctx, hipMemcpyAsync(s.bytes, bytes + offsets[0], s.nbytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s.offs, offs0.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
+                                ctx->stream));
+    int64_t* d_woffs = nullptr;
+    if (mode == TAXI2_MODE_PREALIGNED && n) {
+        HIP_TRY(ctx, hipMalloc(&d_woffs, n * sizeof(int64_t)));
+        HIP_TRY(ctx, hipMemcpyAsync(d_woffs, woffs.data(), n * sizeof(int64_t), hipMemcpyHostToDevice,
+                                    ctx->stream));
+        HIP_TRY(ctx, hipMalloc(&s.planes, std::max<int64_t>(nwords, 1) * sizeof(uint4)));
+    }
+    if (n) {
+        hipLaunchKernelGGL(k_meta, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, ctx->stream, s.bytes,
+                           s.offs, d_woffs, n, s.meta);
+        HIP_TRY(ctx, hipGetLastError());
+        if (mode == TAXI2_MODE_PREALIGNED) {
+            hipLaunchKernelGGL(k_planes, dim3((unsigned)n), dim3(64), 0, ctx->stream, s.bytes, s.offs,
+                               s.meta, n, s.planes);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (d_woffs) (void)hipFree(d_woffs);
+    s.live = true;
+    ctx->sets.push_back(s);
+    *set_id = (int)ctx->sets.size() - 1;
+    return 0;
+}
+
+int taxi2_set_destroy(taxi2_ctx* ctx, int set_id) {
+    if (!ctx) return -1;
+    DevSet* s = get_set(ctx, set_id);
+    if (!s) return 0;
+    (void)hipSetDevice(ctx->device);
+    if (s->bytes) (void)hipFree(s->bytes);
+    if (s->offs) (void)hipFree(s->offs);
+    if (s->meta) (void)hipFree(s->meta);
+    if (s->planes) (void)hipFree(s->planes);
+    *s = DevSet();
+    return 0;
+}
+
+int taxi2_set_info(taxi2_ctx* ctx, int set_id, int64_t* n, int32_t* max_len, int* mode) {
+    DevSet* s = ctx ? get_set(ctx, set_id) : nullptr;
+    if (!s) return fail(ctx, "unknown set %d", set_id);
+    if (n) *n = s->n;
+    if (max_len) *max_len = s->max_len;
+    if (mode) *mode = s->mode;
+    return 0;
+}
+
+int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
+                    const int32_t* metrics, int nmetrics, double* out, int32_t* scores_out) {
+    if (!ctx) return -1;
+    DevSet* s = get_set(ctx, set);
+    if (!s) return fail(ctx, "unknown set %d", set);
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    const int64_t total = s->n * (s->n - 1) / 2;
+    if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
+    if (s->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
+    if (s->mode == TAXI2_MODE_PREALIGNED && scores_out) return fail(ctx, "no scores in PREALIGNED mode");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    PairSrc ps{PAIRS_TRI, k0, count, s->n, 0, nullptr, nullptr};
+    return run_pairs(ctx, *s, *s, ps, sc, ms, OUT_BOTH, out, scores_out);
+}
+
+int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
+                        const int32_t* metrics, int nmetrics, double* d_out, int32_t* d_scores,
+                        void* stream) {
+    if (!ctx) return -1;
+    DevSet* s = get_set(ctx, set);
+    if (!s) return fail(ctx, "unknown set %d", set);
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    const int64_t total = s->n * (s->n - 1) / 2;
+    if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairSrc ps{PAIRS_TRI, k0, count, s->n, 0, nullptr, nullptr};
+    if (s->mode == TAXI2_MODE_ALIGN) {
+        if (!sc) return fail(ctx, "scores required in ALIGN mode");
+        return launch_align_pairs(ctx, *s, *s, ps, sc, ms, OUT_BOTH, d_out, d_scores, st);
+    }
+    return launch_prealigned(ctx, *s, *s, ps, ms, d_out, st);
+}
+
+int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
+                     const int32_t* metrics, int nmetrics, double* out, int32_t* scores_out) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (Q->mode != R->mode) return fail(ctx, "query and reference sets differ in mode");
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if (Q->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
+    if (Q->mode == TAXI2_MODE_PREALIGNED && scores_out) return fail(ctx, "no scores in PREALIGNED mode");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    PairSrc ps{PAIRS_RECT, q0 * R->n, (q1 - q0) * R->n, 0, R->n, nullptr, nullptr};
+    return run_pairs(ctx, *Q, *R, ps, sc, ms, OUT_AB, out, scores_out);
+}
+
+int taxi2_list_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
+                     int64_t count, const taxi2_scores* sc, const int32_t* metrics, int nmetrics,
+                     double* out, int32_t* scores_out) {
+    if (!ctx) return -1;
+    DevSet* X = get_set(ctx, set_x);
+    DevSet* Y = get_set(ctx, set_y);
+    if (!X || !Y) return fail(ctx, "unknown set");
+    if (X->mode != Y->mode) return fail(ctx, "sets differ in mode");
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (count < 0) return fail(ctx, "negative count");
+    if (count == 0) return 0;
+    if (X->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
+    if (X->mode == TAXI2_MODE_PREALIGNED && scores_out) return fail(ctx, "no scores in PREALIGNED mode");
+    for (int64_t k = 0; k < count; ++k)
+        if (xs[k] < 0 || xs[k] >= X->n || ys[k] < 0 || ys[k] >= Y->n)
+            return fail(ctx, "pair %lld index out of bounds", (long long)k);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int64_t* d_idx = nullptr;
+    HIP_TRY(ctx, hipMalloc(&d_idx, 2 * count * sizeof(int64_t)));
+    int rc = 0;
+    do {
+        if (hipMemcpyAsync(d_idx, xs, count * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(d_idx + count, ys, count * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+            rc = fail(ctx, "pair list upload failed");
+            break;
+        }
+        PairSrc ps{PAIRS_LIST, 0, count, 0, 0, d_idx, d_idx + count};
+        rc = run_pairs(ctx, *X, *Y, ps, sc, ms, OUT_BOTH, out, scores_out);
+    } while (0);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_idx);
+    return rc;
+}
+
+int taxi2_closest(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
+                  int32_t primary, double scale, const int32_t* metrics, int nmetrics, int64_t* idx_out,
+                  double* d_out, double* extra_out, double* primary_out) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (Q->mode != R->mode) return fail(ctx, "query and reference sets differ in mode");
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if (!idx_out || !d_out) return fail(ctx, "idx_out and d_out are required");
+    MetricSpec pm;
+    if (check_metrics(ctx, &primary, 1, pm)) return -1;
+    MetricSpec em{};
+    if (extra_out && check_metrics(ctx, metrics, nmetrics, em)) return -1;
+    if (Q->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int64_t Rn = R->n;
+    if (q1 == q0) return 0;
+    if (Rn == 0) {
+        for (int64_t q = 0; q < q1 - q0; ++q) {
+            idx_out[q] = -1;
+            d_out[q] = NAN;
+        }
+        return 0;
+    }
+    // query chunks sized so the primary block stays <= 256 MiB of device memory
+    const int64_t qchunk = std::max<int64_t>(1, ((int64_t)256 << 20) / (8 * Rn));
+    std::vector<int64_t> all_idx;
+    for (int64_t qa = q0; qa < q1; qa += qchunk) {
+        const int64_t qb = std::min(q1, qa + qchunk);
+        const int64_t nq = qb - qa;
+        if (ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)nq * Rn * 8)) return -1;
+        if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)nq * 16)) return -1;
+        double* d_prim = (double*)ctx->d_out;
+        int64_t* d_idx = (int64_t*)ctx->d_aux;
+        double* d_best = (double*)(d_idx + nq);
+        PairSrc ps{PAIRS_RECT, qa * Rn, nq * Rn, 0, Rn, nullptr, nullptr};
+        int rc = Q->mode == TAXI2_MODE_ALIGN
+                     ? launch_align_pairs(ctx, *Q, *R, ps, sc, pm, OUT_AB, d_prim, nullptr, ctx->stream)
+                     : launch_prealigned(ctx, *Q, *R, ps, pm, d_prim, ctx->stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_row_argmin, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, ctx->stream, d_prim,
+                           nq, Rn, scale, d_idx, d_best);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipMemcpyAsync(idx_out + (qa - q0), d_idx, nq * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_out + (qa - q0), d_best, nq * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (primary_out)
+            HIP_TRY(ctx, hipMemcpyAsync(primary_out + (qa - q0) * Rn, d_prim, (size_t)nq * Rn * 8,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    if (extra_out) {
+        // extras only for each query's closest reference (versus_reference.py:124-129)
+        std::vector<int64_t> xs, ys, slot;
+        for (int64_t q = 0; q < q1 - q0; ++q) {
+            if (idx_out[q] >= 0) {
+                xs.push_back(q0 + q);
+                ys.push_back(idx_out[q]);
+                slot.push_back(q);
+            } else {
+                for (int m = 0; m < em.n; ++m) extra_out[q * em.n + m] = NAN;
+            }
+        }
+        if (!xs.empty()) {
+            const bool align = Q->mode == TAXI2_MODE_ALIGN;
+            const int per = align ? 2 * em.n : em.n;
+            std::vector<double> tmp(xs.size() * per);
+            int rc = taxi2_list_pairs(ctx, set_q, set_r, xs.data(), ys.data(), (int64_t)xs.size(), sc,
+                                      em.code, em.n, tmp.data(), nullptr);
+            if (rc) return rc;
+            for (size_t t = 0; t < xs.size(); ++t)
+                for (int m = 0; m < em.n; ++m) extra_out[slot[t] * em.n + m] = tmp[t * per + m];
+        }
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,228 @@
+"""GPU parity: the HIP engine (through the C ABI) against the C restatement.
+
+Bar (BASELINE.json north_star): alignment scores and p / p-gaps bit-exact; jc / k2p within
+1e-12 absolute; undefined (NaN/inf -> None) in exactly the same places.
+"""
+
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+from tests.seqgen import family_sequences, mutate, random_sequences
+
+pytestmark = pytest.mark.gpu
+
+METRICS = ("p", "p-gaps", "jc", "k2p")
+TOL_LOG = 1e-12  # jc / k2p (f64 log on GPU vs glibc)
+
+SCORE_SETS = {
+    "default": (1, -1, -8, -1, -1, -1),
+    "generic": (2, -3, -5, -2, -1, -1),
+    "linear": (1, -1, -2, -2, -1, -1),
+}
+
+
+def assert_metrics_equal(got: np.ndarray, exp: np.ndarray, metrics=METRICS):
+    assert got.shape == exp.shape
+    for mi, m in enumerate(metrics):
+        g = got[..., mi].ravel()
+        e = exp[..., mi].ravel()
+        gu, eu = ~np.isfinite(g), ~np.isfinite(e)
+        bad = np.nonzero(gu != eu)[0]
+        assert bad.size == 0, f"{m}: undefined mismatch at {bad[:10]} got={g[bad[:5]]} exp={e[bad[:5]]}"
+        gd, ed = g[~gu], e[~eu]
+        if m in ("p", "p-gaps"):
+            diff = np.nonzero(gd != ed)[0]
+            assert diff.size == 0, f"{m}: {diff.size} values differ, e.g. {gd[diff[:5]]} vs {ed[diff[:5]]}"
+        else:
+            err = np.max(np.abs(gd - ed)) if gd.size else 0.0
+            assert err <= TOL_LOG, f"{m}: max abs err {err}"
+        # sign of zero (jc/k2p print -0.0000 for p = 0)
+        assert np.array_equal(np.signbit(gd[gd == 0]), np.signbit(ed[ed == 0]))
+
+
+# ----------------------------------------------------------------------------- golden vectors
+def test_align_golden_vectors(engine, oracle_c):
+    """tests/test_align.py:49-163 vectors: GPU counters == restatement (whose alignment is one
+    of the accepted solutions for every vector)."""
+    from oracle import restatement as R
+
+    rows = json.loads((GOLDEN / "align_tests.json").read_text())
+    for r in rows:
+        sc = tuple(r["scores"].values())
+        s = engine.upload([r["x"], r["y"]], align=True)
+        got, score = engine.list_pairs(s, s, [0], [1], METRICS, sc, with_scores=True)
+        exp, escore = oracle_c.batch([r["x"], r["y"]], [0], [1], align=True, scores=sc, threads=1)
+        assert_metrics_equal(got, exp)
+        ax, ay, bs = R.align(r["x"], r["y"], R.Scores(*sc))
+        assert [ax, ay] in r["solutions"]
+        assert int(score[0]) == int(escore[0]) == int(bs), r
+        s.free()
+
+
+def test_prealigned_metrics_fixture(engine):
+    """tests/test_distances/metrics.tsv (26 rows x 4 metrics, tolerance 0.00051 as in
+    tests/test_distances.py:524) and the exact metric_tests (test_distances.py:515-521)."""
+    lines = (GOLDEN / "metrics.tsv").read_text().splitlines()
+    hdr = lines[0].split("\t")
+    xs, ys, exp = [], [], []
+    for ln in lines[1:]:
+        f = ln.split("\t")
+        xs.append(f[0])
+        ys.append(f[1])
+        exp.append([np.nan if v == "NA" else float(v) for v in f[2:]])
+    labels = tuple(hdr[2:])
+    s = engine.upload(xs + ys, align=False)
+    n = len(xs)
+    got = engine.list_pairs(s, s, np.arange(n), np.arange(n) + n, labels)
+    exp = np.asarray(exp)
+    for k in range(n):
+        for m in range(len(labels)):
+            g, e = got[k, m], exp[k, m]
+            if np.isnan(e):
+                assert not np.isfinite(g), (xs[k], ys[k], labels[m], g)
+            else:
+                assert abs(g - e) <= 0.00051, (xs[k], ys[k], labels[m], g, e)
+    s.free()
+    for r in json.loads((GOLDEN / "metric_tests.json").read_text()):
+        label = {"Uncorrected": "p", "UncorrectedWithGaps": "p-gaps"}[r["metric"]]
+        s = engine.upload([r["x"], r["y"]], align=False)
+        g = engine.list_pairs(s, s, [0], [1], [label])[0, 0]
+        if r["d"] is None:
+            assert not np.isfinite(g)
+        else:
+            assert g == r["d"]
+        s.free()
+
+
+# ----------------------------------------------------------------------------- aligned, random
+BUCKETS = [  # (lo, hi) lengths chosen to exercise every (K, W) kernel variant
+    (1, 40), (60, 250), (300, 380), (420, 512), (600, 760), (900, 1024), (1100, 1500), (1700, 2048),
+    (2200, 2600),
+]
+
+
+@pytest.mark.parametrize("bucket", BUCKETS)
+@pytest.mark.parametrize("scores", list(SCORE_SETS))
+def test_align_all_pairs_random(engine, oracle_c, bucket, scores):
+    lo, hi = bucket
+    if lo >= 2200 and scores != "default":
+        pytest.skip("long buckets: default scores only (oracle time)")
+    n = 10 if hi > 1100 else 16
+    seed = hash((lo, hi, scores)) & 0xFFFF
+    base = random_sequences(n // 2, lo, hi, seed, "ACGT", n_rate=0.02)
+    seqs = base + mutate(base, seed + 1, rate=0.15)
+    seqs = [s if s else "A" for s in seqs]
+    sc = SCORE_SETS[scores]
+    st = engine.upload(seqs, align=True)
+    total = n * (n - 1) // 2
+    got, gsc = engine.all_pairs(st, 0, total, METRICS, sc, with_scores=True)
+    from taxi2_amd._native import tri_pairs
+
+    a, b = tri_pairs(n)
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
+    assert np.array_equal(gsc, esc)
+    assert_metrics_equal(got, exp)
+    st.free()
+
+
+def test_align_family_1000bp(engine, oracle_c):
+    """The bench workload shape (config 3 generator, 1 000 bp) on a small sample."""
+    seqs = family_sequences(24, 1000, 0x7A12, ancestors=4)
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    got, gsc = engine.all_pairs(st, 0, n * (n - 1) // 2, METRICS, None, with_scores=True)
+    from taxi2_amd._native import tri_pairs
+
+    a, b = tri_pairs(n)
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=SCORE_SETS["default"])
+    assert np.array_equal(gsc, esc)
+    assert_metrics_equal(got, exp)
+    # the (x, y) / (y, x) asymmetry the survey found (~1 % of aligned pairs) must be reproduced
+    st.free()
+
+
+def test_align_edge_cases(engine, oracle_c):
+    seqs = ["", "A", "N", "NNNN", "ACGT", "ACGT", "TTTT", "ACGTNNACGT", "GATTACA" * 3, "-" * 0, "C"]
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    from taxi2_amd._native import tri_pairs
+
+    a, b = tri_pairs(n)
+    for sc in SCORE_SETS.values():
+        got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
+        exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc, threads=1)
+        assert_metrics_equal(got, exp)
+        nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
+        assert np.array_equal(gsc[nonempty], esc[nonempty])
+    st.free()
+
+
+# ----------------------------------------------------------------------------- pre-aligned
+def test_prealigned_all_pairs_random(engine, oracle_c):
+    seqs = random_sequences(150, 0, 300, 5, "ACGTacgtN--?RY")
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    from taxi2_amd._native import tri_pairs
+
+    a, b = tri_pairs(n)
+    got = engine.all_pairs(st, 0, len(a), METRICS)
+    exp, _ = oracle_c.batch(seqs, a, b, align=False, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp[:, 0, :])
+    assert_metrics_equal(got, exp[:, 1, :])
+    st.free()
+
+
+def test_prealigned_samples_ca200(engine, oracle_c):
+    """samples/Taxi2test1_ca200.tab (unaligned 416-618 bp, acgt + n) pre-aligned, config-2 shape."""
+    from taxi2_amd.sequences import Sequences, SequenceHandler
+
+    seqs = [s.seq for s in Sequences.fromPath(GOLDEN / "samples" / "Taxi2test1_ca200.tab",
+                                              SequenceHandler.Tabfile, idHeader="seqid", seqHeader="sequence")]
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    from taxi2_amd._native import tri_pairs
+
+    a, b = tri_pairs(n)
+    got = engine.all_pairs(st, 0, len(a), ("p", "jc", "k2p"))
+    exp, _ = oracle_c.batch(seqs, a, b, align=False, scores=SCORE_SETS["default"], metrics=("p", "jc", "k2p"))
+    assert_metrics_equal(got, exp[:, 0, :], ("p", "jc", "k2p"))
+    st.free()
+
+
+# ----------------------------------------------------------------------------- rect / closest
+@pytest.mark.parametrize("align", [True, False])
+def test_rect_and_closest(engine, oracle_c, align):
+    q = random_sequences(20, 50, 200, 11, "ACGTN")
+    r = mutate(q[:7], 12, rate=0.2) + random_sequences(9, 50, 200, 13, "ACGT")
+    if not align:
+        q = [s.lower() for s in q]
+    qs = engine.upload(q, align=align)
+    rs = engine.upload(r, align=align)
+    sc = SCORE_SETS["default"]
+    got = engine.rect_pairs(qs, rs, 0, len(q), METRICS, sc)
+    allseq = q + r
+    pa = np.repeat(np.arange(len(q)), len(r))
+    pb = np.tile(np.arange(len(r)), len(q)) + len(q)
+    exp, _ = oracle_c.batch(allseq, pa, pb, align=align, scores=sc)
+    assert_metrics_equal(got, exp[:, 0, :])
+    # closest: first minimum of the primary metric over defined values (versus_reference.py:184-188)
+    idx, d, ex, mat = engine.closest(qs, rs, 0, len(q), "p", ("p-gaps", "jc", "k2p"), sc, want_matrix=True)
+    prim = exp[:, 0, 0].reshape(len(q), len(r))
+    assert_metrics_equal(mat[..., None], prim[..., None], ("p",))
+    for k in range(len(q)):
+        row = prim[k]
+        ok = np.isfinite(row)
+        if not ok.any():
+            assert idx[k] == -1
+            continue
+        j = int(np.nonzero(ok & (row == row[ok].min()))[0][0])
+        assert idx[k] == j and d[k] == row[j]
+        e = exp[k * len(r) + j, 0, 1:]
+        assert_metrics_equal(ex[k][None, :], e[None, :], ("p-gaps", "jc", "k2p"))
+    qs.free()
+    rs.free()
