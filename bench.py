@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Headline benchmark: aligned pairs/sec for versusAll at 1 000 bp (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): 50 000 synthetic 1 000 bp
+sequences (seed 0x7A12, 64 ancestors, substitutions U(0, 0.20) ts:tv 2:1, 1 % indel pairs),
+versusAll pair space N(N-1)/2 = 1.25e9 unordered pairs, every pair globally aligned (Gotoh,
+default TaxI2 scores) and measured with p, p-gaps, jc, k2p for BOTH ordered pairs -- exactly
+the work VersusAll.start() does per pair (versus_all.py:746-752).
+
+A step = one block of `--batch` consecutive unordered pairs per GPU (shards of the pair space;
+weak scaling: per-GPU work is fixed as N grows), results written to device memory, then (N > 1)
+gathered to every rank with an RCCL all-gather over xGMI.  Inputs are resident in HBM before
+the timed region.  value = pairs processed by all ranks / max-over-ranks wall time.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "aligned pairs/sec (versusAll, 1 000 bp) at 1/2/4/8 MI355X; % HBM roofline"
+METRICS = ("p", "p-gaps", "jc", "k2p")
+N_SEQS = 50_000
+SEQ_LEN = 1000
+SEED = 0x7A12
+HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
+INT_VALU_PEAK = 256 * 128 * 2.4e9   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+OPS_PER_CELL = 62                   # VALU instructions per DP cell, counted in the ISA
+
+
+def b_pair(L: int, M: int) -> int:
+    """SURVEY.md §8(d) canonical algorithmic bytes per unordered pair: 2 * ceil(L/4) + 8 * M."""
+    return 2 * math.ceil(L / 4) + 8 * M
+
+
+def parse() -> argparse.Namespace:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1 << 19, help="unordered pairs per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="pairs timed on the host oracle")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores (max 16)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def main() -> None:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from taxi2_amd._native import Engine
+    from taxi2_amd.synth import family_packed
+
+    # ---- inputs resident in HBM before timing (every rank packs the same seeded set)
+    buf, offs = family_packed(N_SEQS, SEQ_LEN, SEED)
+    eng = Engine(local)
+    seqset = eng.upload_packed(buf, offs, align=True)
+    total_pairs = N_SEQS * (N_SEQS - 1) // 2
+    B = int(args.batch)
+    M = len(METRICS)
+    out = torch.empty((B, 2, M), dtype=torch.float64, device="cuda")
+    scores = torch.empty((B,), dtype=torch.int32, device="cuda")
+    gathered = torch.empty((world * B, 2, M), dtype=torch.float64, device="cuda") if world > 1 else None
+    stream = torch.cuda.Stream()  # a real stream handle: the kernel and its HIP events share it
+    torch.cuda.set_stream(stream)
+
+    def block(step: int) -> int:
+        return ((step * world + rank) * B) % (total_pairs - B)
+
+    ev = []
+
+    def run_step(step: int, record: bool) -> None:
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        eng.all_pairs_dev(seqset, block(step), B, METRICS, out.data_ptr(), None, scores.data_ptr(),
+                          stream.cuda_stream)
+        if record:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for w in range(args.warmup):
+        run_step(w, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        run_step(args.warmup + s, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
+    pairs = args.steps * B * world
+    value = pairs / elapsed
+    bp = b_pair(SEQ_LEN, M)
+    achieved_gbs = B * bp / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tj = Path(args.traffic_json)
+    if tj.exists():
+        try:
+            rec = json.loads(tj.read_text())
+            if rec.get("batch") == B and rec.get("workload") == "config3":
+                traffic = rec.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cells = float(SEQ_LEN) * SEQ_LEN
+    gcups = B * cells / (kern_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, buf, offs, eng, seqset)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {
+                "workload": "config3: versusAll 50 000 x 1 000 bp synthetic, Gotoh align (default "
+                            "TaxI2 scores) + p/p-gaps/jc/k2p for both ordered pairs",
+                "n_seqs": N_SEQS,
+                "seq_len": SEQ_LEN,
+                "pairs_per_step_per_gpu": B,
+                "pair_space": total_pairs,
+                "parallelism": f"pair-space shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_pair": bp,
+                "kernel_ms": kern_ms,
+            },
+            "compute_roofline": {
+                "bound": "valu-int32",
+                "gcups": gcups,
+                "ops_per_cell": OPS_PER_CELL,
+                "achieved_tops": gcups * 1e9 * OPS_PER_CELL / 1e12,
+                "peak_tops": INT_VALU_PEAK / 1e12,
+                "frac": gcups * 1e9 * OPS_PER_CELL / INT_VALU_PEAK,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, buf, offs, eng, seqset):
+    """Oracle (C restatement, kind "port") on the first `--cpu-sample` pairs of the bench's pair
+    space, on the host cores; the same pairs' GPU results are checked against it."""
+    from oracle import oracle_c
+    from taxi2_amd._native import tri_pairs
+
+    S = int(args.cpu_sample)
+    threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
+    a, b = tri_pairs(N_SEQS, 0, S)
+    t0 = time.perf_counter()
+    exp, _ = oracle_c.batch((buf, offs), a, b, align=True, scores=(1, -1, -8, -1, -1, -1),
+                            metrics=METRICS, threads=threads)
+    dt = time.perf_counter() - t0
+    got = eng.all_pairs(seqset, 0, S, METRICS)
+    fin = np.isfinite(exp)
+    same = bool(np.array_equal(np.isfinite(got), fin)
+                and np.all(np.abs(got[fin] - exp[fin]) <= 1e-12))
+    return {
+        "value": S / dt,
+        "unit": "pairs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {S} pairs of the config3 pair space (row 0), C restatement "
+                  f"(oracle/taxi2_oracle.c, gcc -O2) on {threads} host threads; GPU==CPU on the "
+                  f"sample: {same}",
+    }
+
+
+if __name__ == "__main__":
+    main()
