@@ -129,6 +129,18 @@ int taxi2_closest(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1,
                   int nmetrics, int64_t* idx_out, double* d_out, double* extra_out,
                   double* primary_out);
 
+/* ---- aligned strings (align.py:151-157 Biopython.align; pairs.py:51-97 Formatted writer) -- *
+ * First Biopython global alignment of (xs[k] of set_x = target, ys[k] of set_y = query), as
+ * gapped strings.  Both sets must be ALIGN mode.  Outputs are right-aligned in fixed slots:
+ *   out_x / out_y [count][2][cap] bytes, out_len[count][2]; slot [k][0] = alignment of
+ *   (x, y); slot [k][1] (only when both != 0) = the alignment Biopython returns for (y, x),
+ *   written in (x, y) column order.  The alignment of slot o occupies bytes
+ *   [len(x)+len(y)-out_len[k][o], len(x)+len(y)) of its slot; cap >= len(x)+len(y) for every
+ *   pair. */
+int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
+                        int64_t count, const taxi2_scores* sc, int both, int32_t cap, uint8_t* out_x,
+                        uint8_t* out_y, int32_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

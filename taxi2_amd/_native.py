@@ -37,6 +37,7 @@ EXPORTS = (
     "taxi2_rect_pairs",
     "taxi2_list_pairs",
     "taxi2_closest",
+    "taxi2_align_strings",
 )
 
 MODE_PREALIGNED = 0
@@ -81,6 +82,7 @@ _SIGNATURES = {
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
+    "taxi2_align_strings": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _INT, _I32, _P, _P, _P]),
 }
 
 _lib = None
@@ -172,12 +174,20 @@ def encode_sequences(seqs: Seq[str], *, strict: bool) -> tuple[np.ndarray, np.nd
 class SeqSet:
     """A sequence set resident in HBM (freed with the engine or by ``free``)."""
 
-    def __init__(self, engine: "Engine", set_id: int, n: int, max_len: int, mode: int):
+    def __init__(self, engine: "Engine", set_id: int, n: int, max_len: int, mode: int,
+                 lengths: np.ndarray | None = None):
         self.engine = engine
         self.id = set_id
         self.n = n
         self.max_len = max_len
         self.mode = mode
+        self._lengths = lengths
+
+    def has_lengths(self) -> bool:
+        return self._lengths is not None
+
+    def lengths(self) -> np.ndarray:
+        return self._lengths
 
     @property
     def aligned(self) -> bool:
@@ -256,7 +266,7 @@ class Engine:
                 self._lib.taxi2_set_info(self._ctx, sid.value, ctypes.byref(nn), ctypes.byref(ml), ctypes.byref(md)),
                 "taxi2_set_info",
             )
-        return SeqSet(self, sid.value, nn.value, ml.value, md.value)
+        return SeqSet(self, sid.value, nn.value, ml.value, md.value, np.diff(offs))
 
     # ------------------------------------------------------------------ pair blocks
     def all_pairs(self, s: SeqSet, k0: int, count: int, metrics, scores=None, *, with_scores=False):
@@ -354,6 +364,41 @@ class Engine:
                 "taxi2_closest",
             )
         return idx, d, ex, mat
+
+
+    def align_strings(self, x: SeqSet, y: SeqSet, xs, ys, scores=None, *, both: bool = False):
+        """Gapped alignment strings: list of (ax, ay) per pair, plus the (y, x) alignment written
+        in (x, y) column order when ``both`` (list of pairs of tuples)."""
+        xs = np.ascontiguousarray(xs, dtype=np.int64)
+        ys = np.ascontiguousarray(ys, dtype=np.int64)
+        count = len(xs)
+        if count == 0:
+            return []
+        cap = int(x.max_len + y.max_len) or 1
+        ox = np.zeros((count, 2, cap), dtype=np.uint8)
+        oy = np.zeros((count, 2, cap), dtype=np.uint8)
+        ln = np.zeros((count, 2), dtype=np.int32)
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_align_strings(
+                    self._ctx, x.id, y.id, xs.ctypes.data, ys.ctypes.data, count, ctypes.byref(cs),
+                    1 if both else 0, cap, ox.ctypes.data, oy.ctypes.data, ln.ctypes.data,
+                ),
+                "taxi2_align_strings",
+            )
+        lens_x = x.lengths()[xs] if x.has_lengths() else None
+        lens_y = y.lengths()[ys] if y.has_lengths() else None
+        out = []
+        for k in range(count):
+            end = int(lens_x[k] + lens_y[k])
+            res = []
+            for o in range(2 if both else 1):
+                L = int(ln[k, o])
+                res.append((ox[k, o, end - L:end].tobytes().decode("latin-1"),
+                            oy[k, o, end - L:end].tobytes().decode("latin-1")))
+            out.append(tuple(res) if both else res[0])
+        return out
 
 
 def tri_index(a: np.ndarray, b: np.ndarray, n: int) -> np.ndarray:

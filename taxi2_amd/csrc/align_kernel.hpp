@@ -308,8 +308,8 @@ __device__ __forceinline__ void dp_step(int s, int lane, int nA, typename StateO
 // Dynamic LDS: [uint32 xinfo[xcap]] [RingEntry ring[W-1][RING]]
 // xinfo[i-1] = byte | lut shift << 8 (base 0..3, 24 = not ACGT) |
 //              (row i contributes Iy gaps: i-1 >= fx && i <= lx) << 13 | (byte is ACGT) << 14
-template <int K, int W, bool LINEAR, bool DEF>
-__global__ void __launch_bounds__(64 * W, 2)
+template <int K, int W, bool LINEAR, bool DEF, int OCC>
+__global__ void __launch_bounds__(64 * W, OCC)
 k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xcap, int out_mode,
         double* __restrict__ out, int32_t* __restrict__ sout) {
     using S = typename StateOf<LINEAR>::T;

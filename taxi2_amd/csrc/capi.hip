@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -16,6 +17,7 @@
 #include "common.hpp"
 #include "pack_kernels.hpp"
 #include "prealigned_kernel.hpp"
+#include "trace_kernel.hpp"
 
 using namespace taxi2;
 
@@ -105,50 +107,77 @@ bool is_linear(const KScores& k) { return k.io == k.ie && k.eo == k.ee; }
 
 // ---------------------------------------------------------------- align variant table
 struct Variant {
-    int K, W;
+    int K, W, occ;
     bool linear, def;
     const void* fn;
     void (*launch)(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec,
                    int, int, double*, int32_t*);
 };
 
-template <int K, int W, bool LIN, bool DEF>
+template <int K, int W, bool LIN, bool DEF, int OCC>
 void launch_align(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView y, PairSrc ps,
                   KScores sc, MetricSpec ms, int xcap, int om, double* out, int32_t* so) {
-    hipLaunchKernelGGL((k_align<K, W, LIN, DEF>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so);
+    hipLaunchKernelGGL((k_align<K, W, LIN, DEF, OCC>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so);
 }
 
-#define T2_VARIANT(K, W, LIN, DEF) \
-    Variant{K, W, LIN, DEF, (const void*)&k_align<K, W, LIN, DEF>, &launch_align<K, W, LIN, DEF>}
+#define T2_VARIANT(K, W, LIN, DEF, OCC)                                                   \
+    Variant{K, W, OCC, LIN, DEF, (const void*)&k_align<K, W, LIN, DEF, OCC>,             \
+            &launch_align<K, W, LIN, DEF, OCC>}
 
 // Ordered by column capacity (64 * K * W); the first one that fits the longest sequence wins.
-// DEF = the default TaxI2 scores (align.py:20-27) as compile-time constants.
+// DEF = the default TaxI2 scores (align.py:20-27) as compile-time constants; OCC = waves per
+// SIMD the register allocation targets.
 const Variant kGotohDef[] = {
-    T2_VARIANT(4, 1, false, true), T2_VARIANT(6, 1, false, true), T2_VARIANT(8, 1, false, true),
-    T2_VARIANT(6, 2, false, true), T2_VARIANT(8, 2, false, true), T2_VARIANT(6, 4, false, true),
-    T2_VARIANT(8, 4, false, true), T2_VARIANT(8, 8, false, true),
+    T2_VARIANT(4, 1, false, true, 2), T2_VARIANT(6, 1, false, true, 2), T2_VARIANT(8, 1, false, true, 2),
+    T2_VARIANT(6, 2, false, true, 2), T2_VARIANT(8, 2, false, true, 2), T2_VARIANT(6, 4, false, true, 2),
+    T2_VARIANT(8, 4, false, true, 2), T2_VARIANT(8, 8, false, true, 2),
 };
 const Variant kGotoh[] = {
-    T2_VARIANT(4, 1, false, false), T2_VARIANT(6, 1, false, false), T2_VARIANT(8, 1, false, false),
-    T2_VARIANT(6, 2, false, false), T2_VARIANT(8, 2, false, false), T2_VARIANT(6, 4, false, false),
-    T2_VARIANT(8, 4, false, false), T2_VARIANT(8, 8, false, false),
+    T2_VARIANT(4, 1, false, false, 2), T2_VARIANT(6, 1, false, false, 2), T2_VARIANT(8, 1, false, false, 2),
+    T2_VARIANT(6, 2, false, false, 2), T2_VARIANT(8, 2, false, false, 2), T2_VARIANT(6, 4, false, false, 2),
+    T2_VARIANT(8, 4, false, false, 2), T2_VARIANT(8, 8, false, false, 2),
 };
 const Variant kLinear[] = {
-    T2_VARIANT(4, 1, true, false), T2_VARIANT(8, 1, true, false), T2_VARIANT(8, 2, true, false),
-    T2_VARIANT(8, 4, true, false), T2_VARIANT(8, 8, true, false),
+    T2_VARIANT(4, 1, true, false, 2), T2_VARIANT(8, 1, true, false, 2), T2_VARIANT(8, 2, true, false, 2),
+    T2_VARIANT(8, 4, true, false, 2), T2_VARIANT(8, 8, true, false, 2),
+};
+// Experimental shapes for tuning (selected only through TAXI2_VARIANT="K,W,OCC").
+const Variant kSweep[] = {
+    T2_VARIANT(8, 2, false, true, 3), T2_VARIANT(6, 3, false, true, 2), T2_VARIANT(6, 3, false, true, 3),
+    T2_VARIANT(4, 4, false, true, 3), T2_VARIANT(4, 4, false, true, 4), T2_VARIANT(5, 4, false, true, 3),
+    T2_VARIANT(4, 4, false, true, 2),
 };
 
 bool is_default(const KScores& k) {
     return k.ma == 1 && k.mi == -1 && k.io == -8 && k.ie == -1 && k.eo == -1 && k.ee == -1;
 }
 
+template <size_t N>
+const Variant* find_variant(const Variant (&tab)[N], int K, int W, int occ, bool lin, bool def) {
+    for (size_t i = 0; i < N; ++i)
+        if (tab[i].K == K && tab[i].W == W && tab[i].occ == occ && tab[i].linear == lin && tab[i].def == def)
+            return &tab[i];
+    return nullptr;
+}
+
 const Variant* pick_variant(const KScores& k, int max_len) {
+    const bool lin = is_linear(k), def = !lin && is_default(k);
+    if (const char* force = getenv("TAXI2_VARIANT")) {  // tuning hook: "K,W,OCC"
+        int K = 0, W = 0, occ = 0;
+        if (sscanf(force, "%d,%d,%d", &K, &W, &occ) == 3 && 64 * K * W >= max_len) {
+            const Variant* v = find_variant(kSweep, K, W, occ, lin, def);
+            if (!v) v = find_variant(kGotohDef, K, W, occ, lin, def);
+            if (!v) v = find_variant(kGotoh, K, W, occ, lin, def);
+            if (!v) v = find_variant(kLinear, K, W, occ, lin, def);
+            if (v) return v;
+        }
+    }
     const Variant* tab;
     int n;
-    if (is_linear(k)) {
+    if (lin) {
         tab = kLinear;
         n = (int)(sizeof kLinear / sizeof kLinear[0]);
-    } else if (is_default(k)) {
+    } else if (def) {
         tab = kGotohDef;
         n = (int)(sizeof kGotohDef / sizeof kGotohDef[0]);
     } else {
@@ -526,6 +555,111 @@ int taxi2_closest(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, 
         }
     }
     return 0;
+}
+
+int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
+                        int64_t count, const taxi2_scores* sc, int both, int32_t cap, uint8_t* out_x,
+                        uint8_t* out_y, int32_t* out_len) {
+    if (!ctx) return -1;
+    DevSet* X = get_set(ctx, set_x);
+    DevSet* Y = get_set(ctx, set_y);
+    if (!X || !Y) return fail(ctx, "unknown set");
+    if (X->mode != TAXI2_MODE_ALIGN || Y->mode != TAXI2_MODE_ALIGN) return fail(ctx, "align_strings needs ALIGN sets");
+    if (!sc) return fail(ctx, "scores required");
+    if (count <= 0) return 0;
+    const int max_len = std::max(X->max_len, Y->max_len);
+    if (max_len > 4095) return fail(ctx, "sequence length %d exceeds 4095", max_len);
+    if (cap < X->max_len + Y->max_len) return fail(ctx, "cap %d < longest x + longest y", cap);
+    for (int64_t k = 0; k < count; ++k)
+        if (xs[k] < 0 || xs[k] >= X->n || ys[k] < 0 || ys[k] >= Y->n)
+            return fail(ctx, "pair %lld index out of bounds", (long long)k);
+    const KScores k = kscores(sc);
+    const bool lin = is_linear(k);
+    int K = 8, W = 1;
+    if (max_len <= 256) K = 4;
+    else if (max_len <= 512) W = 1;
+    else if (max_len <= 1024) W = 2;
+    else if (max_len <= 2048) W = 4;
+    else W = 8;
+    const int xcap = std::max(max_len, 1);
+    const size_t lds = ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(W - 1) * RING * sizeof(RingEntry);
+    const int64_t stride = (int64_t)(xcap + 63) * 64 * W * K;  // u16 per pair
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 30) / (stride * 2)));
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint16_t* d_trace = nullptr;
+    int4* d_ends = nullptr;
+    int64_t* d_idx = nullptr;
+    uint8_t* d_out = nullptr;
+    int32_t* d_len = nullptr;
+    int rc = 0;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(ctx->stream);
+        if (d_trace) (void)hipFree(d_trace);
+        if (d_ends) (void)hipFree(d_ends);
+        if (d_idx) (void)hipFree(d_idx);
+        if (d_out) (void)hipFree(d_out);
+        if (d_len) (void)hipFree(d_len);
+    };
+#define T2_TRY(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            rc = fail(ctx, "%s failed: %s", #expr, hipGetErrorString(e_));                    \
+            cleanup();                                                                        \
+            return rc;                                                                        \
+        }                                                                                     \
+    } while (0)
+    T2_TRY(hipMalloc(&d_trace, (size_t)chunk * stride * 2));
+    T2_TRY(hipMalloc(&d_ends, (size_t)chunk * sizeof(int4)));
+    T2_TRY(hipMalloc(&d_idx, (size_t)chunk * 2 * sizeof(int64_t)));
+    T2_TRY(hipMalloc(&d_out, (size_t)chunk * 2 * cap * 2));
+    T2_TRY(hipMalloc(&d_len, (size_t)chunk * 2 * sizeof(int32_t)));
+    for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+        const int64_t n = std::min(chunk, count - c0);
+        T2_TRY(hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        T2_TRY(hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        const dim3 grid((unsigned)n), block(64 * W);
+#define T2_FILL(KK, WW, LIN)                                                                    \
+    hipLaunchKernelGGL((k_trace_fill<KK, WW, LIN>), grid, block, lds, ctx->stream, view(*X), view(*Y), \
+                       d_idx, d_idx + chunk, n, k, xcap, d_trace, d_ends)
+        if (K == 4) {
+            if (lin) T2_FILL(4, 1, true); else T2_FILL(4, 1, false);
+        } else if (W == 1) {
+            if (lin) T2_FILL(8, 1, true); else T2_FILL(8, 1, false);
+        } else if (W == 2) {
+            if (lin) T2_FILL(8, 2, true); else T2_FILL(8, 2, false);
+        } else if (W == 4) {
+            if (lin) T2_FILL(8, 4, true); else T2_FILL(8, 4, false);
+        } else {
+            if (lds > 64 * 1024) {
+                T2_TRY(hipFuncSetAttribute(lin ? (const void*)&k_trace_fill<8, 8, true>
+                                               : (const void*)&k_trace_fill<8, 8, false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            }
+            if (lin) T2_FILL(8, 8, true); else T2_FILL(8, 8, false);
+        }
+#undef T2_FILL
+        T2_TRY(hipGetLastError());
+        const int64_t threads = n * (both ? 2 : 1);
+        const dim3 g2((unsigned)((threads + 255) / 256));
+        if (lin)
+            hipLaunchKernelGGL(k_traceback<true>, g2, dim3(256), 0, ctx->stream, view(*X), view(*Y), d_idx,
+                               d_idx + chunk, n, K, W, xcap, d_trace, d_ends, cap, d_out, d_out + chunk * 2 * cap,
+                               d_len, both);
+        else
+            hipLaunchKernelGGL(k_traceback<false>, g2, dim3(256), 0, ctx->stream, view(*X), view(*Y), d_idx,
+                               d_idx + chunk, n, K, W, xcap, d_trace, d_ends, cap, d_out, d_out + chunk * 2 * cap,
+                               d_len, both);
+        T2_TRY(hipGetLastError());
+        T2_TRY(hipMemcpyAsync(out_x + c0 * 2 * cap, d_out, (size_t)n * 2 * cap, hipMemcpyDeviceToHost, ctx->stream));
+        T2_TRY(hipMemcpyAsync(out_y + c0 * 2 * cap, d_out + chunk * 2 * cap, (size_t)n * 2 * cap,
+                              hipMemcpyDeviceToHost, ctx->stream));
+        T2_TRY(hipMemcpyAsync(out_len + c0 * 2, d_len, (size_t)n * 2 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        T2_TRY(hipStreamSynchronize(ctx->stream));
+    }
+#undef T2_TRY
+    cleanup();
+    return rc;
 }
 
 }  // extern "C"

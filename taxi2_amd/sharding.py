@@ -1,0 +1,81 @@
+"""Pair-space sharding across GPUs (one process per GPU, torch.distributed).
+
+versusAll's unordered pairs are the row-major upper triangle of the N x N product; row a holds
+N-1-a pairs.  Ranks take contiguous row blocks balanced by pair count; the
+pair blocks are independent, so the only exchange is the final gather of each rank's results
+(RCCL all-gather over xGMI on GPUs, gloo on CPU for tests).  RCCL has no all-gather-v, so
+blocks are padded to the largest one.
+"""
+
+from __future__ import annotations
+
+from typing import Callable
+
+import numpy as np
+
+
+def tri_row_start(a: int, n: int) -> int:
+    return a * (2 * n - a - 1) // 2
+
+
+def shard_rows(n: int, world: int) -> list[tuple[int, int]]:
+    """Row ranges [r0, r1) per rank with nearly equal pair counts."""
+    total = n * (n - 1) // 2
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        lo, hi = bounds[-1], n
+        while lo < hi:  # smallest row whose start >= target
+            mid = (lo + hi) // 2
+            if tri_row_start(mid, n) >= target:
+                hi = mid
+            else:
+                lo = mid + 1
+        bounds.append(lo)
+    bounds.append(n)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def shard_pairs(n: int, world: int) -> list[tuple[int, int]]:
+    """(k0, count) of each rank's contiguous block of the linear pair index."""
+    out = []
+    for r0, r1 in shard_rows(n, world):
+        k0 = tri_row_start(r0, n)
+        out.append((k0, tri_row_start(r1, n) - k0))
+    return out
+
+
+def gather_blocks(local: np.ndarray, counts: list[int], group=None, device=None) -> np.ndarray:
+    """All-gather variable-length leading-dim blocks; returns the concatenation in rank order.
+
+    ``local`` has shape (counts[rank], ...).  Uses torch.distributed (the default group's
+    backend: nccl = RCCL on ROCm GPUs, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    pad = max(counts) if counts else 0
+    tail = local.shape[1:]
+    buf = np.zeros((pad,) + tail, dtype=local.dtype)
+    buf[: local.shape[0]] = local
+    t = torch.from_numpy(buf)
+    if device is not None:
+        t = t.to(device)
+    outs = torch.empty((world * pad,) + tuple(tail), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(outs, t, group=group)
+    outs = outs.cpu().numpy().reshape((world, pad) + tail)
+    return np.concatenate([outs[r, : counts[r]] for r in range(world)], axis=0)
+
+
+def distributed_all_pairs(n: int, compute: Callable[[int, int], np.ndarray], group=None, device=None) -> np.ndarray:
+    """Every rank computes its pair block with ``compute(k0, count)`` and receives all blocks.
+
+    Returns the full (n(n-1)/2, ...) result in pair-index order on every rank."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    blocks = shard_pairs(n, world)
+    k0, cnt = blocks[rank]
+    local = compute(k0, cnt)
+    return gather_blocks(local, [c for _, c in blocks], group=group, device=device)

@@ -1,0 +1,230 @@
+"""VersusReference task (``src/itaxotools/taxi2/tasks/versus_reference.py:33-247``), GPU-backed.
+
+``start`` computes, for the Q x R product (query outer, reference inner):
+  * the primary metric for every pair (default p, :83-86), x100 when percentage_multiply;
+  * per group of consecutive queries with equal id (``groupby(x.id)``, :184-188) the first
+    minimum over defined values (``min`` raises ValueError when a group has none);
+  * the extra metrics (default p-gaps / jc / k2p minus the primary, :87-93) for that closest
+    pair only, on the same alignment (:124-129);
+and writes ``distances/<metric>.linear.tsv``, ``distances/<metric>.matricial.tsv``,
+``closest.tsv`` and (``params.pairs.write``) ``aligned_pairs.txt``.
+Argmin runs on the GPU (``taxi2_closest``), so the Q x R block never round-trips through
+Python unless a writer needs it.
+"""
+
+from __future__ import annotations
+
+from pathlib import Path
+from time import perf_counter
+from typing import Callable
+
+import numpy as np
+
+from ..align import PairwiseAligner, Scores
+from ..distances import Distance, DistanceHandler, DistanceMetric
+from ..pairs import SequencePair, SequencePairHandler
+from ..types import AttrDict
+from .common import Results, console_report, create_parents, format_values, report
+
+ENGINE_LABELS = ("p", "p-gaps", "jc", "k2p")
+
+
+class VersusReference:
+    def __init__(self):
+        self.work_dir: Path = None
+        self.paths = AttrDict()
+        self.progress_handler: Callable = console_report
+        self.progress_interval: float = 0.015
+        self.engine = None
+
+        self.input = AttrDict()
+        self.input.data = None
+        self.input.reference = None
+
+        self.params = AttrDict()
+        self.params.pairs = AttrDict()
+        self.params.pairs.align = True
+        self.params.pairs.write = True
+        self.params.pairs.scores = None
+
+        self.params.distances = AttrDict()
+        self.params.distances.metric = None
+        self.params.distances.extra_metrics = None
+        self.params.distances.write_linear = True
+        self.params.distances.write_matricial = True
+
+        self.params.format = AttrDict()
+        self.params.format.float = "{:.4f}"
+        self.params.format.percentage = "{:.2f}"
+        self.params.format.missing = "NA"
+        self.params.format.percentage_multiply = False
+
+        self.closest: list | None = None  # [(query index range, ref index, d, extras)] after start()
+
+    def generate_paths(self):
+        assert self.work_dir
+        w = Path(self.work_dir)
+        create_parents(w)
+        metric = str(self.params.distances.metric)
+        self.paths.closest = w / "closest.tsv"
+        self.paths.aligned_pairs = w / "aligned_pairs.txt"
+        self.paths.distances_linear = w / "distances" / f"{metric}.linear.tsv"
+        self.paths.distances_matricial = w / "distances" / f"{metric}.matricial.tsv"
+
+    def check_metrics(self):
+        self.params.distances.metric = self.params.distances.metric or DistanceMetric.Uncorrected()
+        self.params.distances.extra_metrics = self.params.distances.extra_metrics or [
+            DistanceMetric.UncorrectedWithGaps(),
+            DistanceMetric.JukesCantor(),
+            DistanceMetric.Kimura2P(),
+        ]
+        if self.params.distances.metric in self.params.distances.extra_metrics:
+            self.params.distances.extra_metrics.remove(self.params.distances.metric)
+        for m in [self.params.distances.metric, *self.params.distances.extra_metrics]:
+            if str(m) not in ENGINE_LABELS:
+                raise NotImplementedError(f"metric {m} is not computed by the MI355X engine (DESIGN.md)")
+
+    def _engine(self):
+        if self.engine is None:
+            from .._native import Engine
+
+            self.engine = Engine.default()
+        return self.engine
+
+    def start(self) -> Results:
+        ts = perf_counter()
+        self.check_metrics()
+        self.generate_paths()
+        align = bool(self.params.pairs.align)
+        data = list(self.input.data)
+        refs = list(self.input.reference)
+        if align:
+            data = [s.normalize() for s in data]
+            refs = [s.normalize() for s in refs]
+        Q, R = len(data), len(refs)
+        primary = self.params.distances.metric
+        extras = list(self.params.distances.extra_metrics)
+        scores = Scores(**(self.params.pairs.scores or {})).as_tuple()
+        pct = bool(self.params.format.percentage_multiply)
+        want_matrix = bool(self.params.distances.write_linear or self.params.distances.write_matricial)
+        total = Q * R
+        eng = self._engine()
+        qs = eng.upload([s.seq for s in data], align=align)
+        rs = eng.upload([s.seq for s in refs], align=align)
+        try:
+            idx = np.full(Q, -1, dtype=np.int64)
+            dmin = np.full(Q, np.nan)
+            ext = np.full((Q, len(extras)), np.nan)
+            mat = np.full((Q, R), np.nan) if want_matrix else None
+            step = max(1, (1 << 22) // max(R, 1))
+            for q0 in range(0, Q, step):
+                q1 = min(Q, q0 + step)
+                if R:
+                    i, d, e, m = eng.closest(qs, rs, q0, q1, str(primary), [str(x) for x in extras] if extras else (),
+                                             scores, scale=100.0 if pct else 1.0, want_matrix=want_matrix)
+                    idx[q0:q1], dmin[q0:q1] = i, d
+                    if e is not None:
+                        ext[q0:q1] = e
+                    if m is not None:
+                        mat[q0:q1] = m
+                report(self.progress_handler, "distance.x.id", q1 * R, total)
+        finally:
+            qs.free()
+            rs.free()
+
+        # groupby(x.id) over consecutive queries, first minimum wins (versus_reference.py:184-188)
+        groups = []
+        g0 = 0
+        for k in range(1, Q + 1):
+            if k == Q or data[k].id != data[g0].id:
+                groups.append((g0, k))
+                g0 = k
+        closest = []
+        for a, b in groups:
+            best = None
+            for q in range(a, b):
+                if idx[q] < 0:
+                    continue
+                v = dmin[q] * (100.0 if pct else 1.0)
+                if best is None or v < best[0]:
+                    best = (v, q)
+            if best is None:
+                raise ValueError("min() arg is an empty sequence")  # the reference's min() on all-None
+            q = best[1]
+            closest.append((q, int(idx[q]), float(dmin[q]), ext[q].copy()))
+        self.closest = closest
+
+        if self.params.pairs.write:
+            self.write_pairs(data, refs)
+        if mat is not None:
+            A = mat * 100.0 if pct else mat
+            self.write_distances_linear(data, refs, A)
+            self.write_distances_matrix(data, refs, A)
+        self.write_closest(data, refs, closest)
+        report(self.progress_handler, "Finalizing...", total, total)
+        return Results(self.work_dir, perf_counter() - ts)
+
+    # ------------------------------------------------------------------ writers
+    def write_pairs(self, data, refs):
+        create_parents(self.paths.aligned_pairs)
+        with SequencePairHandler.Formatted(self.paths.aligned_pairs, "w") as fh:
+            if not self.params.pairs.align:
+                for x in data:
+                    for y in refs:
+                        fh.write(SequencePair(x, y))
+                return
+            aligner = PairwiseAligner.Biopython(self.params.pairs.scores, engine=self._engine())
+            for x in data:
+                for pair in aligner.align_many([SequencePair(x, y) for y in refs]):
+                    fh.write(pair)
+
+    def write_distances_linear(self, data, refs, A):
+        if not self.params.distances.write_linear:
+            return
+        create_parents(self.paths.distances_linear)
+        fmt, missing = self.params.format.float, self.params.format.missing
+        metric = self.params.distances.metric
+        with DistanceHandler.Linear.WithExtras(self.paths.distances_linear, "w", missing=missing,
+                                               formatter=fmt) as fh:
+            for i, x in enumerate(data):
+                for j, y in enumerate(refs):
+                    v = A[i, j]
+                    fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+
+    def write_distances_matrix(self, data, refs, A):
+        if not self.params.distances.write_matricial:
+            return
+        create_parents(self.paths.distances_matricial)
+        fmt, missing = self.params.format.float, self.params.format.missing
+        ids = [s.id for s in data]
+        if len(set(ids)) != len(ids):
+            metric = self.params.distances.metric
+            with DistanceHandler.Matrix(self.paths.distances_matricial, "w", missing=missing, formatter=fmt) as fh:
+                for i, x in enumerate(data):
+                    for j, y in enumerate(refs):
+                        v = A[i, j]
+                        fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+            return
+        text = format_values(A, fmt, missing)
+        with open(self.paths.distances_matricial, "w") as fh:
+            if data and refs:
+                fh.write("\t".join(["", *[s.id for s in refs]]) + "\n")
+            for i, x in enumerate(data):
+                if refs:
+                    fh.write("\t".join((x.id, *text[i])) + "\n")
+
+    def write_closest(self, data, refs, closest):
+        create_parents(self.paths.closest)
+        fmt, missing = self.params.format.float, self.params.format.missing
+        pct = bool(self.params.format.percentage_multiply)
+        primary = self.params.distances.metric
+        extras = list(self.params.distances.extra_metrics)
+        with DistanceHandler.Linear.WithExtras(self.paths.closest, "w", missing=missing, formatter=fmt) as fh:
+            for q, r, d, ex in closest:
+                x, y = data[q], refs[r]
+                fh.write(Distance(primary, x, y, d * 100.0 if pct else d))
+                for metric, v in zip(extras, ex):
+                    fv = float(v) if np.isfinite(v) else None
+                    if fv is not None and pct:
+                        fv *= 100.0
+                    fh.write(Distance(metric, x, y, fv))

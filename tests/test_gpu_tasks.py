@@ -1,0 +1,244 @@
+"""GPU: aligned strings, per-pair API and the end-to-end tasks against the oracle."""
+
+from __future__ import annotations
+
+import json
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+SAMPLES = GOLDEN / "samples"
+
+
+def read_tab(name):
+    from taxi2_amd.sequences import SequenceHandler, Sequences
+
+    return list(Sequences.fromPath(SAMPLES / name, SequenceHandler.Tabfile, idHeader="seqid", seqHeader="sequence"))
+
+
+# ----------------------------------------------------------------------------- aligned strings
+def test_aligner_golden_vectors(engine):
+    """PairwiseAligner.Biopython.align on tests/test_align.py:49-163 vectors."""
+    from taxi2_amd.align import PairwiseAligner, Scores
+    from taxi2_amd.pairs import SequencePair
+    from taxi2_amd.sequences import Sequence
+
+    for r in json.loads((GOLDEN / "align_tests.json").read_text()):
+        al = PairwiseAligner.Biopython(Scores(**r["scores"]), engine=engine)
+        ax, ay = al.align(SequencePair(Sequence("idx", r["x"]), Sequence("idy", r["y"])))
+        assert ax.id == "idx" and ay.id == "idy"
+        assert [ax.seq, ay.seq] in r["solutions"], (r, ax.seq, ay.seq)
+
+
+@pytest.mark.parametrize("scores", [(1, -1, -8, -1, -1, -1), (2, -3, -5, -2, -1, -1), (1, -1, -2, -2, -1, -1),
+                                    (1, 0, 0, 0, 0, 0)])
+def test_align_strings_both_orientations(engine, scores):
+    """GPU trace + walk == the restatement's traceback, for (x, y) and for (y, x)."""
+    from oracle import restatement as R
+
+    rng = random.Random(sum(scores) + 17)
+    seqs = []
+    for _ in range(24):
+        x = "".join(rng.choice("ACGTN") for _ in range(rng.randint(1, 120)))
+        seqs.append(x)
+    for k in range(12):
+        seqs.append("".join(c if rng.random() > 0.15 else rng.choice("ACGT") for c in seqs[k]))
+    st = engine.upload(seqs, align=True)
+    xs = np.array([rng.randrange(len(seqs)) for _ in range(60)])
+    ys = np.array([rng.randrange(len(seqs)) for _ in range(60)])
+    got = engine.align_strings(st, st, xs, ys, scores, both=True)
+    sc = R.Scores(*scores)
+    for (a, b), (ab, ba) in zip(zip(xs, ys), got):
+        ax, ay, _ = R.align(seqs[a], seqs[b], sc)
+        assert ab == (ax, ay)
+        # the (y, x) alignment Biopython returns, in (x, y) column order
+        by, bx, _ = R.align(seqs[b], seqs[a], sc)
+        assert ba == (bx, by)
+    st.free()
+
+
+def test_distance_metric_calculate_per_pair(engine, oracle_c):
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequence
+
+    x, y = Sequence("idx", "gg-ccnccta"), Sequence("idy", "ggaccaccaa")
+    assert DistanceMetric.Uncorrected().calculate(x, y).d == 1.0 / 8.0
+    assert DistanceMetric.UncorrectedWithGaps().calculate(x, y).d == 2.0 / 9.0
+    assert DistanceMetric.Uncorrected().calculate(Sequence("a", "---"), Sequence("b", "nnn")).d is None
+    r = DistanceMetric.Kimura2P().calculate(x, y)
+    assert r.metric == DistanceMetric.Kimura2P() and r.x.id == "idx" and r.y.id == "idy"
+
+
+# ----------------------------------------------------------------------------- tasks
+def expected_versus_all(seqs, labels, align, oracle_c):
+    """(N, N, M) expected matrix from the C oracle + the diagonal rule."""
+    from oracle import restatement as R
+
+    work = [s.normalize() for s in seqs] if align else seqs
+    n = len(work)
+    a = np.repeat(np.arange(n), n)
+    b = np.tile(np.arange(n), n)
+    out, _ = oracle_c.batch([s.seq for s in work], a, b, align=align, scores=(1, -1, -8, -1, -1, -1),
+                            metrics=labels)
+    D = out[:, 0, :].reshape(n, n, len(labels))
+    for i in range(n):
+        for j in range(n):
+            if (work[i].id, work[i].seq, work[i].extras) == (work[j].id, work[j].seq, work[j].extras):
+                if not align or R.align(work[i].seq, work[j].seq)[0] == R.align(work[i].seq, work[j].seq)[1]:
+                    D[i, j] = np.nan
+    return work, D
+
+
+def render_expected(tmp, work, D, metrics, fmt="{:.4f}", missing="NA"):
+    from taxi2_amd.distances import Distance, DistanceHandler
+
+    lin = tmp / "exp_linear.tsv"
+    with DistanceHandler.Linear.WithExtras(lin, "w", missing=missing, formatter=fmt) as fh:
+        for i, x in enumerate(work):
+            for j, y in enumerate(work):
+                for m, metric in enumerate(metrics):
+                    v = D[i, j, m]
+                    fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+    mats = {}
+    for m, metric in enumerate(metrics):
+        p = tmp / f"exp_{metric}.tsv"
+        with DistanceHandler.Matrix(p, "w", missing=missing, formatter=fmt) as fh:
+            for i, x in enumerate(work):
+                for j, y in enumerate(work):
+                    v = D[i, j, m]
+                    fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+        mats[str(metric)] = p
+    return lin, mats
+
+
+def test_versus_all_config1(tmp_path, engine, oracle_c):
+    """Config 1: samples/Taxi2test1_10.tab, versusAll, p only, align=True (reference default),
+    100 ordered rows; plus aligned_pairs.txt on a truncated copy (pure-Python traceback oracle)."""
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    seqs = read_tab("Taxi2test1_10.tab")
+    task = VersusAll()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input.sequences = Sequences(seqs)
+    task.params.distances.metrics = [DistanceMetric.Uncorrected()]
+    task.params.pairs.write = False
+    res = task.start()
+    assert res.seconds_taken > 0
+    work, D = expected_versus_all(seqs, ("p",), True, oracle_c)
+    lin, mats = render_expected(tmp_path, work, D, task.params.distances.metrics)
+    assert (tmp_path / "out/distances/linear.tsv").read_text() == lin.read_text()
+    assert (tmp_path / "out/distances/matricial/p.tsv").read_text() == mats["p"].read_text()
+
+
+def test_versus_all_aligned_pairs_file(tmp_path, engine):
+    from oracle import restatement as R
+    from taxi2_amd.pairs import SequencePair, SequencePairHandler
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    seqs = [Sequence(s.id, s.seq[:80], s.extras) for s in read_tab("Taxi2test1_10.tab")[:5]]
+    task = VersusAll()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input.sequences = Sequences(seqs)
+    task.start()
+    exp = tmp_path / "exp_pairs.txt"
+    with SequencePairHandler.Formatted(exp, "w") as fh:
+        for x in seqs:
+            for y in seqs:
+                xn, yn = x.normalize(), y.normalize()
+                ax, ay, _ = R.align(xn.seq, yn.seq)
+                fh.write(SequencePair(Sequence(x.id, ax), Sequence(y.id, ay)))
+    assert (tmp_path / "out/align/aligned_pairs.txt").read_text() == exp.read_text()
+
+
+def test_versus_all_prealigned_ca200(tmp_path, engine, oracle_c):
+    """Config-2 shape (pre-aligned p / jc / k2p) on samples/Taxi2test1_ca200.tab."""
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    seqs = read_tab("Taxi2test1_ca200.tab")
+    metrics = [DistanceMetric.Uncorrected(), DistanceMetric.JukesCantor(), DistanceMetric.Kimura2P()]
+    task = VersusAll()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input.sequences = Sequences(seqs)
+    task.params.pairs.align = False
+    task.params.distances.metrics = metrics
+    task.params.format.percentage_multiply = True
+    task.start()
+    work, D = expected_versus_all(seqs, ("p", "jc", "k2p"), False, oracle_c)
+    lin, mats = render_expected(tmp_path, work, D * 100.0, metrics)
+    assert (tmp_path / "out/distances/linear.tsv").read_text() == lin.read_text()
+    for m in ("p", "jc", "k2p"):
+        assert (tmp_path / f"out/distances/matricial/{m}.tsv").read_text() == mats[m].read_text()
+
+
+@pytest.mark.parametrize("align", [True, False])
+def test_versus_reference(tmp_path, engine, oracle_c, align):
+    from taxi2_amd.distances import Distance, DistanceHandler, DistanceMetric
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusReference
+
+    allseqs = read_tab("Taxi2test1_120.tab")
+    data = allseqs[:30]
+    refs = allseqs[30:75]
+    # duplicate consecutive query ids merge in groupby (versus_reference.py:185)
+    data = data[:5] + [Sequence(data[4].id, data[10].seq, data[10].extras)] + data[5:]
+    task = VersusReference()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input.data = Sequences(data)
+    task.input.reference = Sequences(refs)
+    task.params.pairs.align = align
+    task.params.pairs.write = False
+    task.start()
+    wd = [s.normalize() for s in data] if align else data
+    wr = [s.normalize() for s in refs] if align else refs
+    seqs = [s.seq for s in wd] + [s.seq for s in wr]
+    Q, R = len(wd), len(wr)
+    pa = np.repeat(np.arange(Q), R)
+    pb = np.tile(np.arange(R), Q) + Q
+    out, _ = oracle_c.batch(seqs, pa, pb, align=align, scores=(1, -1, -8, -1, -1, -1))
+    vals = out[:, 0, :].reshape(Q, R, 4)
+    metrics = [DistanceMetric.Uncorrected(), DistanceMetric.UncorrectedWithGaps(), DistanceMetric.JukesCantor(),
+               DistanceMetric.Kimura2P()]
+    exp = tmp_path / "exp_closest.tsv"
+    with DistanceHandler.Linear.WithExtras(exp, "w", missing="NA", formatter="{:.4f}") as fh:
+        q = 0
+        while q < Q:
+            g = q
+            while g + 1 < Q and wd[g + 1].id == wd[q].id:
+                g += 1
+            best = None
+            for qq in range(q, g + 1):
+                for r in range(R):
+                    v = vals[qq, r, 0]
+                    if np.isfinite(v) and (best is None or v < best[0]):
+                        best = (v, qq, r)
+            _, qq, r = best
+            for m, metric in enumerate(metrics):
+                v = vals[qq, r, m]
+                fh.write(Distance(metric, wd[qq], wr[r], float(v) if np.isfinite(v) else None))
+            q = g + 1
+    assert (tmp_path / "out/closest.tsv").read_text() == exp.read_text()
+    lin = tmp_path / "exp_lin.tsv"
+    with DistanceHandler.Linear.WithExtras(lin, "w", missing="NA", formatter="{:.4f}") as fh:
+        for qq in range(Q):
+            for r in range(R):
+                v = vals[qq, r, 0]
+                fh.write(Distance(metrics[0], wd[qq], wr[r], float(v) if np.isfinite(v) else None))
+    assert (tmp_path / "out/distances/p.linear.tsv").read_text() == lin.read_text()
