@@ -37,8 +37,11 @@ N_SEQS = 50_000
 SEQ_LEN = 1000
 SEED = 0x7A12
 HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
-INT_VALU_PEAK = 256 * 128 * 2.4e9   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
-OPS_PER_CELL = 62                   # VALU instructions per DP cell, counted in the ISA
+# lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz -- one wave64 int32 VALU instruction per 4 clk per
+# SIMD, measured with tools/valu_peak.hip (DESIGN.md "Compute ceiling")
+INT_VALU_PEAK = 256 * 64 * 2.4e9
+OPS_PER_CELL = 60.5                 # VALU instructions per DP cell in the k_align<8,2> step loop
+                                    # (484 per 8-cell step, tools/loop_stats.py)
 
 
 def b_pair(L: int, M: int) -> int:

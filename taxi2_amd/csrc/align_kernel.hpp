@@ -18,15 +18,16 @@
 // Mapping to gfx950:
 //   * a workgroup of W waves owns one pair; lane l of wave w owns columns
 //     j0 = (w*64 + l)*K + 1 .. j0+K-1 of the column sequence and keeps their previous-row
-//     state in VGPRs (15 x K); rows stream through the lanes as a systolic wavefront: at local
+//     state in VGPRs (11 x K); rows stream through the lanes as a systolic wavefront: at local
 //     step s lane l works on row i = s - l + 1.
 //   * lane l-1 -> lane l hand-off of the last column state is one DPP `wave_shr:1` per
 //     32-bit word (counters use bound_ctrl zero-fill for wave 0's left boundary); wave w-1
 //     lane 63 -> wave w lane 0 goes through an LDS ring, wave w running two 64-step
 //     intervals behind (one s_barrier per interval).
-//   * a cell only needs its diagonal neighbour's best state (score + the two priority-selected
-//     counter pairs, 5 VGPRs), so that summary is taken before the column is overwritten in
-//     place: no register copies between cells or steps.
+//   * per column only G = max(M, Iy) and Ix are kept (with both orientations' counters); the
+//     3-way Biopython priorities reduce to 2-way selects on (G, Ix) and (F = max(M, Ix), Iy)
+//     (see GCol below), and a cell's diagonal summary is derived from the column state before
+//     the column is overwritten in place: no register copies between cells or steps.
 //   * counters are packed two fields per VGPR: w0 = valid | ts << 16, w1 = gap | tv << 20
 //     (lengths <= 4095); the M contribution is a 32-bit per-column LUT shifted by the row's
 //     base code (bits 0-3 valid, 8-15 the column byte, 16-19 transition, 20-23 transversion),
@@ -56,90 +57,140 @@ __device__ __forceinline__ uint32_t shr_zero(uint32_t v) {
 }
 
 // ---------------------------------------------------------------- Gotoh state per column
-struct GState {
-    int M, X, Y;
-    C2 m0, m1, x0, x1, y0, y1;  // counters of the traceback path from this cell/state;
-                                // suffix 0 = orientation A (x, y), 1 = orientation B (y, x)
+// A column keeps, for the cell of the previous row: G = max(M, Iy) (+ whether M won, `gsrc`)
+// and Ix, each with the counters of both orientations.  That is all the next row needs:
+//   * Ix(i,j) = max(M + o, Ix + e, Iy + o) over (i-1, j) = max(G + o, Ix + e), and the 3-way
+//     priorities reduce to 2-way rules on (G, Ix):
+//       A (M>Ix>Iy): take G iff G+o > Ix+e, or equal and G came from M;
+//       B (M>Iy>Ix): take G iff G+o >= Ix+e;
+//   * the diagonal successor's best state = max(G, Ix) with the same two rules (offsets 0).
+// A cell hands its right neighbour F = max(M, Ix) (+ `fsrc` = M won) and Iy:
+//   * Iy(i,j+1) = max(F + o, Iy + e): A takes F iff F+o >= Iy+e (M and Ix beat Iy);
+//     B takes F iff F+o > Iy+e, or equal and F came from M (Iy beats Ix in B);
+//   * the best state of the cell = max(F, Iy) with the same rules (offsets 0).
+// Tie-tagged scores: every score is stored doubled and bit 0 of G / F is the "M won" flag
+// (M is formed odd, Ix / Iy are kept even), so max(M, Iy) sets the flag by itself and each
+// rule above is ONE compare: "G+o > Ix+e, or equal and gsrc" == (2G+gsrc+2o > 2Ix+2e) and
+// "G+o >= Ix+e" == (2G+gsrc+2o >= 2Ix+2e).  No boolean state crosses cells, rows or the
+// divergent active-row branch.  The Gotoh path runs on doubled scores (KScores2).
+// (Derivation checked exhaustively against the 3-way rules by the GPU parity tests.)
+struct GCol {
+    int G;      // 2 * max(M, Iy) + (M won)
+    C2 ga, gb;  // counters of G's state; a = orientation A (x, y), b = orientation B (y, x)
+    int X;      // 2 * Ix
+    C2 xa, xb;
 };
 
-// Best state of a cell under both priorities (what the diagonal successor reads).
+struct GLeft {
+    int F;      // 2 * max(M, Ix) + (M won)
+    C2 fa, fb;
+    int Y;      // 2 * Iy
+    C2 ya, yb;
+};
+
+// Best state of a cell under both priorities (what the diagonal successor reads); h is the
+// doubled score with an arbitrary bit 0.
 struct GBest {
     int h;
     C2 a, b;
 };
 
-__device__ __forceinline__ GBest g_best(const GState& e) {
-    const int h = imax3(e.M, e.X, e.Y);
-    const bool tm = e.M == h, tx = e.X == h, ty = e.Y == h;
-    return GBest{h, csel(tm, e.m0, csel(tx, e.x0, e.y0)), csel(tm, e.m1, csel(ty, e.y1, e.x1))};
+__device__ __forceinline__ KScores doubled(const KScores& k) {
+    return KScores{2 * k.ma, 2 * k.mi, 2 * k.io, 2 * k.ie, 2 * k.eo, 2 * k.ee};
 }
 
-__device__ __forceinline__ GState g_row0(int j, const KScores& sc) {
-    GState s;
-    s.M = (j == 0) ? 0 : NEG_INF;
-    s.X = NEG_INF;
-    s.Y = (j == 0) ? NEG_INF : sc.eo + sc.ee * (j - 1);
-    s.m0 = s.m1 = s.x0 = s.x1 = s.y0 = s.y1 = C2{0u, 0u};
-    return s;
+__device__ __forceinline__ GBest g_best_col(const GCol& u) {
+    const bool pa = u.G > u.X;
+    const bool pb = u.G >= u.X;
+    return GBest{max(u.G, u.X), csel(pa, u.ga, u.xa), csel(pb, u.gb, u.xb)};
 }
 
-// Column-0 boundary at row i (only the Ix score is finite; all counters are zero).
-__device__ __forceinline__ GState g_shr_first(const GState& v, int i, const KScores& sc) {
-    GState r;
-    r.M = (int)shr_old((uint32_t)v.M, (uint32_t)NEG_INF);
-    r.X = (int)shr_old((uint32_t)v.X, (uint32_t)(sc.eo + sc.ee * (i - 1)));
+__device__ __forceinline__ GBest g_best_left(const GLeft& l) {
+    const bool pa = l.F >= l.Y;
+    const bool pb = l.F > l.Y;
+    return GBest{max(l.F, l.Y), csel(pa, l.fa, l.ya), csel(pb, l.fb, l.yb)};
+}
+
+// Row 0 (doubled scores d): M(0,0) = 0, Iy(0,j) = eo + ee*(j-1), everything else -inf,
+// counters 0.
+__device__ __forceinline__ GCol g_col_row0(int j, const KScores& d) {
+    GCol c;
+    c.G = (j == 0) ? 1 : d.eo + d.ee * (j - 1);
+    c.X = NEG_INF;
+    c.ga = c.gb = c.xa = c.xb = C2{0u, 0u};
+    return c;
+}
+__device__ __forceinline__ GLeft g_left_row0(int j, const KScores& d) {
+    GLeft l;
+    l.F = (j == 0) ? 1 : NEG_INF;
+    l.Y = (j == 0) ? NEG_INF : d.eo + d.ee * (j - 1);
+    l.fa = l.fb = l.ya = l.yb = C2{0u, 0u};
+    return l;
+}
+
+// Lane 0 of wave 0 receives column 0 at row i: Ix = eo + ee*(i-1) (so F = Ix, untagged),
+// M = Iy = -inf, counters 0 (bound_ctrl zero-fill).
+__device__ __forceinline__ GLeft g_shr_first(const GLeft& v, int i, const KScores& d) {
+    GLeft r;
+    r.F = (int)shr_old((uint32_t)v.F, (uint32_t)(d.eo + d.ee * (i - 1)));
     r.Y = (int)shr_old((uint32_t)v.Y, (uint32_t)NEG_INF);
 #define T2_SZ(f) r.f.w0 = shr_zero(v.f.w0); r.f.w1 = shr_zero(v.f.w1);
-    T2_SZ(m0) T2_SZ(m1) T2_SZ(x0) T2_SZ(x1) T2_SZ(y0) T2_SZ(y1)
+    T2_SZ(fa) T2_SZ(fb) T2_SZ(ya) T2_SZ(yb)
 #undef T2_SZ
     return r;
 }
 
-__device__ __forceinline__ GState g_shr_old(const GState& v, const GState& o) {
-    GState r;
-    r.M = (int)shr_old((uint32_t)v.M, (uint32_t)o.M);
-    r.X = (int)shr_old((uint32_t)v.X, (uint32_t)o.X);
+__device__ __forceinline__ GLeft g_shr_old(const GLeft& v, const GLeft& o) {
+    GLeft r;
+    r.F = (int)shr_old((uint32_t)v.F, (uint32_t)o.F);
     r.Y = (int)shr_old((uint32_t)v.Y, (uint32_t)o.Y);
 #define T2_SO(f) r.f.w0 = shr_old(v.f.w0, o.f.w0); r.f.w1 = shr_old(v.f.w1, o.f.w1);
-    T2_SO(m0) T2_SO(m1) T2_SO(x0) T2_SO(x1) T2_SO(y0) T2_SO(y1)
+    T2_SO(fa) T2_SO(fb) T2_SO(ya) T2_SO(yb)
 #undef T2_SO
     return r;
 }
 
-// One Gotoh cell, in place.  d = best of (i-1, j-1); u = (i-1, j) on entry, (i, j) on exit;
-// l = (i, j-1).  Returns the best of the old u for the next column's diagonal.
-__device__ __forceinline__ GBest g_cell(const GBest& d, GState& u, const GState& l, int s,
-                                        uint32_t inc0, uint32_t inc1, uint32_t gx, uint32_t gy,
-                                        int ox, int ex, int oy, int ey) {
-    const GBest nd = g_best(u);
-    GState r;
-    // M: diagonal move from the best state of (i-1, j-1)
-    r.M = d.h + s;
-    r.m0 = C2{d.a.w0 + inc0, d.a.w1 + inc1};
-    r.m1 = C2{d.b.w0 + inc0, d.b.w1 + inc1};
-    // Ix: consume x[i-1] against a gap (from above); A: M>Ix>Iy, B: M>Iy>Ix
-    {
-        const int ca = u.M + ox, cb = u.X + ex, cc = u.Y + ox;
-        const int X = imax3(ca, cb, cc);
-        r.X = X;
-        const bool xa = ca == X, xb = cb == X, xc = cc == X;
-        const C2 a = csel(xa, u.m0, csel(xb, u.x0, u.y0));
-        const C2 b = csel(xa, u.m1, csel(xc, u.y1, u.x1));
-        r.x0 = C2{a.w0, a.w1 + gx};
-        r.x1 = C2{b.w0, b.w1 + gx};
-    }
+// One Gotoh cell, in place, on doubled scores.  d = best of (i-1, j-1); u = column state of
+// (i-1, j) on entry, (i, j) on exit; l = left payload of (i, j-1) on entry, (i, j) on exit.
+// Returns the best of (i-1, j) for the next column's diagonal.
+__device__ __forceinline__ GBest g_cell(const GBest& d, GCol& u, GLeft& l, int s, uint32_t inc0,
+                                        uint32_t inc1, uint32_t gx, uint32_t gy, int ox, int ex, int oy,
+                                        int ey) {
+    const GBest nd = g_best_col(u);
+    // M: diagonal move from the best state of (i-1, j-1); odd = tagged "M"
+    const int M = (d.h | 1) + s;
+    const C2 ma{d.a.w0 + inc0, d.a.w1 + inc1};
+    const C2 mb{d.b.w0 + inc0, d.b.w1 + inc1};
+    // Ix: consume x[i-1] against a gap (from above)
+    const int cg = u.G + ox, cx = u.X + ex;
+    const int X = max(cg, cx) & ~1;
+    C2 xa = csel(cg > cx, u.ga, u.xa);
+    C2 xb = csel(cg >= cx, u.gb, u.xb);
+    xa.w1 += gx;
+    xb.w1 += gx;
     // Iy: consume y[j-1] against a gap (from the left)
-    {
-        const int ca = l.M + oy, cb = l.X + oy, cc = l.Y + ey;
-        const int Y = imax3(ca, cb, cc);
-        r.Y = Y;
-        const bool ya = ca == Y, yb = cb == Y, yc = cc == Y;
-        const C2 a = csel(ya, l.m0, csel(yb, l.x0, l.y0));
-        const C2 b = csel(ya, l.m1, csel(yc, l.y1, l.x1));
-        r.y0 = C2{a.w0, a.w1 + gy};
-        r.y1 = C2{b.w0, b.w1 + gy};
-    }
-    u = r;
+    const int cf = l.F + oy, cy = l.Y + ey;
+    const int Y = max(cf, cy) & ~1;
+    C2 ya = csel(cf >= cy, l.fa, l.ya);
+    C2 yb = csel(cf > cy, l.fb, l.yb);
+    ya.w1 += gy;
+    yb.w1 += gy;
+    // column state of (i, j) for the next row: M wins ties (M odd, Y even)
+    const bool gs = M > Y;
+    u.G = max(M, Y);
+    u.ga = csel(gs, ma, ya);
+    u.gb = csel(gs, mb, yb);
+    u.X = X;
+    u.xa = xa;
+    u.xb = xb;
+    // left payload of (i, j) for the next column
+    const bool fs = M > X;
+    l.F = max(M, X);
+    l.fa = csel(fs, ma, xa);
+    l.fb = csel(fs, mb, xb);
+    l.Y = Y;
+    l.ya = ya;
+    l.yb = yb;
     return nd;
 }
 
@@ -192,21 +243,19 @@ __device__ __forceinline__ NBest n_cell(const NBest& d, NState& u, const NState&
 
 // ---------------------------------------------------------------- LDS ring entry
 struct RingEntry {
-    uint4 q[4];  // 16 words; Gotoh uses 15, NW 5
+    uint4 q[4];  // 16 words; Gotoh uses 10, NW 5
 };
 
-__device__ __forceinline__ void ring_put(RingEntry* e, const GState& s) {
-    e->q[0] = make_uint4((uint32_t)s.M, (uint32_t)s.X, (uint32_t)s.Y, s.m0.w0);
-    e->q[1] = make_uint4(s.m0.w1, s.m1.w0, s.m1.w1, s.x0.w0);
-    e->q[2] = make_uint4(s.x0.w1, s.x1.w0, s.x1.w1, s.y0.w0);
-    e->q[3] = make_uint4(s.y0.w1, s.y1.w0, s.y1.w1, 0u);
+__device__ __forceinline__ void ring_put(RingEntry* e, const GLeft& s) {
+    e->q[0] = make_uint4((uint32_t)s.F, s.fa.w0, s.fa.w1, s.fb.w0);
+    e->q[1] = make_uint4(s.fb.w1, (uint32_t)s.Y, s.ya.w0, s.ya.w1);
+    e->q[2] = make_uint4(s.yb.w0, s.yb.w1, 0u, 0u);
 }
-__device__ __forceinline__ void ring_get(const RingEntry* e, GState& s) {
-    const uint4 a = e->q[0], b = e->q[1], c = e->q[2], d = e->q[3];
-    s.M = (int)a.x; s.X = (int)a.y; s.Y = (int)a.z; s.m0.w0 = a.w;
-    s.m0.w1 = b.x; s.m1.w0 = b.y; s.m1.w1 = b.z; s.x0.w0 = b.w;
-    s.x0.w1 = c.x; s.x1.w0 = c.y; s.x1.w1 = c.z; s.y0.w0 = c.w;
-    s.y0.w1 = d.x; s.y1.w0 = d.y; s.y1.w1 = d.z;
+__device__ __forceinline__ void ring_get(const RingEntry* e, GLeft& s) {
+    const uint4 a = e->q[0], b = e->q[1], c = e->q[2];
+    s.F = (int)a.x; s.fa.w0 = a.y; s.fa.w1 = a.z; s.fb.w0 = a.w;
+    s.fb.w1 = b.x; s.Y = (int)b.y; s.ya.w0 = b.z; s.ya.w1 = b.w;
+    s.yb.w0 = c.x; s.yb.w1 = c.y;
 }
 __device__ __forceinline__ void ring_put(RingEntry* e, const NState& s) {
     e->q[0] = make_uint4((uint32_t)s.S, s.a.w0, s.a.w1, s.b.w0);
@@ -224,22 +273,19 @@ constexpr int WAVE_LAG = 2;    // intervals wave w runs behind wave w-1
 // Output layout selector.
 enum OutMode : int { OUT_BOTH = 0, OUT_AB = 1 };
 
+// Per-variant state types: T = per-column state, P = lane-to-lane payload, B = diagonal summary.
 template <bool LINEAR>
 struct StateOf {
-    using T = GState;
+    using T = GCol;
+    using P = GLeft;
     using B = GBest;
 };
 template <>
 struct StateOf<true> {
     using T = NState;
+    using P = NState;
     using B = NBest;
 };
-
-template <bool LINEAR>
-__device__ __forceinline__ typename StateOf<LINEAR>::B best_of(const typename StateOf<LINEAR>::T& s) {
-    if constexpr (LINEAR) return s;
-    else return g_best(s);
-}
 
 // Per-lane, per-pair column constants.
 template <int K>
@@ -250,26 +296,27 @@ struct LaneCols {
     uint32_t lastbits; // column j == nB (end-gap scores for Ix / vertical)
 };
 
-// One systolic step for this lane: receive the left column state, then update K cells of
-// row i = s - lane + 1.  `carry` is the best-state summary of the left input of the
+// One systolic step for this lane: receive the left payload, then update K cells of row
+// i = s - lane + 1.  `pay` is this lane's outgoing payload (its last column, previous row on
+// entry, this row on exit); `carry` is the best-state summary of the left input of the
 // previous step (the diagonal of this step's first cell) and is replaced by this step's.
 template <int K, int W, bool LINEAR, bool FIRST>
 __device__ __forceinline__ void dp_step(int s, int lane, int nA, typename StateOf<LINEAR>::T (&st)[K],
-                                        typename StateOf<LINEAR>::B& carry, const LaneCols<K>& lc,
-                                        const uint32_t* __restrict__ xinfo,
+                                        typename StateOf<LINEAR>::P& pay, typename StateOf<LINEAR>::B& carry,
+                                        const LaneCols<K>& lc, const uint32_t* __restrict__ xinfo,
                                         const RingEntry* __restrict__ ring_in, RingEntry* __restrict__ ring_out,
                                         const KScores& sc) {
-    using S = typename StateOf<LINEAR>::T;
+    using P = typename StateOf<LINEAR>::P;
     using B = typename StateOf<LINEAR>::B;
-    S in;
+    P in;
     if constexpr (FIRST) {
-        if constexpr (LINEAR) in = n_shr_first(st[K - 1], s + 1, sc);
-        else in = g_shr_first(st[K - 1], s + 1, sc);
+        if constexpr (LINEAR) in = n_shr_first(pay, s + 1, sc);
+        else in = g_shr_first(pay, s + 1, sc);
     } else {
-        S old;
+        P old;
         ring_get(ring_in + ((s + 1) & (RING - 1)), old);
-        if constexpr (LINEAR) in = n_shr_old(st[K - 1], old);
-        else in = g_shr_old(st[K - 1], old);
+        if constexpr (LINEAR) in = n_shr_old(pay, old);
+        else in = g_shr_old(pay, old);
     }
     const int i = s - lane + 1;
     if (i >= 1 && i <= nA) {
@@ -282,6 +329,7 @@ __device__ __forceinline__ void dp_step(int s, int lane, int nA, typename StateO
         const int oy = lastrow ? sc.eo : sc.io;
         const int ey = lastrow ? sc.ee : sc.ie;
         B d = carry;
+        P l = in;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t lut = lc.lut[k];
@@ -293,16 +341,19 @@ __device__ __forceinline__ void dp_step(int s, int lane, int nA, typename StateO
             const uint32_t gy = (gym >> k) & 1u;    // gap (Iy move)
             const bool lastcol = (lc.lastbits >> k) & 1u;
             if constexpr (LINEAR) {
-                d = n_cell(d, st[k], k == 0 ? in : st[k - 1], sv, inc0, inc1, gx, gy,
+                d = n_cell(d, st[k], k == 0 ? l : st[k - 1], sv, inc0, inc1, gx, gy,
                            lastcol ? sc.ee : sc.ie, ey);
             } else {
-                d = g_cell(d, st[k], k == 0 ? in : st[k - 1], sv, inc0, inc1, gx, gy,
-                           lastcol ? sc.eo : sc.io, lastcol ? sc.ee : sc.ie, oy, ey);
+                d = g_cell(d, st[k], l, sv, inc0, inc1, gx, gy, lastcol ? sc.eo : sc.io,
+                           lastcol ? sc.ee : sc.ie, oy, ey);
             }
         }
-        if (W > 1 && ring_out != nullptr && lane == 63) ring_put(ring_out + (i & (RING - 1)), st[K - 1]);
+        if constexpr (LINEAR) pay = st[K - 1];
+        else pay = l;
+        if (W > 1 && ring_out != nullptr && lane == 63) ring_put(ring_out + (i & (RING - 1)), pay);
     }
-    carry = best_of<LINEAR>(in);
+    if constexpr (LINEAR) carry = in;
+    else carry = g_best_left(in);
 }
 
 // Dynamic LDS: [uint32 xinfo[xcap]] [RingEntry ring[W-1][RING]]
@@ -314,7 +365,8 @@ k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xca
         double* __restrict__ out, int32_t* __restrict__ sout) {
     using S = typename StateOf<LINEAR>::T;
     using B = typename StateOf<LINEAR>::B;
-    const KScores sc = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
+    const KScores sc0 = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
+    const KScores sc = LINEAR ? sc0 : doubled(sc0);  // DP scores (Gotoh: tie-tagged, doubled)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* xinfo = reinterpret_cast<uint32_t*>(smem);
     RingEntry* rings = reinterpret_cast<RingEntry*>(smem + ((size_t)xcap * 4 + 15) / 16 * 16);
@@ -354,7 +406,7 @@ k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xca
                 }
                 if (sout) {
                     const int n = nA + nB;
-                    sout[p] = n == 0 ? 0 : (LINEAR ? n * sc.ee : sc.eo + sc.ee * (n - 1));
+                    sout[p] = n == 0 ? 0 : (LINEAR ? n * sc0.ee : sc0.eo + sc0.ee * (n - 1));
                 }
             }
             continue;
@@ -401,11 +453,17 @@ k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xca
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if constexpr (LINEAR) st[k] = n_row0(j0 + k, sc);
-            else st[k] = g_row0(j0 + k, sc);
+            else st[k] = g_col_row0(j0 + k, sc);
         }
+        typename StateOf<LINEAR>::P pay;
         B carry;
-        if constexpr (LINEAR) carry = n_row0(j0 - 1, sc);
-        else carry = g_best(g_row0(j0 - 1, sc));
+        if constexpr (LINEAR) {
+            pay = st[K - 1];
+            carry = n_row0(j0 - 1, sc);
+        } else {
+            pay = g_left_row0(j0 + K - 1, sc);
+            carry = g_best_col(g_col_row0(j0 - 1, sc));
+        }
 
         const RingEntry* ring_in = (w > 0) ? rings + (size_t)(w - 1) * RING : nullptr;
         RingEntry* ring_out = (w < W - 1) ? rings + (size_t)w * RING : nullptr;
@@ -421,10 +479,10 @@ k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xca
             if (W == 1 || (blk >= 0 && blk < nblk)) {
                 if (w == 0) {
                     for (int s = s0; s < s1; ++s)
-                        dp_step<K, W, LINEAR, true>(s, lane, nA, st, carry, lc, xinfo, ring_in, ring_out, sc);
+                        dp_step<K, W, LINEAR, true>(s, lane, nA, st, pay, carry, lc, xinfo, ring_in, ring_out, sc);
                 } else {
                     for (int s = s0; s < s1; ++s)
-                        dp_step<K, W, LINEAR, false>(s, lane, nA, st, carry, lc, xinfo, ring_in, ring_out, sc);
+                        dp_step<K, W, LINEAR, false>(s, lane, nA, st, pay, carry, lc, xinfo, ring_in, ring_out, sc);
                 }
             }
             if (W > 1) __syncthreads();
@@ -440,17 +498,17 @@ k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xca
 #pragma unroll
             for (int k = 1; k < K; ++k)
                 if (k == kk) e = st[k];
-            const B fin = best_of<LINEAR>(e);
             C2 ca, cb;
             int score;
             if constexpr (LINEAR) {
-                ca = fin.a;
-                cb = fin.b;
-                score = fin.S;
+                ca = e.a;
+                cb = e.b;
+                score = e.S;
             } else {
+                const GBest fin = g_best_col(e);
                 ca = fin.a;
                 cb = fin.b;
-                score = fin.h;
+                score = fin.h >> 1;
             }
             // orientation A is (rows, cols); map back to (a, b)
             const C2 ab = swp ? cb : ca;

@@ -128,14 +128,14 @@ void launch_align(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView
 // DEF = the default TaxI2 scores (align.py:20-27) as compile-time constants; OCC = waves per
 // SIMD the register allocation targets.
 const Variant kGotohDef[] = {
-    T2_VARIANT(4, 1, false, true, 2), T2_VARIANT(6, 1, false, true, 2), T2_VARIANT(8, 1, false, true, 2),
-    T2_VARIANT(6, 2, false, true, 2), T2_VARIANT(8, 2, false, true, 2), T2_VARIANT(6, 4, false, true, 2),
-    T2_VARIANT(8, 4, false, true, 2), T2_VARIANT(8, 8, false, true, 2),
+    T2_VARIANT(4, 1, false, true, 3), T2_VARIANT(6, 1, false, true, 3), T2_VARIANT(8, 1, false, true, 3),
+    T2_VARIANT(6, 2, false, true, 3), T2_VARIANT(8, 2, false, true, 3), T2_VARIANT(6, 4, false, true, 3),
+    T2_VARIANT(8, 4, false, true, 3), T2_VARIANT(8, 8, false, true, 3),
 };
 const Variant kGotoh[] = {
-    T2_VARIANT(4, 1, false, false, 2), T2_VARIANT(6, 1, false, false, 2), T2_VARIANT(8, 1, false, false, 2),
-    T2_VARIANT(6, 2, false, false, 2), T2_VARIANT(8, 2, false, false, 2), T2_VARIANT(6, 4, false, false, 2),
-    T2_VARIANT(8, 4, false, false, 2), T2_VARIANT(8, 8, false, false, 2),
+    T2_VARIANT(4, 1, false, false, 3), T2_VARIANT(6, 1, false, false, 3), T2_VARIANT(8, 1, false, false, 3),
+    T2_VARIANT(6, 2, false, false, 3), T2_VARIANT(8, 2, false, false, 3), T2_VARIANT(6, 4, false, false, 3),
+    T2_VARIANT(8, 4, false, false, 3), T2_VARIANT(8, 8, false, false, 3),
 };
 const Variant kLinear[] = {
     T2_VARIANT(4, 1, true, false, 2), T2_VARIANT(8, 1, true, false, 2), T2_VARIANT(8, 2, true, false, 2),
@@ -143,9 +143,9 @@ const Variant kLinear[] = {
 };
 // Experimental shapes for tuning (selected only through TAXI2_VARIANT="K,W,OCC").
 const Variant kSweep[] = {
-    T2_VARIANT(8, 2, false, true, 3), T2_VARIANT(6, 3, false, true, 2), T2_VARIANT(6, 3, false, true, 3),
-    T2_VARIANT(4, 4, false, true, 3), T2_VARIANT(4, 4, false, true, 4), T2_VARIANT(5, 4, false, true, 3),
-    T2_VARIANT(4, 4, false, true, 2),
+    T2_VARIANT(8, 2, false, true, 2), T2_VARIANT(8, 1, false, true, 2), T2_VARIANT(8, 1, false, true, 4),
+    T2_VARIANT(8, 2, false, true, 4), T2_VARIANT(6, 3, false, true, 3), T2_VARIANT(4, 4, false, true, 4),
+    T2_VARIANT(4, 4, false, true, 3),
 };
 
 bool is_default(const KScores& k) {
@@ -201,10 +201,10 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (max_len > 4095) return fail(ctx, "sequence length %d exceeds the aligner's limit of 4095", max_len);
     const Variant* v = pick_variant(k, max_len);
     if (!v) return fail(ctx, "sequence length %d exceeds the aligner's column capacity", max_len);
-    // int DP range check: every finite score stays far above NEG_INF
+    // int DP range check: every finite (doubled, tie-tagged) score stays far above NEG_INF
     const long long mag = std::max({std::llabs(k.ma), std::llabs(k.mi), std::llabs(k.io),
                                     std::llabs(k.ie), std::llabs(k.eo), std::llabs(k.ee)});
-    if (mag * (2LL * max_len + 2) >= (1LL << 27))
+    if (mag * (2LL * max_len + 2) >= (1LL << 26))
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
     const size_t lds = align_lds_bytes(*v, xcap);

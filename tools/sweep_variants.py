@@ -28,10 +28,15 @@ def main() -> None:
     ap.add_argument("--len", type=int, default=1000)
     ap.add_argument("--nseq", type=int, default=50000)
     ap.add_argument("--scores", default="1,-1,-8,-1,-1,-1")
+    ap.add_argument("--lib", default=None, help="A/B another build of the engine library")
     args = ap.parse_args()
     import torch
 
+    from taxi2_amd import _native
     from taxi2_amd._native import Engine
+
+    if args.lib:
+        _native.LIB_PATH = Path(args.lib).resolve()
     from taxi2_amd.synth import family_packed
 
     metrics = ("p", "p-gaps", "jc", "k2p")
