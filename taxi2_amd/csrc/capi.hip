@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/taxi2_mi355x.h"
+#include "align1_kernel.hpp"
 #include "align_kernel.hpp"
 #include "common.hpp"
 #include "pack_kernels.hpp"
@@ -49,6 +50,8 @@ struct taxi2_ctx {
     size_t d_out_bytes = 0;
     void* d_aux = nullptr;
     size_t d_aux_bytes = 0;
+    void* d_work = nullptr;  // single-orientation aligner: [count][worklist...]
+    size_t d_work_bytes = 0;
 };
 
 namespace {
@@ -193,6 +196,92 @@ size_t align_lds_bytes(const Variant& v, int xcap) {
     return ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(v.W - 1) * RING * sizeof(RingEntry);
 }
 
+// ---------------------------------------------------------------- single-orientation variants
+struct Variant1 {
+    int K, W, occ;
+    bool def;
+    const void* fn[2];  // pass 1 (orientation A + divergence flag), pass 2 (orientation B)
+    void (*launch[2])(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int,
+                      int, double*, int32_t*, uint32_t*, uint32_t*);
+};
+
+template <int K, int W, bool DEF, int OCC, bool B>
+void launch_align1(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc,
+                   MetricSpec ms, int xcap, int om, double* out, int32_t* so, uint32_t* wl, uint32_t* wc) {
+    hipLaunchKernelGGL((k_align1<K, W, DEF, OCC, B>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so, wl, wc);
+}
+
+#define T2_VARIANT1(K, W, DEF, OCC)                                                                   \
+    Variant1{K, W, OCC, DEF,                                                                         \
+             {(const void*)&k_align1<K, W, DEF, OCC, false>, (const void*)&k_align1<K, W, DEF, OCC, true>}, \
+             {&launch_align1<K, W, DEF, OCC, false>, &launch_align1<K, W, DEF, OCC, true>}}
+
+// Ordered by column capacity 64 * K * W (max 1023 = A1_MAX_LEN).
+const Variant1 kAlign1Def[] = {
+    T2_VARIANT1(4, 1, true, 4), T2_VARIANT1(8, 1, true, 4), T2_VARIANT1(6, 2, true, 4), T2_VARIANT1(8, 2, true, 4),
+};
+const Variant1 kAlign1[] = {
+    T2_VARIANT1(4, 1, false, 4), T2_VARIANT1(8, 1, false, 4), T2_VARIANT1(6, 2, false, 4),
+    T2_VARIANT1(8, 2, false, 4),
+};
+// Tuning shapes (TAXI2_VARIANT1="K,W,OCC").
+const Variant1 kAlign1Sweep[] = {
+    T2_VARIANT1(8, 2, true, 3), T2_VARIANT1(8, 2, true, 5), T2_VARIANT1(4, 4, true, 4), T2_VARIANT1(4, 4, true, 6),
+    T2_VARIANT1(10, 2, true, 3), T2_VARIANT1(10, 2, true, 4),
+};
+
+const Variant1* pick_variant1(const KScores& k, int max_len) {
+    const bool def = is_default(k);
+    if (const char* force = getenv("TAXI2_VARIANT1")) {
+        int K = 0, W = 0, occ = 0;
+        if (sscanf(force, "%d,%d,%d", &K, &W, &occ) == 3 && 64 * K * W >= max_len) {
+            for (const auto* tab : {kAlign1Sweep, kAlign1Def, kAlign1}) {
+                const size_t n = tab == kAlign1Sweep ? sizeof kAlign1Sweep / sizeof kAlign1Sweep[0]
+                                 : tab == kAlign1Def ? sizeof kAlign1Def / sizeof kAlign1Def[0]
+                                                     : sizeof kAlign1 / sizeof kAlign1[0];
+                for (size_t i = 0; i < n; ++i)
+                    if (tab[i].K == K && tab[i].W == W && tab[i].occ == occ && tab[i].def == def) return &tab[i];
+            }
+        }
+    }
+    const Variant1* tab = def ? kAlign1Def : kAlign1;
+    const int n = (int)(def ? sizeof kAlign1Def / sizeof kAlign1Def[0] : sizeof kAlign1 / sizeof kAlign1[0]);
+    for (int i = 0; i < n; ++i)
+        if (64 * tab[i].K * tab[i].W >= max_len) return &tab[i];
+    return nullptr;
+}
+
+// Both passes of the single-orientation aligner, stream-ordered (no host synchronisation).
+int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
+                        const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
+                        hipStream_t st, int xcap) {
+    const size_t lds = ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(v.W - 1) * RING * sizeof(RingEntry1);
+    if (lds > 160 * 1024) return fail(ctx, "LDS requirement %zu exceeds 160 KiB", lds);
+    if (lds > 64 * 1024)
+        for (const void* fn : v.fn)
+            HIP_TRY(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, ((size_t)ps.count + 1) * 4)) return -1;
+    uint32_t* wcount = (uint32_t*)ctx->d_work;
+    uint32_t* wlist = wcount + 1;
+    HIP_TRY(ctx, hipMemsetAsync(wcount, 0, 4, st));
+    const int64_t grid1 = std::min<int64_t>(ps.count, (int64_t)1 << 30);
+    v.launch[0](dim3((unsigned)grid1), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
+                d_out, d_scores, wlist, wcount);
+    HIP_TRY(ctx, hipGetLastError());
+    // pass 2 walks the worklist with a resident-size grid (its length is known only on the device)
+    const int64_t grid2 = std::min<int64_t>(ps.count, (int64_t)ctx->num_cus * 16);
+    v.launch[1](dim3((unsigned)grid2), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
+                d_out, nullptr, wlist, wcount);
+    HIP_TRY(ctx, hipGetLastError());
+    if (getenv("TAXI2_A1_STATS")) {  // diagnostics: share of pairs re-run in orientation B
+        uint32_t n2 = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(&n2, wcount, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(ctx, hipStreamSynchronize(st));
+        fprintf(stderr, "taxi2: single-orientation pass 2 re-ran %u of %lld pairs\n", n2, (long long)ps.count);
+    }
+    return 0;
+}
+
 int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                        const taxi2_scores* sc, const MetricSpec& ms, int out_mode, double* d_out,
                        int32_t* d_scores, hipStream_t st) {
@@ -207,6 +296,11 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (mag * (2LL * max_len + 2) >= (1LL << 26))
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
+    if (!is_linear(k) && max_len <= A1_MAX_LEN && !getenv("TAXI2_NO_ALIGN1")) {
+        if (ps.count <= 0) return 0;
+        const Variant1* v1 = pick_variant1(k, max_len);
+        if (v1) return launch_align1_pairs(ctx, *v1, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, xcap);
+    }
     const size_t lds = align_lds_bytes(*v, xcap);
     if (lds > 160 * 1024) return fail(ctx, "LDS requirement %zu exceeds 160 KiB", lds);
     if (lds > 64 * 1024)
@@ -305,6 +399,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     for (int i = 0; i < (int)ctx->sets.size(); ++i) taxi2_set_destroy(ctx, i);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
+    if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -226,3 +226,70 @@ def test_rect_and_closest(engine, oracle_c, align):
         assert_metrics_equal(ex[k][None, :], e[None, :], ("p-gaps", "jc", "k2p"))
     qs.free()
     rs.free()
+
+
+# ----------------------------------------------------------------------------- single orientation
+def _with_env(name, value, fn):
+    import os
+
+    old = os.environ.get(name)
+    if value is None:
+        os.environ.pop(name, None)
+    else:
+        os.environ[name] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop(name, None)
+        else:
+            os.environ[name] = old
+
+
+def test_single_orientation_divergent_pairs(engine, oracle_c):
+    """Sequences <= 1023 run the single-orientation kernel (align1_kernel.hpp): orientation A for
+    every pair, orientation B re-run only for pairs whose A path passes a divergent Ix/Iy tie.
+    Tie-heavy families (identical ancestors, short indels), ragged lengths, lowercase and IUPAC
+    bytes (the byte-compare path of the substitution score): counters must equal the oracle's
+    AND the two-orientation kernel's, and the (a, b) / (b, a) results must actually differ for
+    some pairs so pass 2 is exercised."""
+    from taxi2_amd._native import tri_pairs
+
+    fam = family_sequences(20, 700, 0x51, ancestors=3, max_sub=0.05, indel_rate=0.02)
+    rng = np.random.default_rng(5)
+    seqs = []
+    for k, s in enumerate(fam):
+        s = s[: 500 + int(rng.integers(0, 200))]
+        if k % 4 == 1:
+            s = s[:100] + s[100:160].lower() + s[160:]
+        if k % 5 == 2:
+            b = bytearray(s.encode())
+            for pos in rng.integers(0, len(b), 6):
+                b[pos] = ord("NRYKM"[int(rng.integers(0, 5))])
+            s = b.decode()
+        seqs.append(s)
+    seqs += ["ACGT" * 255 + "ACG", "A"]  # 1023 (capacity limit) and 1
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    a, b = tri_pairs(n)
+    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"]):
+        got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
+        two, tsc = _with_env("TAXI2_NO_ALIGN1", "1",
+                             lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
+        exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
+        assert np.array_equal(gsc, esc) and np.array_equal(tsc, esc)
+        assert_metrics_equal(got, exp)
+        assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(two, nan=9.0))
+        asym = ~np.all(np.isclose(np.nan_to_num(exp[:, 0]), np.nan_to_num(exp[:, 1])), axis=1)
+        assert asym.sum() > 0
+    # rectangular (one ordered orientation only), longer query than reference: swapped rows
+    qs = engine.upload(seqs[:6], align=True)
+    rs = engine.upload([s[:300] for s in seqs[6:14]], align=True)
+    got = engine.rect_pairs(qs, rs, 0, 6, METRICS, SCORE_SETS["default"])
+    allseq = seqs[:6] + [s[:300] for s in seqs[6:14]]
+    pa = np.repeat(np.arange(6), 8)
+    pb = np.tile(np.arange(8), 6) + 6
+    exp, _ = oracle_c.batch(allseq, pa, pb, align=True, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp[:, 0, :])
+    for s in (st, qs, rs):
+        s.free()

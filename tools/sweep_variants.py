@@ -4,6 +4,7 @@ process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).  Every vari
 compared bit-for-bit with the first variant's.
 
 usage: python tools/sweep_variants.py [--batch 131072] [--rounds 3] [--len 1000] K,W,OCC ...
+(K,W,OCC = single-orientation kernel shape; o:K,W,OCC = two-orientation kernel shape)
 """
 
 from __future__ import annotations
@@ -52,7 +53,12 @@ def main() -> None:
     times = {v: [] for v in args.variants}
     for rnd in range(args.rounds):
         for v in args.variants:
-            os.environ["TAXI2_VARIANT"] = v
+            if v.startswith("o:"):  # two-orientation kernel
+                os.environ["TAXI2_NO_ALIGN1"] = "1"
+                os.environ["TAXI2_VARIANT"] = v[2:]
+            else:  # single-orientation kernel (sequences <= 1023)
+                os.environ.pop("TAXI2_NO_ALIGN1", None)
+                os.environ["TAXI2_VARIANT1"] = v
             k0 = (rnd * 7919 * B) % (args.nseq * (args.nseq - 1) // 2 - B)
             eng.all_pairs_dev(st, k0, B, metrics, out.data_ptr(), sc, sco.data_ptr(), stream.cuda_stream)
             e0 = torch.cuda.Event(enable_timing=True)
