@@ -157,15 +157,31 @@ __device__ __forceinline__ void ring_get(const RingEntry1* e, S1Left& s) {
     s.y.w1 = b.y;
 }
 
+// Per-lane column constants.  The LUT (two uses per cell) and the equality fields stay in
+// VGPRs; the once-per-cell constants live in LDS (ColC, [k][thread]) so that K = 8 fits the
+// 128-VGPR budget of occupancy 4 without spilling: LDS reads issue on the LDS pipe, not the
+// (saturated) VALU.
 template <int K>
 struct LaneCols1 {
     uint32_t lut[K];  // w0 units by row base: valid bit r, ts bit 10+r, tv bit 20+r;
                       // bit 14 (= A1_GAP): an x-gap in column j lies in y's nucleotide span;
                       // column byte << 24
-    uint32_t ynk[K];  // A1_GAP if y[j-1] is a nucleotide
-    int ox[K], ex[K]; // doubled Ix open / extend (end-gap scores on column nB)
     uint32_t eqp0, eqp1, eqp2, eqp3;  // 3-bit field per column: 4 where the byte is "ACGT"[r]
 };
+struct ColC {
+    uint32_t yn;  // A1_GAP if y[j-1] is a nucleotide
+    int ox;       // doubled Ix open (end-gap open on column nB)
+};
+
+// Dynamic LDS of k_align1: [uint32 xinfo[xcap]] [RingEntry1 ring[W-1][RING]]
+// [ColC colc[K][64W]] [int colex[K][64W] (non-default scores: Ix extend)]
+__host__ __device__ inline size_t a1_lds_ring_off(int xcap) { return ((size_t)xcap * 4 + 15) / 16 * 16; }
+__host__ __device__ inline size_t a1_lds_colc_off(int xcap, int W) {
+    return a1_lds_ring_off(xcap) + (size_t)(W - 1) * RING * sizeof(RingEntry1);
+}
+__host__ __device__ inline size_t a1_lds_bytes(int xcap, int K, int W, bool def) {
+    return a1_lds_colc_off(xcap, W) + (size_t)K * 64 * W * (sizeof(ColC) + (def ? 0 : sizeof(int)));
+}
 
 // xinfo[i-1] (LDS) for row i: byte | base code << 8 (0..3; >= 4 not a nucleotide) |
 // exact "ACGT" code << 11 (4 = other byte) | (x-gap row in x's span) << 14 | nucleotide << 15
@@ -178,7 +194,8 @@ __device__ __forceinline__ uint32_t a1_xinfo(uint32_t c, int i, int fx, int lx) 
 
 template <int K, int W, bool DEF, bool B, bool FIRST>
 __device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col (&st)[K], S1Left& pay, S1Best& carry,
-                                         const LaneCols1<K>& lc, const uint32_t* __restrict__ xinfo,
+                                         const LaneCols1<K>& lc, const ColC* __restrict__ colc,
+                                         const int* __restrict__ colex, const uint32_t* __restrict__ xinfo,
                                          const RingEntry1* __restrict__ ring_in, RingEntry1* __restrict__ ring_out,
                                          const KScores& sc) {
     constexpr bool TRACK = !B;
@@ -218,8 +235,9 @@ __device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col (&st)[K]
             const uint32_t e = (eq >> (3 * k)) & 7u;
             const int sM = DEF ? sc.mi + (int)e : (e ? sc.ma : sc.mi);
             const uint32_t inc = (lc.lut[k] >> xsh) & incm;
-            d = s1_cell<B, TRACK>(d, st[k], l, sM, inc, lc.lut[k] & gxrow, lc.ynk[k] & gyrow, lc.ox[k], lc.ex[k],
-                                  oy, ey);
+            const ColC cc = colc[k * 64 * W];
+            const int ex = DEF ? sc.ie : colex[k * 64 * W];
+            d = s1_cell<B, TRACK>(d, st[k], l, sM, inc, lc.lut[k] & gxrow, cc.yn & gyrow, cc.ox, ex, oy, ey);
         }
         pay = l;
         if (W > 1 && ring_out != nullptr && lane == 63) ring_put(ring_out + (i & (RING - 1)), pay);
@@ -236,25 +254,35 @@ __device__ __forceinline__ void a1_write(double* o, const MetricSpec& ms, C2 c) 
 // Pass 1 (B = false): every pair of `ps` in orientation A (rows = the shorter sequence);
 // writes A's slot, and B's slot too when A's path has no divergent tie, else appends the pair
 // to wlist.  Pass 2 (B = true): the pairs of wlist[0, *wcount) in orientation B, B's slot.
-// Dynamic LDS: [uint32 xinfo[xcap]] [RingEntry1 ring[W-1][RING]]
 template <int K, int W, bool DEF, int OCC, bool B>
 __global__ void __launch_bounds__(64 * W, OCC)
 k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xcap, int out_mode,
          double* __restrict__ out, int32_t* __restrict__ sout, uint32_t* __restrict__ wlist,
-         uint32_t* __restrict__ wcount) {
+         uint32_t* __restrict__ wcount, unsigned long long* __restrict__ next) {
     static_assert(K <= A1_MAX_K, "equality fields hold at most 10 columns");
     const KScores sc0 = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
     const KScores sc = doubled(sc0);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* xinfo = reinterpret_cast<uint32_t*>(smem);
-    RingEntry1* rings = reinterpret_cast<RingEntry1*>(smem + ((size_t)xcap * 4 + 15) / 16 * 16);
+    RingEntry1* rings = reinterpret_cast<RingEntry1*>(smem + a1_lds_ring_off(xcap));
+    ColC* colc = reinterpret_cast<ColC*>(smem + a1_lds_colc_off(xcap, W)) + threadIdx.x;
+    int* colex = reinterpret_cast<int*>(reinterpret_cast<ColC*>(smem + a1_lds_colc_off(xcap, W)) + K * 64 * W) +
+                 threadIdx.x;
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int nm = ms.n;
     const int64_t total = B ? (int64_t)*wcount : ps.count;
+    __shared__ int64_t s_next;
 
-    for (int64_t q = blockIdx.x; q < total; q += gridDim.x) {
+    // Persistent workgroups pull pairs from a device counter: the per-lane prologue runs once
+    // per workgroup, and ragged lengths balance dynamically.
+    for (;;) {
+        __syncthreads();  // previous pair is done with xinfo / rings / s_next
+        if (threadIdx.x == 0) s_next = (int64_t)atomicAdd(next, 1ull);
+        __syncthreads();
+        const int64_t q = s_next;
+        if (q >= total) break;
         const int64_t p = B ? (int64_t)wlist[q] : q;
         int64_t a, b;
         decode_pair(ps, p, a, b);
@@ -294,7 +322,6 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
             continue;
         }
 
-        __syncthreads();  // previous pair is done with xinfo / rings
         for (int i = threadIdx.x; i < nA; i += 64 * W) xinfo[i] = a1_xinfo(rseq[i], i, fx, lx);
         __syncthreads();
 
@@ -326,9 +353,8 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
                 if (j - 1 >= fy && j <= ly) l |= A1_GAP;
             }
             lc.lut[k] = l;
-            lc.ynk[k] = yn;
-            lc.ox[k] = (j == nB) ? sc.eo : sc.io;
-            lc.ex[k] = (j == nB) ? sc.ee : sc.ie;
+            colc[k * 64 * W] = ColC{yn, (j == nB) ? sc.eo : sc.io};
+            if (!DEF) colex[k * 64 * W] = (j == nB) ? sc.ee : sc.ie;
         }
 
         S1Col st[K];
@@ -350,10 +376,10 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
             if (W == 1 || (blk >= 0 && blk < nblk)) {
                 if (w == 0) {
                     for (int s = s0; s < s1; ++s)
-                        dp_step1<K, W, DEF, B, true>(s, lane, nA, st, pay, carry, lc, xinfo, ring_in, ring_out, sc);
+                        dp_step1<K, W, DEF, B, true>(s, lane, nA, st, pay, carry, lc, colc, colex, xinfo, ring_in, ring_out, sc);
                 } else {
                     for (int s = s0; s < s1; ++s)
-                        dp_step1<K, W, DEF, B, false>(s, lane, nA, st, pay, carry, lc, xinfo, ring_in, ring_out, sc);
+                        dp_step1<K, W, DEF, B, false>(s, lane, nA, st, pay, carry, lc, colc, colex, xinfo, ring_in, ring_out, sc);
                 }
             }
             if (W > 1) __syncthreads();

@@ -202,13 +202,14 @@ struct Variant1 {
     bool def;
     const void* fn[2];  // pass 1 (orientation A + divergence flag), pass 2 (orientation B)
     void (*launch[2])(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int,
-                      int, double*, int32_t*, uint32_t*, uint32_t*);
+                      int, double*, int32_t*, uint32_t*, uint32_t*, unsigned long long*);
 };
 
 template <int K, int W, bool DEF, int OCC, bool B>
 void launch_align1(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc,
-                   MetricSpec ms, int xcap, int om, double* out, int32_t* so, uint32_t* wl, uint32_t* wc) {
-    hipLaunchKernelGGL((k_align1<K, W, DEF, OCC, B>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so, wl, wc);
+                   MetricSpec ms, int xcap, int om, double* out, int32_t* so, uint32_t* wl, uint32_t* wc,
+                   unsigned long long* nx) {
+    hipLaunchKernelGGL((k_align1<K, W, DEF, OCC, B>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so, wl, wc, nx);
 }
 
 #define T2_VARIANT1(K, W, DEF, OCC)                                                                   \
@@ -255,23 +256,26 @@ const Variant1* pick_variant1(const KScores& k, int max_len) {
 int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
                         hipStream_t st, int xcap) {
-    const size_t lds = ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(v.W - 1) * RING * sizeof(RingEntry1);
+    const size_t lds = a1_lds_bytes(xcap, v.K, v.W, v.def);
     if (lds > 160 * 1024) return fail(ctx, "LDS requirement %zu exceeds 160 KiB", lds);
     if (lds > 64 * 1024)
         for (const void* fn : v.fn)
             HIP_TRY(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, ((size_t)ps.count + 1) * 4)) return -1;
+    // d_work: [u32 worklist count, pad] [u64 pass-1 cursor] [u64 pass-2 cursor] [u32 worklist...]
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32 + (size_t)ps.count * 4)) return -1;
     uint32_t* wcount = (uint32_t*)ctx->d_work;
-    uint32_t* wlist = wcount + 1;
-    HIP_TRY(ctx, hipMemsetAsync(wcount, 0, 4, st));
-    const int64_t grid1 = std::min<int64_t>(ps.count, (int64_t)1 << 30);
-    v.launch[0](dim3((unsigned)grid1), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
-                d_out, d_scores, wlist, wcount);
+    unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
+    uint32_t* wlist = (uint32_t*)((char*)ctx->d_work + 32);
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 32, st));
+    // persistent grids: the workgroups resident at the variant's occupancy (pairs are pulled from
+    // a device cursor; pass 2's length is known only on the device)
+    const int64_t resident = (int64_t)ctx->num_cus * std::max(1, 4 * v.occ / v.W);
+    const int64_t grid = std::min<int64_t>(ps.count, resident);
+    v.launch[0](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
+                d_out, d_scores, wlist, wcount, next);
     HIP_TRY(ctx, hipGetLastError());
-    // pass 2 walks the worklist with a resident-size grid (its length is known only on the device)
-    const int64_t grid2 = std::min<int64_t>(ps.count, (int64_t)ctx->num_cus * 16);
-    v.launch[1](dim3((unsigned)grid2), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
-                d_out, nullptr, wlist, wcount);
+    v.launch[1](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
+                d_out, nullptr, wlist, wcount, next + 1);
     HIP_TRY(ctx, hipGetLastError());
     if (getenv("TAXI2_A1_STATS")) {  // diagnostics: share of pairs re-run in orientation B
         uint32_t n2 = 0;

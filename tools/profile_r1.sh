@@ -6,7 +6,7 @@
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/prof_r1
+OUT=$R/gpurun_out/${PROF_NAME:-prof_r1}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
@@ -14,11 +14,11 @@ timeout -k 10 420 python3 $R/bench.py --steps 5 --warmup 1 > $OUT/bench.json 2> 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/trace_bench.json 2> $OUT/trace.err &&
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
-    --kernel-include-regex k_align --output-format csv -d $OUT/pmc_valu -o run -- \
+    --kernel-include-regex "k_align" --output-format csv -d $OUT/pmc_valu -o run -- \
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_valu.err &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_align --output-format csv -d $OUT/pmc_fetch -o run -- \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_align" --output-format csv -d $OUT/pmc_fetch -o run -- \
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_align --output-format csv -d $OUT/pmc_write -o run -- \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_align" --output-format csv -d $OUT/pmc_write -o run -- \
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err
 rc=$?
 echo "profile rc=$rc"
