@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_r1.sh run into profiles/: kernel stats + per-launch HBM traffic.
+
+usage: python tools/pmc_summary.py gpurun_out/prof_a1 profiles/r1 --tag align1
+
+Writes <dst>/kernel_stats_<tag>.csv, <dst>/pmc_{valu,fetch,write}_<tag>.csv, <dst>/bench_<tag>.json
+and profiles/pmc_traffic.json (read by bench.py for roofline.traffic): FETCH_SIZE + WRITE_SIZE (KB,
+separate rocprofv3 --pmc passes over one bench launch) summed over the path's kernels, x 1024.
+"""
+
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import shutil
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def counters(path: Path) -> dict[str, dict[str, float]]:
+    out: dict[str, dict[str, float]] = defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0]
+        out[name][r["Counter_Name"]] = out[name].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--batch", type=int, default=524288)
+    args = ap.parse_args()
+    src, dst = Path(args.src), Path(args.dst)
+    dst.mkdir(parents=True, exist_ok=True)
+    shutil.copy(src / "trace/run_kernel_stats.csv", dst / f"kernel_stats_{args.tag}.csv")
+    for k in ("valu", "fetch", "write"):
+        shutil.copy(src / f"pmc_{k}/run_counter_collection.csv", dst / f"pmc_{k}_{args.tag}.csv")
+    shutil.copy(src / "bench.json", dst / f"bench_{args.tag}.json")
+    fetch = counters(src / "pmc_fetch/run_counter_collection.csv")
+    write = counters(src / "pmc_write/run_counter_collection.csv")
+    kernels = sorted(set(fetch) | set(write))
+    per = {k: {"fetch_kb": fetch.get(k, {}).get("FETCH_SIZE", 0.0), "write_kb": write.get(k, {}).get("WRITE_SIZE", 0.0)}
+           for k in kernels}
+    total_kb = sum(v["fetch_kb"] + v["write_kb"] for v in per.values())
+    rec = {
+        "workload": "config3",
+        "batch": args.batch,
+        "kernels": per,
+        "hbm_bytes_per_launch": total_kb * 1024.0,
+        "source": f"profiles/{dst.name}/pmc_fetch_{args.tag}.csv, pmc_write_{args.tag}.csv",
+        "note": "FETCH_SIZE + WRITE_SIZE (KB) x 1024 from separate rocprofv3 --pmc passes over one launch of the "
+                "bench command (--steps 1 --warmup 0), summed over the path's kernels (single-orientation pass 1 "
+                "+ pass 2).  The reads are byte gathers of sequence rows (not the 16-B/lane stream the gfx950 "
+                "FETCH_SIZE x2 correction is calibrated for), so FETCH_SIZE is reported uncorrected; consecutive "
+                "pairs share their first sequence, so most reads hit L2.",
+    }
+    (ROOT / "profiles/pmc_traffic.json").write_text(json.dumps(rec, indent=1) + "\n")
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
