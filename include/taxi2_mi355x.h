@@ -141,6 +141,23 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
                         int64_t count, const taxi2_scores* sc, int both, int32_t cap, uint8_t* out_x,
                         uint8_t* out_y, int32_t* out_len);
 
+/* ---- NCD (distances.py:351-358 NCD._calculate -> alfpy 1.0.6 ncd.Distance) ---------------- *
+ * NCD(x, y) = (C(X+Y) - min(C(X), C(Y))) / max(C(X), C(Y)), X / Y = upper-cased strings,
+ * C(s) = len(zlib.compress(s)) with zlib 1.2.11 level 6 (computed exactly on the GPU).
+ * For each pair k: out[k*no] = value of the ordered pair (x, y) and, when both != 0 (no = 2),
+ * out[k*2+1] = value of (y, x).  With scores (ALIGN sets): x, y are the first Biopython
+ * alignment's gapped strings of that ordered pair, as VersusAll feeds them to the metric
+ * (versus_all.py:532, 546-552); scores == NULL: the sequences as stored.  Raw sequences must
+ * satisfy len(x) + len(y) <= 16382 (one deflate block). */
+int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
+                    int64_t count, const taxi2_scores* sc, int both, double* out);
+
+/* ---- compressed length (alfpy ncd.complexity) --------------------------------------------- *
+ * out[k] = len(zlib.compress(upper(x[xs[k]]) + upper(y[ys[k]]))), zlib 1.2.11 level 6;
+ * ys == NULL compresses x[xs[k]] alone.  Inputs up to 16382 bytes. */
+int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
+                       int64_t count, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,11 @@ Parity anchors:
     ``itaxotools.calculate_distances`` 0.1.1 (third-party Rust, absent); semantics inferred and
     pinned by ``tests/test_distances/metrics.tsv`` (26 rows x 4 metrics) and
     ``tests/test_distances.py:515-521`` (``tests/golden/metric_tests.json``).
+  * ``ncd``                  <- ``src/itaxotools/taxi2/distances.py:351-358`` calling alfpy 1.0.6
+    ``ncd.Distance(SeqRecords((0, 1), (x, y))).pairwise_distance(0, 1)`` (third-party, absent;
+    restated: SeqRecords upper-cases, complexity = len(zlib.compress(s.encode())), default level).
+    zlib itself is this interpreter's zlib 1.2.11 -- the same library alfpy calls.  No reference
+    test pins an NCD value: parity for NCD is pinned to zlib 1.2.11's own output only.
 
 Pure-Python loops: use it for small cases only (golden vectors, < ~300 bp pairs).
 """
@@ -260,3 +265,18 @@ def aligned_counts(x: str, y: str, scores: Scores = Scores()) -> tuple[Counts, C
 
 
 METRICS = ("p", "p-gaps", "jc", "k2p")
+
+
+# --------------------------------------------------------------------------- A9
+def complexity(s: str) -> int:
+    """alfpy ``ncd.complexity``: size of the zlib-compressed (default level) encoded string."""
+    import zlib
+
+    return len(zlib.compress(s.encode()))
+
+
+def ncd(x: str, y: str) -> float:
+    """alfpy ``ncd.Distance.pairwise_distance`` on ``SeqRecords`` (upper-cased) x, y."""
+    X, Y = x.upper(), y.upper()
+    c1, c2, c12 = float(complexity(X)), float(complexity(Y)), float(complexity(X + Y))
+    return (c12 - min(c1, c2)) / max(c1, c2)

@@ -38,6 +38,8 @@ EXPORTS = (
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
+    "taxi2_ncd_pairs",
+    "taxi2_zlib_lengths",
 )
 
 MODE_PREALIGNED = 0
@@ -83,6 +85,8 @@ _SIGNATURES = {
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
     "taxi2_align_strings": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _INT, _I32, _P, _P, _P]),
+    "taxi2_ncd_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P, _INT, _P]),
+    "taxi2_zlib_lengths": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P]),
 }
 
 _lib = None
@@ -365,6 +369,45 @@ class Engine:
             )
         return idx, d, ex, mat
 
+
+    def ncd_pairs(self, x: SeqSet, y: SeqSet, xs, ys, scores=None, *, aligned: bool = True, both: bool = True):
+        """NCD (distances.py:351-358) per pair: (count, 2) [(x, y), (y, x)] when ``both``, else (count,).
+        ALIGN sets with ``aligned``: on the first alignment's gapped strings of each ordered pair
+        (the strings VersusAll hands the metric); otherwise on the stored sequences."""
+        xs = np.ascontiguousarray(xs, dtype=np.int64)
+        ys = np.ascontiguousarray(ys, dtype=np.int64)
+        if xs.shape != ys.shape:
+            raise ValueError("xs and ys must have the same length")
+        count = len(xs)
+        out = np.empty((count, 2) if both else (count,), dtype=np.float64)
+        use_aln = aligned and x.aligned
+        cs = to_cscores(scores)
+        if count:
+            with self._lock:
+                self._check(
+                    self._lib.taxi2_ncd_pairs(
+                        self._ctx, x.id, y.id, xs.ctypes.data, ys.ctypes.data, count,
+                        ctypes.byref(cs) if use_aln else None, 1 if both else 0, out.ctypes.data,
+                    ),
+                    "taxi2_ncd_pairs",
+                )
+        return out
+
+    def zlib_lengths(self, x: SeqSet, xs, y: SeqSet | None = None, ys=None) -> np.ndarray:
+        """len(zlib.compress(upper(x[xs[k]]) (+ upper(y[ys[k]])))) per k (zlib 1.2.11, level 6)."""
+        xs = np.ascontiguousarray(xs, dtype=np.int64)
+        yarr = None if ys is None else np.ascontiguousarray(ys, dtype=np.int64)
+        out = np.empty(len(xs), dtype=np.int32)
+        if len(xs):
+            with self._lock:
+                self._check(
+                    self._lib.taxi2_zlib_lengths(
+                        self._ctx, x.id, (y or x).id, xs.ctypes.data,
+                        yarr.ctypes.data if yarr is not None else None, len(xs), out.ctypes.data,
+                    ),
+                    "taxi2_zlib_lengths",
+                )
+        return out
 
     def align_strings(self, x: SeqSet, y: SeqSet, xs, ys, scores=None, *, both: bool = False):
         """Gapped alignment strings: list of (ax, ay) per pair, plus the (y, x) alignment written

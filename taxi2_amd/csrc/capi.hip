@@ -15,6 +15,7 @@
 #include "../../include/taxi2_mi355x.h"
 #include "align1_kernel.hpp"
 #include "align_kernel.hpp"
+#include "ncd_kernels.hpp"
 #include "common.hpp"
 #include "pack_kernels.hpp"
 #include "prealigned_kernel.hpp"
@@ -52,6 +53,9 @@ struct taxi2_ctx {
     size_t d_aux_bytes = 0;
     void* d_work = nullptr;  // single-orientation aligner: [count][worklist...]
     size_t d_work_bytes = 0;
+    void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
+    void* d_zslabs = nullptr;
+    int64_t z_threads = 0;
 };
 
 namespace {
@@ -359,6 +363,124 @@ int run_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, PairSrc base, co
     return 0;
 }
 
+
+int check_pair_indices(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
+                       int64_t count) {
+    for (int64_t k = 0; k < count; ++k)
+        if (xs[k] < 0 || xs[k] >= X.n || ys[k] < 0 || ys[k] >= Y.n)
+            return fail(ctx, "pair %lld index out of bounds", (long long)k);
+    return 0;
+}
+
+// Aligned strings on the device (k_trace_fill + k_traceback), chunked: slots [chunk][2][cap] for
+// x and for y, right-aligned, plus lengths [chunk][2].
+struct Tracer {
+    uint16_t* d_trace = nullptr;
+    int4* d_ends = nullptr;
+    int64_t* d_idx = nullptr;
+    uint8_t* d_out = nullptr;
+    int32_t* d_len = nullptr;
+    int64_t chunk = 0, stride = 0;
+    int K = 8, W = 1, xcap = 1, cap = 0;
+    size_t lds = 0;
+    KScores k{};
+    bool lin = false;
+
+    ~Tracer() {
+        if (d_trace) (void)hipFree(d_trace);
+        if (d_ends) (void)hipFree(d_ends);
+        if (d_idx) (void)hipFree(d_idx);
+        if (d_out) (void)hipFree(d_out);
+        if (d_len) (void)hipFree(d_len);
+    }
+
+    int setup(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const KScores& ks, int cap_) {
+        if (X.mode != TAXI2_MODE_ALIGN || Y.mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need ALIGN sets");
+        const int max_len = std::max(X.max_len, Y.max_len);
+        if (max_len > 4095) return fail(ctx, "sequence length %d exceeds 4095", max_len);
+        k = ks;
+        lin = is_linear(k);
+        cap = cap_;
+        if (max_len <= 256) K = 4, W = 1;
+        else if (max_len <= 512) W = 1;
+        else if (max_len <= 1024) W = 2;
+        else if (max_len <= 2048) W = 4;
+        else W = 8;
+        xcap = std::max(max_len, 1);
+        lds = ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(W - 1) * RING * sizeof(RingEntry);
+        stride = (int64_t)(xcap + 63) * 64 * W * K;  // u16 per pair
+        chunk = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 30) / (stride * 2)));
+        HIP_TRY(ctx, hipMalloc(&d_trace, (size_t)chunk * stride * 2));
+        HIP_TRY(ctx, hipMalloc(&d_ends, (size_t)chunk * sizeof(int4)));
+        HIP_TRY(ctx, hipMalloc(&d_idx, (size_t)chunk * 2 * sizeof(int64_t)));
+        HIP_TRY(ctx, hipMalloc(&d_out, (size_t)chunk * 2 * cap * 2));
+        HIP_TRY(ctx, hipMalloc(&d_len, (size_t)chunk * 2 * sizeof(int32_t)));
+        if (K == 8 && W == 8 && lds > 64 * 1024)
+            HIP_TRY(ctx, hipFuncSetAttribute(lin ? (const void*)&k_trace_fill<8, 8, true>
+                                                 : (const void*)&k_trace_fill<8, 8, false>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        return 0;
+    }
+
+    // pairs (xs[0..n), ys[0..n)) host indices, n <= chunk; stream-ordered, no synchronisation
+    int run(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys, int64_t n,
+            int both) {
+        HIP_TRY(ctx, hipMemcpyAsync(d_idx, xs, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_idx + chunk, ys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        const dim3 grid((unsigned)n), block(64 * W);
+#define T2_FILL(KK, WW, LIN)                                                                         \
+    hipLaunchKernelGGL((k_trace_fill<KK, WW, LIN>), grid, block, lds, ctx->stream, view(X), view(Y), d_idx, \
+                       d_idx + chunk, n, k, xcap, d_trace, d_ends)
+        if (K == 4) {
+            if (lin) T2_FILL(4, 1, true); else T2_FILL(4, 1, false);
+        } else if (W == 1) {
+            if (lin) T2_FILL(8, 1, true); else T2_FILL(8, 1, false);
+        } else if (W == 2) {
+            if (lin) T2_FILL(8, 2, true); else T2_FILL(8, 2, false);
+        } else if (W == 4) {
+            if (lin) T2_FILL(8, 4, true); else T2_FILL(8, 4, false);
+        } else {
+            if (lin) T2_FILL(8, 8, true); else T2_FILL(8, 8, false);
+        }
+#undef T2_FILL
+        HIP_TRY(ctx, hipGetLastError());
+        const int64_t threads = n * (both ? 2 : 1);
+        const dim3 g2((unsigned)((threads + 255) / 256));
+        if (lin)
+            hipLaunchKernelGGL(k_traceback<true>, g2, dim3(256), 0, ctx->stream, view(X), view(Y), d_idx, d_idx + chunk,
+                               n, K, W, xcap, d_trace, d_ends, cap, d_out, d_out + chunk * 2 * cap, d_len, both);
+        else
+            hipLaunchKernelGGL(k_traceback<false>, g2, dim3(256), 0, ctx->stream, view(X), view(Y), d_idx,
+                               d_idx + chunk, n, K, W, xcap, d_trace, d_ends, cap, d_out, d_out + chunk * 2 * cap,
+                               d_len, both);
+        HIP_TRY(ctx, hipGetLastError());
+        return 0;
+    }
+};
+
+// Compressed lengths of `n` device stream descriptors (persistent threads, per-thread scratch
+// slabs kept in the context; the head tables are zeroed once at allocation).
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out) {
+    if (n <= 0) return 0;
+    const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 64);
+    const int64_t threads = (want + 63) / 64 * 64;
+    if (ctx->z_threads < threads) {
+        if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
+        if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
+        ctx->d_zheads = nullptr;
+        ctx->d_zslabs = nullptr;
+        ctx->z_threads = 0;
+        HIP_TRY(ctx, hipMalloc(&ctx->d_zheads, (size_t)threads * ZS_HEAD));
+        HIP_TRY(ctx, hipMalloc(&ctx->d_zslabs, (size_t)threads * ZS_SLAB));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_zheads, 0, (size_t)threads * ZS_HEAD, ctx->stream));
+        ctx->z_threads = threads;
+    }
+    hipLaunchKernelGGL(k_zlen, dim3((unsigned)(threads / 64)), dim3(64), 0, ctx->stream, d_st, n,
+                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -404,6 +526,8 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
+    if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
+    if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -663,102 +787,120 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
     DevSet* X = get_set(ctx, set_x);
     DevSet* Y = get_set(ctx, set_y);
     if (!X || !Y) return fail(ctx, "unknown set");
-    if (X->mode != TAXI2_MODE_ALIGN || Y->mode != TAXI2_MODE_ALIGN) return fail(ctx, "align_strings needs ALIGN sets");
     if (!sc) return fail(ctx, "scores required");
     if (count <= 0) return 0;
-    const int max_len = std::max(X->max_len, Y->max_len);
-    if (max_len > 4095) return fail(ctx, "sequence length %d exceeds 4095", max_len);
     if (cap < X->max_len + Y->max_len) return fail(ctx, "cap %d < longest x + longest y", cap);
-    for (int64_t k = 0; k < count; ++k)
-        if (xs[k] < 0 || xs[k] >= X->n || ys[k] < 0 || ys[k] >= Y->n)
-            return fail(ctx, "pair %lld index out of bounds", (long long)k);
-    const KScores k = kscores(sc);
-    const bool lin = is_linear(k);
-    int K = 8, W = 1;
-    if (max_len <= 256) K = 4;
-    else if (max_len <= 512) W = 1;
-    else if (max_len <= 1024) W = 2;
-    else if (max_len <= 2048) W = 4;
-    else W = 8;
-    const int xcap = std::max(max_len, 1);
-    const size_t lds = ((size_t)xcap * 4 + 15) / 16 * 16 + (size_t)(W - 1) * RING * sizeof(RingEntry);
-    const int64_t stride = (int64_t)(xcap + 63) * 64 * W * K;  // u16 per pair
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 30) / (stride * 2)));
+    if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    uint16_t* d_trace = nullptr;
-    int4* d_ends = nullptr;
-    int64_t* d_idx = nullptr;
-    uint8_t* d_out = nullptr;
-    int32_t* d_len = nullptr;
-    int rc = 0;
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(ctx->stream);
-        if (d_trace) (void)hipFree(d_trace);
-        if (d_ends) (void)hipFree(d_ends);
-        if (d_idx) (void)hipFree(d_idx);
-        if (d_out) (void)hipFree(d_out);
-        if (d_len) (void)hipFree(d_len);
-    };
-#define T2_TRY(expr)                                                                          \
-    do {                                                                                      \
-        hipError_t e_ = (expr);                                                               \
-        if (e_ != hipSuccess) {                                                               \
-            rc = fail(ctx, "%s failed: %s", #expr, hipGetErrorString(e_));                    \
-            cleanup();                                                                        \
-            return rc;                                                                        \
-        }                                                                                     \
-    } while (0)
-    T2_TRY(hipMalloc(&d_trace, (size_t)chunk * stride * 2));
-    T2_TRY(hipMalloc(&d_ends, (size_t)chunk * sizeof(int4)));
-    T2_TRY(hipMalloc(&d_idx, (size_t)chunk * 2 * sizeof(int64_t)));
-    T2_TRY(hipMalloc(&d_out, (size_t)chunk * 2 * cap * 2));
-    T2_TRY(hipMalloc(&d_len, (size_t)chunk * 2 * sizeof(int32_t)));
+    Tracer tr;
+    if (tr.setup(ctx, *X, *Y, kscores(sc), cap)) return -1;
+    for (int64_t c0 = 0; c0 < count; c0 += tr.chunk) {
+        const int64_t n = std::min(tr.chunk, count - c0);
+        if (tr.run(ctx, *X, *Y, xs + c0, ys + c0, n, both)) return -1;
+        HIP_TRY(ctx, hipMemcpyAsync(out_x + c0 * 2 * cap, tr.d_out, (size_t)n * 2 * cap, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(out_y + c0 * 2 * cap, tr.d_out + tr.chunk * 2 * cap, (size_t)n * 2 * cap,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(out_len + c0 * 2, tr.d_len, (size_t)n * 2 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return 0;
+}
+
+int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
+                    const taxi2_scores* sc, int both, double* out) {
+    if (!ctx) return -1;
+    DevSet* X = get_set(ctx, set_x);
+    DevSet* Y = get_set(ctx, set_y);
+    if (!X || !Y) return fail(ctx, "unknown set");
+    if (count <= 0) return 0;
+    if (!out || !xs || !ys) return fail(ctx, "null argument");
+    if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
+    const bool aligned = sc != nullptr;
+    // aligned strings are <= nA + nB <= 2 * 4095 each, so a concatenation fits one deflate block;
+    // raw sequences must fit it too
+    if (!aligned && (int64_t)X->max_len + Y->max_len > zl::ZMAX_INPUT)
+        return fail(ctx, "NCD: sequences longer than %d bytes together exceed one deflate block", zl::ZMAX_INPUT);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int no = both ? 2 : 1;
+    const int cap = X->max_len + Y->max_len;
+    Tracer tr;
+    int64_t chunk = (int64_t)1 << 16;
+    if (aligned) {
+        if (tr.setup(ctx, *X, *Y, kscores(sc), std::max(cap, 1))) return -1;
+        chunk = tr.chunk;
+    } else {
+        if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)chunk * 2 * 8)) return -1;
+    }
+    const int64_t nstreams = chunk * no * 3;
+    if (ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)nstreams * (sizeof(ZStream) + 4) + chunk * no * 8))
+        return -1;
+    ZStream* d_st = (ZStream*)ctx->d_out;
+    int32_t* d_c = (int32_t*)(d_st + nstreams);
+    double* d_v = (double*)(((uintptr_t)(d_c + nstreams) + 7) & ~(uintptr_t)7);
     for (int64_t c0 = 0; c0 < count; c0 += chunk) {
         const int64_t n = std::min(chunk, count - c0);
-        T2_TRY(hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
-        T2_TRY(hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
-        const dim3 grid((unsigned)n), block(64 * W);
-#define T2_FILL(KK, WW, LIN)                                                                    \
-    hipLaunchKernelGGL((k_trace_fill<KK, WW, LIN>), grid, block, lds, ctx->stream, view(*X), view(*Y), \
-                       d_idx, d_idx + chunk, n, k, xcap, d_trace, d_ends)
-        if (K == 4) {
-            if (lin) T2_FILL(4, 1, true); else T2_FILL(4, 1, false);
-        } else if (W == 1) {
-            if (lin) T2_FILL(8, 1, true); else T2_FILL(8, 1, false);
-        } else if (W == 2) {
-            if (lin) T2_FILL(8, 2, true); else T2_FILL(8, 2, false);
-        } else if (W == 4) {
-            if (lin) T2_FILL(8, 4, true); else T2_FILL(8, 4, false);
+        const int64_t* d_xs;
+        const int64_t* d_ys;
+        if (aligned) {
+            if (tr.run(ctx, *X, *Y, xs + c0, ys + c0, n, both)) return -1;
+            d_xs = tr.d_idx;
+            d_ys = tr.d_idx + tr.chunk;
         } else {
-            if (lds > 64 * 1024) {
-                T2_TRY(hipFuncSetAttribute(lin ? (const void*)&k_trace_fill<8, 8, true>
-                                               : (const void*)&k_trace_fill<8, 8, false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            }
-            if (lin) T2_FILL(8, 8, true); else T2_FILL(8, 8, false);
+            int64_t* di = (int64_t*)ctx->d_aux;
+            HIP_TRY(ctx, hipMemcpyAsync(di, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(di + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+            d_xs = di;
+            d_ys = di + chunk;
         }
-#undef T2_FILL
-        T2_TRY(hipGetLastError());
-        const int64_t threads = n * (both ? 2 : 1);
-        const dim3 g2((unsigned)((threads + 255) / 256));
-        if (lin)
-            hipLaunchKernelGGL(k_traceback<true>, g2, dim3(256), 0, ctx->stream, view(*X), view(*Y), d_idx,
-                               d_idx + chunk, n, K, W, xcap, d_trace, d_ends, cap, d_out, d_out + chunk * 2 * cap,
-                               d_len, both);
-        else
-            hipLaunchKernelGGL(k_traceback<false>, g2, dim3(256), 0, ctx->stream, view(*X), view(*Y), d_idx,
-                               d_idx + chunk, n, K, W, xcap, d_trace, d_ends, cap, d_out, d_out + chunk * 2 * cap,
-                               d_len, both);
-        T2_TRY(hipGetLastError());
-        T2_TRY(hipMemcpyAsync(out_x + c0 * 2 * cap, d_out, (size_t)n * 2 * cap, hipMemcpyDeviceToHost, ctx->stream));
-        T2_TRY(hipMemcpyAsync(out_y + c0 * 2 * cap, d_out + chunk * 2 * cap, (size_t)n * 2 * cap,
-                              hipMemcpyDeviceToHost, ctx->stream));
-        T2_TRY(hipMemcpyAsync(out_len + c0 * 2, d_len, (size_t)n * 2 * 4, hipMemcpyDeviceToHost, ctx->stream));
-        T2_TRY(hipStreamSynchronize(ctx->stream));
+        const int64_t m = n * no;
+        hipLaunchKernelGGL(k_ncd_streams, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, view(*X),
+                           view(*Y), d_xs, d_ys, n, both, aligned ? tr.d_out : nullptr,
+                           aligned ? tr.d_out + tr.chunk * 2 * tr.cap : nullptr, aligned ? tr.d_len : nullptr,
+                           aligned ? tr.cap : 0, d_st);
+        HIP_TRY(ctx, hipGetLastError());
+        if (launch_zlen(ctx, d_st, m * 3, d_c)) return -1;
+        hipLaunchKernelGGL(k_ncd_finish, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, d_c, m, d_v);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipMemcpyAsync(out + c0 * no, d_v, (size_t)m * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
-#undef T2_TRY
-    cleanup();
-    return rc;
+    return 0;
+}
+
+int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
+                       int32_t* out) {
+    if (!ctx) return -1;
+    DevSet* X = get_set(ctx, set_x);
+    DevSet* Y = ys ? get_set(ctx, set_y) : X;
+    if (!X || !Y) return fail(ctx, "unknown set");
+    if (count <= 0) return 0;
+    if (!out || !xs) return fail(ctx, "null argument");
+    for (int64_t k = 0; k < count; ++k) {
+        if (xs[k] < 0 || xs[k] >= X->n || (ys && (ys[k] < 0 || ys[k] >= Y->n)))
+            return fail(ctx, "stream %lld index out of bounds", (long long)k);
+    }
+    if ((int64_t)X->max_len + (ys ? Y->max_len : 0) > zl::ZMAX_INPUT)
+        return fail(ctx, "zlib lengths: inputs longer than %d bytes exceed one deflate block", zl::ZMAX_INPUT);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int64_t chunk = (int64_t)1 << 18;
+    if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)chunk * 2 * 8)) return -1;
+    if (ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)chunk * (sizeof(ZStream) + 4))) return -1;
+    ZStream* d_st = (ZStream*)ctx->d_out;
+    int32_t* d_c = (int32_t*)(d_st + chunk);
+    int64_t* di = (int64_t*)ctx->d_aux;
+    for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+        const int64_t n = std::min(chunk, count - c0);
+        HIP_TRY(ctx, hipMemcpyAsync(di, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (ys) HIP_TRY(ctx, hipMemcpyAsync(di + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_zlen_streams, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, view(*X),
+                           view(*Y), di, ys ? di + chunk : nullptr, n, d_st);
+        HIP_TRY(ctx, hipGetLastError());
+        if (launch_zlen(ctx, d_st, n, d_c)) return -1;
+        HIP_TRY(ctx, hipMemcpyAsync(out + c0, d_c, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return 0;
 }
 
 }  // extern "C"

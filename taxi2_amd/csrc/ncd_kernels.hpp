@@ -1,0 +1,106 @@
+// NCD on the GPU (TaxI2 distances.py:351-358 -> alfpy 1.0.6 ncd.Distance.pairwise_distance):
+//   NCD(x, y) = (C(X + Y) - min(C(X), C(Y))) / max(C(X), C(Y)),  X = x.upper(), Y = y.upper(),
+//   C(s) = len(zlib.compress(s))  (zlib 1.2.11, level 6; deflate_len.hpp).
+// x, y are what VersusAll hands the metric: the Biopython aligned strings of the ordered pair in
+// align mode (versus_all.py:532 -> :546), the raw sequences otherwise.
+//
+// One thread per compressed stream: the lazy-match parse is a serial chain walk per byte, so the
+// work unit is the stream, not the byte.  Each thread owns a zeroed 64 KiB hash-head table and a
+// window / prev / tree scratch slab in HBM (the head table is cleaned per stream, never re-zeroed).
+#pragma once
+#include "common.hpp"
+#include "deflate_len.hpp"
+
+namespace taxi2 {
+
+struct ZStream {
+    const uint8_t* a;
+    const uint8_t* b;
+    int32_t na, nb;
+};
+
+// Per-thread scratch slab after the head tables: [window][prev][Trees]
+constexpr size_t ZS_WIN = ((size_t)zl::WIN_BYTES + 255) / 256 * 256;
+constexpr size_t ZS_PREV = (size_t)zl::WSIZE * 2;
+constexpr size_t ZS_TREES = (sizeof(zl::Trees) + 255) / 256 * 256;
+constexpr size_t ZS_SLAB = ZS_WIN + ZS_PREV + ZS_TREES;
+constexpr size_t ZS_HEAD = (size_t)zl::HASH_SIZE * 2;
+
+__global__ void __launch_bounds__(64)
+k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, uint8_t* __restrict__ slabs,
+       int32_t* __restrict__ out) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    uint8_t* slab = slabs + tid * ZS_SLAB;
+    zl::Scratch z{slab, reinterpret_cast<uint16_t*>(slab + ZS_WIN), heads + tid * zl::HASH_SIZE};
+    zl::Trees* t = reinterpret_cast<zl::Trees*>(slab + ZS_WIN + ZS_PREV);
+    for (int64_t s = tid; s < n; s += nthreads) {
+        const ZStream d = st[s];
+        out[s] = zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t);
+    }
+}
+
+// Three streams per (pair, orientation): C(first), C(second), C(first + second).
+// Orientation 0 = ordered pair (x, y); 1 = (y, x).  Aligned mode reads the traceback slots
+// (ax / ay right-aligned in [0, nA + nB) of slot p*2 + o; orientation 1 holds (bx, by) in (x, y)
+// column order, and the (y, x) metric sees (by, bx)).
+__global__ void __launch_bounds__(256)
+k_ncd_streams(SetView XS, SetView YS, const int64_t* __restrict__ xs, const int64_t* __restrict__ ys, int64_t n,
+              int both, const uint8_t* __restrict__ ax, const uint8_t* __restrict__ ay,
+              const int32_t* __restrict__ alen, int cap, ZStream* __restrict__ st) {
+    const int no = both ? 2 : 1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * no) return;
+    const int64_t p = t / no;
+    const int o = (int)(t % no);
+    const int64_t a = xs[p], b = ys[p];
+    const uint8_t *sx, *sy;
+    int32_t lx, ly;
+    if (ax != nullptr) {
+        const int total = XS.meta[a].x + YS.meta[b].x;
+        const int32_t len = alen[p * 2 + o];
+        const int64_t off = (p * 2 + o) * (int64_t)cap + (total - len);
+        sx = ax + off;
+        sy = ay + off;
+        lx = ly = len;
+    } else {
+        sx = XS.bytes + XS.offs[a];
+        sy = YS.bytes + YS.offs[b];
+        lx = XS.meta[a].x;
+        ly = YS.meta[b].x;
+    }
+    const uint8_t* f = o ? sy : sx;
+    const uint8_t* s = o ? sx : sy;
+    const int32_t lf = o ? ly : lx, ls = o ? lx : ly;
+    ZStream* d = st + t * 3;
+    d[0] = ZStream{f, nullptr, lf, 0};
+    d[1] = ZStream{s, nullptr, ls, 0};
+    d[2] = ZStream{f, s, lf, ls};
+}
+
+__global__ void __launch_bounds__(256)
+k_ncd_finish(const int32_t* __restrict__ c, int64_t m, double* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    const double c1 = c[t * 3], c2 = c[t * 3 + 1], c12 = c[t * 3 + 2];
+    const double mn = c1 < c2 ? c1 : c2, mx = c1 < c2 ? c2 : c1;
+    out[t] = (c12 - mn) / mx;
+}
+
+// Raw-mode streams for taxi2_zlib_lengths: upper(x_a) (+ upper(y_b) when ys != nullptr).
+__global__ void __launch_bounds__(256)
+k_zlen_streams(SetView XS, SetView YS, const int64_t* __restrict__ xs, const int64_t* __restrict__ ys, int64_t n,
+               ZStream* __restrict__ st) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int64_t a = xs[t];
+    ZStream d{XS.bytes + XS.offs[a], nullptr, XS.meta[a].x, 0};
+    if (ys != nullptr) {
+        const int64_t b = ys[t];
+        d.b = YS.bytes + YS.offs[b];
+        d.nb = YS.meta[b].x;
+    }
+    st[t] = d;
+}
+
+}  // namespace taxi2

@@ -8,7 +8,8 @@
   :func:`calculate_many`, one engine call for any number of pairs.
 * Writers ``DistanceHandler.Linear`` / ``Matrix`` / ``Linear.WithExtras`` reproduce the
   reference's tab-separated formats (``distances.py:34-279``, fixtures under tests/golden).
-* NCD / BBC are labels only for now: the engine does not compute them.
+* NCD (``distances.py:351-358`` -> alfpy 1.0.6 ``ncd``) runs on the GPU with zlib-1.2.11-exact
+  compressed lengths (``taxi2_ncd_pairs``); BBC is a label only (out of scope).
 """
 
 from __future__ import annotations
@@ -96,10 +97,11 @@ class Kimura2P(DistanceMetric):
 
 
 class NCD(DistanceMetric):
-    label = "ncd"
+    """alfpy 1.0.6 ``ncd.Distance(SeqRecords((0, 1), (x, y))).pairwise_distance(0, 1)``
+    (``distances.py:351-358``): (C(X+Y) - min(C(X), C(Y))) / max(C(X), C(Y)) with X, Y the
+    upper-cased strings and C = len(zlib.compress(.)) -- computed by the engine."""
 
-    def _calculate(self, x: str, y: str):
-        raise NotImplementedError("NCD is not computed by the MI355X engine yet (DESIGN.md §Next)")
+    label = "ncd"
 
 
 class BBC(DistanceMetric):
@@ -121,18 +123,27 @@ class BBC(DistanceMetric):
         raise NotImplementedError("BBC is out of scope for the MI355X engine (SURVEY.md §2 row 4)")
 
 
-ENGINE_LABELS = ("p", "p-gaps", "jc", "k2p")
+COUNTER_LABELS = ("p", "p-gaps", "jc", "k2p")  # alignment-column counters (one kernel pass)
+ENGINE_LABELS = COUNTER_LABELS + ("ncd",)
 
 
 def engine_metric(metric: DistanceMetric) -> bool:
     return str(metric) in ENGINE_LABELS
 
 
+def check_ncd_strings(strings) -> None:
+    """The engine compresses the stored bytes; the reference compresses ``str.upper().encode()``
+    (UTF-8).  Both agree on ASCII, so non-ASCII input is refused instead of silently differing."""
+    for s in strings:
+        if not s.isascii():
+            raise ValueError("NCD on the MI355X engine needs ASCII sequences")
+
+
 def calculate_many(metrics: Iterable[DistanceMetric], xs: list[str], ys: list[str], *, engine=None) -> np.ndarray:
     """Pre-aligned distances for pairs (xs[k], ys[k]): (count, M) float64, NaN/inf = None.
 
-    One engine call for the whole batch; replaces ``count x M`` Rust calls
-    (``distances.py:323-347``)."""
+    One engine call per kind of metric for the whole batch; replaces ``count x M`` Rust / alfpy
+    calls (``distances.py:323-358``)."""
     from ._native import Engine
 
     metrics = list(metrics)
@@ -143,9 +154,21 @@ def calculate_many(metrics: Iterable[DistanceMetric], xs: list[str], ys: list[st
         raise ValueError("xs and ys differ in length")
     eng = engine or Engine.default()
     n = len(xs)
+    labels = [str(m) for m in metrics]
+    out = np.empty((n, len(labels)))
+    cidx = [k for k, lab in enumerate(labels) if lab != "ncd"]
+    nidx = [k for k, lab in enumerate(labels) if lab == "ncd"]
+    if nidx:
+        check_ncd_strings(xs)
+        check_ncd_strings(ys)
     s = eng.upload(list(xs) + list(ys), align=False)
     try:
-        out = eng.list_pairs(s, s, np.arange(n), np.arange(n) + n, [str(m) for m in metrics])
+        if cidx:
+            out[:, cidx] = eng.list_pairs(s, s, np.arange(n), np.arange(n) + n, [labels[k] for k in cidx])
+        if nidx:
+            v = eng.ncd_pairs(s, s, np.arange(n), np.arange(n) + n, aligned=False, both=False)
+            for k in nidx:
+                out[:, k] = v
     finally:
         s.free()
     return out

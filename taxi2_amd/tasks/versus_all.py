@@ -28,13 +28,11 @@ from typing import Callable
 import numpy as np
 
 from ..align import PairwiseAligner, Scores
-from ..distances import Distance, DistanceHandler, DistanceMetric
+from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric, check_ncd_strings
 from ..pairs import SequencePair, SequencePairHandler
 from ..sequences import Sequences
 from ..types import AttrDict
 from .common import Results, console_report, create_parents, format_values, report, seq_key
-
-ENGINE_LABELS = ("p", "p-gaps", "jc", "k2p")
 
 
 class VersusAll:
@@ -127,6 +125,9 @@ class VersusAll:
 
         labels = [str(m) for m in self.params.distances.metrics]
         M = len(labels)
+        cidx = [k for k, lab in enumerate(labels) if lab != "ncd"]  # counter metrics
+        nidx = [k for k, lab in enumerate(labels) if lab == "ncd"]
+        clabels = [labels[k] for k in cidx]
         align = bool(self.params.pairs.align)
         scores = Scores(**(self.params.pairs.scores or {})).as_tuple()
         n = len(seqs)
@@ -134,30 +135,40 @@ class VersusAll:
         total = M * n * n
         if n == 0:
             return D
+        if nidx:
+            check_ncd_strings(s.seq for s in seqs)
         eng = self._engine()
         st = eng.upload([s.seq for s in seqs], align=align)
         try:
             npairs = n * (n - 1) // 2
-            per = 2 * M if align else M
 
             def compute(k0: int, count: int) -> np.ndarray:
-                out = np.empty((count, per))
-                step = max(1, (1 << 20) if align else (1 << 24))
+                """Unordered pairs [k0, k0 + count) -> (count, 2 * M): (a, b) row then (b, a) row."""
+                out = np.empty((count, 2, M))
+                step = (1 << 20) if align else (1 << 24)
+                if nidx:
+                    step = min(step, 1 << 16)
                 for c0 in range(0, count, step):
                     c = min(step, count - c0)
-                    blk = eng.all_pairs(st, k0 + c0, c, labels, scores)
-                    out[c0 : c0 + c] = blk.reshape(c, per)
+                    if cidx:
+                        blk = eng.all_pairs(st, k0 + c0, c, clabels, scores)
+                        if align:
+                            out[c0 : c0 + c][:, :, cidx] = blk
+                        else:  # counters are symmetric: one value serves both ordered rows
+                            out[c0 : c0 + c][:, 0, cidx] = blk
+                            out[c0 : c0 + c][:, 1, cidx] = blk
+                    if nidx:
+                        a, b = tri_pairs(n, k0 + c0, c)
+                        v = eng.ncd_pairs(st, st, a, b, scores, aligned=align, both=True)
+                        for k in nidx:
+                            out[c0 : c0 + c][:, :, k] = v
                     report(self.progress_handler, "distance.x.id", min(total, 2 * M * (k0 + c0 + c)), total)
-                return out
+                return out.reshape(count, 2 * M)
 
             res = self._run_pairs(n, npairs, compute)
             a, b = tri_pairs(n)
-            if align:
-                D[a, b] = res[:, :M]
-                D[b, a] = res[:, M:]
-            else:
-                D[a, b] = res
-                D[b, a] = res
+            D[a, b] = res[:, :M]
+            D[b, a] = res[:, M:]
             # diagonal rule on full tuples: identical (id, seq, extras) -> None unless the
             # alignment of the sequence with itself is not the identity (non-default scores)
             groups: dict = {}
@@ -167,7 +178,13 @@ class VersusAll:
             if align:
                 reps = np.array([g[0] for g in dup], dtype=np.int64)
                 strings = eng.align_strings(st, st, reps, reps, scores)
-                self_vals = eng.list_pairs(st, st, reps, reps, labels, scores)[:, 0, :]
+                self_vals = np.empty((len(reps), M))
+                if cidx:
+                    self_vals[:, cidx] = eng.list_pairs(st, st, reps, reps, clabels, scores)[:, 0, :]
+                if nidx:
+                    v = eng.ncd_pairs(st, st, reps, reps, scores, aligned=True, both=False)
+                    for k in nidx:
+                        self_vals[:, k] = v
             for gi, g in enumerate(dup):
                 if align and strings[gi][0] != strings[gi][1]:
                     for i in g:

@@ -9,7 +9,9 @@
 and writes ``distances/<metric>.linear.tsv``, ``distances/<metric>.matricial.tsv``,
 ``closest.tsv`` and (``params.pairs.write``) ``aligned_pairs.txt``.
 Argmin runs on the GPU (``taxi2_closest``), so the Q x R block never round-trips through
-Python unless a writer needs it.
+Python unless a writer needs it.  With NCD as the primary metric the Q x R NCD block comes from
+``taxi2_ncd_pairs`` and the same first-minimum rule runs on the host; NCD as an extra metric is
+computed for the closest pairs only.
 """
 
 from __future__ import annotations
@@ -21,12 +23,24 @@ from typing import Callable
 import numpy as np
 
 from ..align import PairwiseAligner, Scores
-from ..distances import Distance, DistanceHandler, DistanceMetric
+from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric, check_ncd_strings
 from ..pairs import SequencePair, SequencePairHandler
 from ..types import AttrDict
 from .common import Results, console_report, create_parents, format_values, report
 
-ENGINE_LABELS = ("p", "p-gaps", "jc", "k2p")
+
+def first_minimum(block: np.ndarray, scale: float) -> tuple[np.ndarray, np.ndarray]:
+    """Per row: index of the first minimum of ``scale * v`` over finite values (the reference's
+    ``min`` over Distances after the x100 adjustment, versus_reference.py:184-188, 232) and the
+    unscaled value; -1 / NaN for rows without a defined value (same contract as taxi2_closest)."""
+    v = block * scale
+    ok = np.isfinite(v)
+    w = np.where(ok, v, np.inf)
+    i = np.argmin(w, axis=1) if block.shape[1] else np.zeros(block.shape[0], dtype=np.int64)
+    has = ok.any(axis=1)
+    idx = np.where(has, i, -1).astype(np.int64)
+    d = np.where(has, block[np.arange(block.shape[0]), np.maximum(idx, 0)], np.nan)
+    return idx, d
 
 
 class VersusReference:
@@ -109,6 +123,12 @@ class VersusReference:
         want_matrix = bool(self.params.distances.write_linear or self.params.distances.write_matricial)
         total = Q * R
         eng = self._engine()
+        ncd_primary = str(primary) == "ncd"
+        ncd_extra = [k for k, m in enumerate(extras) if str(m) == "ncd"]
+        cextra = [k for k, m in enumerate(extras) if str(m) != "ncd"]
+        if ncd_primary or ncd_extra:
+            check_ncd_strings(s.seq for s in data)
+            check_ncd_strings(s.seq for s in refs)
         qs = eng.upload([s.seq for s in data], align=align)
         rs = eng.upload([s.seq for s in refs], align=align)
         try:
@@ -117,17 +137,40 @@ class VersusReference:
             ext = np.full((Q, len(extras)), np.nan)
             mat = np.full((Q, R), np.nan) if want_matrix else None
             step = max(1, (1 << 22) // max(R, 1))
+            if ncd_primary:
+                step = max(1, (1 << 16) // max(R, 1))
             for q0 in range(0, Q, step):
                 q1 = min(Q, q0 + step)
-                if R:
-                    i, d, e, m = eng.closest(qs, rs, q0, q1, str(primary), [str(x) for x in extras] if extras else (),
-                                             scores, scale=100.0 if pct else 1.0, want_matrix=want_matrix)
+                if R and not ncd_primary:
+                    cx = [str(extras[k]) for k in cextra]
+                    i, d, e, m = eng.closest(qs, rs, q0, q1, str(primary), cx, scores,
+                                             scale=100.0 if pct else 1.0, want_matrix=want_matrix)
                     idx[q0:q1], dmin[q0:q1] = i, d
                     if e is not None:
-                        ext[q0:q1] = e
+                        ext[q0:q1, cextra] = e
                     if m is not None:
                         mat[q0:q1] = m
+                elif R:
+                    nq = q1 - q0
+                    qa = np.repeat(np.arange(q0, q1, dtype=np.int64), R)
+                    ra = np.tile(np.arange(R, dtype=np.int64), nq)
+                    block = eng.ncd_pairs(qs, rs, qa, ra, scores, aligned=align, both=False).reshape(nq, R)
+                    i, d = first_minimum(block, 100.0 if pct else 1.0)
+                    idx[q0:q1], dmin[q0:q1] = i, d
+                    if mat is not None:
+                        mat[q0:q1] = block
+                    if cextra:
+                        ok = np.nonzero(i >= 0)[0]
+                        if len(ok):
+                            e = eng.list_pairs(qs, rs, ok + q0, i[ok], [str(extras[k]) for k in cextra], scores)
+                            ext[(ok + q0)[:, None], np.array(cextra)[None, :]] = e[:, 0, :] if align else e
                 report(self.progress_handler, "distance.x.id", q1 * R, total)
+            if ncd_extra:
+                ok = np.nonzero(idx >= 0)[0]
+                if len(ok):
+                    v = eng.ncd_pairs(qs, rs, ok, idx[ok], scores, aligned=align, both=False)
+                    for k in ncd_extra:
+                        ext[ok, k] = v
         finally:
             qs.free()
             rs.free()

@@ -1,0 +1,157 @@
+"""GPU: NCD (distances.py:351-358) against the oracle (Python zlib 1.2.11 + the alignment
+restatement), per pair, through both tasks."""
+
+from __future__ import annotations
+
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+from tests.seqgen import family_sequences, mutate, random_sequences
+
+pytestmark = pytest.mark.gpu
+
+DEFAULT = (1, -1, -8, -1, -1, -1)
+
+
+def test_zlib_lengths_exact(engine):
+    rng = random.Random(21)
+    seqs = []
+    for L in (0, 1, 2, 3, 7, 64, 500, 1000, 3000, 8000):
+        for alpha in ("ACGT", "ACGTN-", "acgtNRYKM", "AC"):
+            seqs.append("".join(rng.choice(alpha) for _ in range(L)))
+    seqs += family_sequences(6, 1000, 5, ancestors=2)
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    got1 = engine.zlib_lengths(st, np.arange(n))
+    exp1 = [len(zlib.compress(s.upper().encode())) for s in seqs]
+    assert got1.tolist() == exp1
+    xs = np.array([rng.randrange(n) for _ in range(200)])
+    ys = np.array([rng.randrange(n) for _ in range(200)])
+    got2 = engine.zlib_lengths(st, xs, st, ys)
+    exp2 = [len(zlib.compress((seqs[a] + seqs[b]).upper().encode())) for a, b in zip(xs, ys)]
+    assert got2.tolist() == exp2
+    st.free()
+
+
+def test_ncd_pairs_raw_both_orders(engine):
+    from oracle import restatement as R
+
+    base = random_sequences(10, 50, 900, 4, "ACGTN", n_rate=0.03)
+    seqs = base + [s.lower() for s in mutate(base, 5, rate=0.1)] + ["", "-A-C-"]
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    rng = random.Random(2)
+    xs = np.array([rng.randrange(n) for _ in range(120)])
+    ys = np.array([rng.randrange(n) for _ in range(120)])
+    got = engine.ncd_pairs(st, st, xs, ys, aligned=False, both=True)
+    for k, (a, b) in enumerate(zip(xs, ys)):
+        assert got[k, 0] == R.ncd(seqs[a], seqs[b])
+        assert got[k, 1] == R.ncd(seqs[b], seqs[a])
+    st.free()
+
+
+@pytest.mark.parametrize("scores", [DEFAULT, (2, -3, -5, -2, -1, -1), (1, -1, -2, -2, -1, -1)])
+def test_ncd_pairs_aligned_both_orders(engine, scores):
+    """On the gapped strings of the first alignment of each ordered pair (the strings VersusAll
+    hands the metric)."""
+    from oracle import restatement as R
+
+    base = random_sequences(6, 20, 140, 8, "ACGT", n_rate=0.02)
+    seqs = [R.normalize(s) for s in base + mutate(base, 9, rate=0.15)]
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    xs = np.repeat(np.arange(n), n)
+    ys = np.tile(np.arange(n), n)
+    got = engine.ncd_pairs(st, st, xs, ys, scores, aligned=True, both=True)
+    sc = R.Scores(*scores)
+    for k, (a, b) in enumerate(zip(xs, ys)):
+        ax, ay, _ = R.align(seqs[a], seqs[b], sc)
+        by, bx, _ = R.align(seqs[b], seqs[a], sc)
+        assert got[k, 0] == R.ncd(ax, ay), (a, b)
+        assert got[k, 1] == R.ncd(by, bx), (a, b)
+    st.free()
+
+
+def test_ncd_metric_calculate(engine):
+    from oracle import restatement as R
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequence
+
+    x, y = Sequence("a", "gg-ccnccta" * 7), Sequence("b", "GGACCACCAA" * 7)
+    d = DistanceMetric.NCD().calculate(x, y)
+    assert d.metric == DistanceMetric.NCD() and d.d == R.ncd(x.seq, y.seq)
+
+
+@pytest.mark.parametrize("align", [True, False])
+def test_versus_all_with_ncd(tmp_path, engine, oracle_c, align):
+    from oracle import restatement as R
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    raw = random_sequences(5, 40, 120, 31, "ACGTN", n_rate=0.05)
+    raw = raw + mutate(raw[:3], 32, rate=0.1)
+    seqs = [Sequence(f"s{k}", s, {"voucher": str(k)}) for k, s in enumerate(raw)]
+    seqs.append(Sequence("s0", raw[0], {"voucher": "0"}))  # duplicate tuple -> None row/col
+    task = VersusAll()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input.sequences = Sequences(seqs)
+    task.params.pairs.align = align
+    task.params.pairs.write = False
+    task.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.NCD()]
+    work = [s.normalize() for s in seqs] if align else seqs
+    D = task.compute_distances(work)
+    n = len(work)
+    for i in range(n):
+        for j in range(n):
+            same = (work[i].id, work[i].seq, work[i].extras) == (work[j].id, work[j].seq, work[j].extras)
+            if same and (not align or R.align(work[i].seq, work[j].seq)[0] == R.align(work[i].seq, work[j].seq)[1]):
+                assert np.isnan(D[i, j]).all()
+                continue
+            if align:
+                ax, ay, _ = R.align(work[i].seq, work[j].seq)
+            else:
+                ax, ay = work[i].seq, work[j].seq
+            assert D[i, j, 1] == R.ncd(ax, ay), (i, j)
+            p = R.metric("p", ax, ay)
+            assert (np.isnan(D[i, j, 0]) and p is None) or D[i, j, 0] == p
+    task.start()
+    assert (tmp_path / "out/distances/matricial/ncd.tsv").exists()
+
+
+def test_versus_reference_ncd_primary_and_extra(tmp_path, engine):
+    from oracle import restatement as R
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusReference
+
+    q = random_sequences(6, 40, 110, 41, "ACGT")
+    r = mutate(q[:4], 42, rate=0.2) + random_sequences(3, 40, 110, 43, "ACGT")
+    for primary, extras in ((DistanceMetric.NCD(), [DistanceMetric.Uncorrected()]),
+                            (DistanceMetric.Uncorrected(), [DistanceMetric.NCD(), DistanceMetric.JukesCantor()])):
+        task = VersusReference()
+        task.engine = engine
+        task.progress_handler = None
+        task.work_dir = tmp_path / f"out_{primary}"
+        task.input.data = Sequences([Sequence(f"q{k}", s) for k, s in enumerate(q)])
+        task.input.reference = Sequences([Sequence(f"r{k}", s) for k, s in enumerate(r)])
+        task.params.pairs.write = False
+        task.params.distances.metric = primary
+        task.params.distances.extra_metrics = list(extras)
+        task.start()
+        for qi, ri, d, ext in task.closest:
+            vals = []
+            for rj in range(len(r)):
+                ax, ay, _ = R.align(R.normalize(q[qi]), R.normalize(r[rj]))
+                vals.append(R.ncd(ax, ay) if str(primary) == "ncd" else R.metric("p", ax, ay))
+            ok = [v for v in vals if v is not None]
+            assert ri == vals.index(min(ok)) and d == min(ok)
+            ax, ay, _ = R.align(R.normalize(q[qi]), R.normalize(r[ri]))
+            for k, m in enumerate(task.params.distances.extra_metrics):
+                exp = R.ncd(ax, ay) if str(m) == "ncd" else R.metric(str(m), ax, ay)
+                assert (exp is None and np.isnan(ext[k])) or ext[k] == exp

@@ -1,0 +1,85 @@
+"""NCD: zlib-1.2.11-exact compressed lengths and the alfpy formula.
+
+CPU: the product's deflate-length header compiled for the host vs Python's zlib.compress (the
+same zlib 1.2.11 alfpy calls); the oracle restatement; labels.  No reference test pins an NCD
+value: parity is pinned to zlib's own output.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import random
+import shutil
+import subprocess
+import zlib
+
+import pytest
+
+from tests.conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def zlen_host(tmp_path_factory):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    out = tmp_path_factory.mktemp("zlen") / "libzlen_host.so"
+    subprocess.run([gxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(out),
+                    str(ROOT / "tests/native/zlen_host.cpp")], check=True)
+    lib = ctypes.CDLL(str(out))
+    lib.zlen_host.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    lib.zlen_host.restype = ctypes.c_int
+    return lambda a, b=b"": lib.zlen_host(a, len(a), b, len(b))
+
+
+def _inputs(seed: int, n: int):
+    rng = random.Random(seed)
+    alphabets = [b"ACGT", b"ACGTN-", b"AC", b"ACGTacgtNRYKM-", bytes(range(65, 91)), bytes(range(32, 127)),
+                 bytes(range(0, 256))]
+    for _ in range(n):
+        L = rng.choice([0, 1, 2, 3, 5, 10, 50, 300, 1000, 2500, 6000])
+        alpha = rng.choice(alphabets)
+        a = bytes(rng.choice(alpha) for _ in range(L))
+        kind = rng.randrange(3)
+        if kind == 0:
+            yield a, b""
+        elif kind == 1:
+            b = bytearray(a)
+            for i in range(len(b)):
+                if rng.random() < 0.1:
+                    b[i] = rng.choice(alpha)
+            yield a, bytes(b)
+        else:
+            unit = a[: rng.randint(1, 40)] or b"A"
+            yield (unit * (L // len(unit) + 1))[:L], a[: L // 2]
+
+
+def test_deflate_len_matches_zlib(zlen_host):
+    bad = [(len(a), len(b)) for a, b in _inputs(11, 600) if zlen_host(a, b) != len(zlib.compress((a + b).upper()))]
+    assert not bad, bad[:10]
+
+
+def test_deflate_len_block_limit(zlen_host):
+    big = bytes(random.Random(3).choice(b"ACGT") for _ in range(16382))
+    assert zlen_host(big) == len(zlib.compress(big))
+    assert zlen_host(big[:16381], b"G") == len(zlib.compress(big[:16381] + b"G"))
+    assert zlen_host(big + b"A") == -1  # more than one deflate block: refused, not approximated
+
+
+def test_oracle_ncd_formula():
+    from oracle import restatement as R
+
+    assert R.ncd("", "") == 0.0
+    x, y = "ACGTTGCA" * 20, "acgttgca" * 20
+    assert R.ncd(x, y) == R.ncd(x.lower(), y)  # SeqRecords upper-cases
+    c = [len(zlib.compress(s.encode())) for s in (x, y.upper(), x + y.upper())]
+    assert R.ncd(x, y) == (c[2] - min(c[0], c[1])) / max(c[0], c[1])
+
+
+def test_ncd_label_is_an_engine_metric():
+    from taxi2_amd.distances import ENGINE_LABELS, DistanceMetric, check_ncd_strings
+
+    assert "ncd" in ENGINE_LABELS
+    assert isinstance(DistanceMetric.fromLabel("ncd"), DistanceMetric.NCD)
+    with pytest.raises(ValueError):
+        check_ncd_strings(["ACGT", "ACGé"])
