@@ -204,7 +204,12 @@ class SeqSet:
 
 
 class Engine:
-    """One engine context per GPU (one process per GPU for multi-GPU runs)."""
+    """One engine context per GPU (one process per GPU for multi-GPU runs).
+
+    Mixing with PyTorch in one process: import torch BEFORE the first Engine.  torch ships its own
+    libamdhip64.so.7 (same soname as /opt/rocm's); whichever loads first serves the whole process,
+    and torch only initialises its devices on the runtime it was built with.  Loaded that way the
+    engine and torch share one runtime, so torch stream handles can be passed to the *_dev calls."""
 
     _default: dict[int, "Engine"] = {}
 
