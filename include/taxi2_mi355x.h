@@ -158,6 +158,19 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
 int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                        int64_t count, int32_t* out);
 
+/* ---- writer text (distances.py:59-279 DistanceHandler.Linear[.WithExtras] / .Matrix) ------- *
+ * Text rows of a float table vals[nrows][ncols][nm] (host, f64; NaN/inf -> `missing`), every
+ * value as Python "%.{decimals}f" % v (= "{:.Nf}".format(v): correctly rounded, ties to even,
+ * "-0.0000" kept); |v| * 10^decimals < 2^63 for finite v.
+ *   mode 0 (linear): per row r, per column c:  row_pre[r] TAB col_pre[c] (TAB value){nm} LF
+ *   mode 1 (matrix): per row r:                row_pre[r] (TAB value[r][c]){ncols} LF   (nm = 1)
+ * row_pre / col_pre: concatenated UTF-8 bytes, offsets [n + 1].  Writes out[0, *out_len);
+ * returns 1 without writing when cap < *out_len (retry with that capacity). */
+int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
+                      const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                      const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                      uint8_t* out, int64_t cap, int64_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,7 @@ EXPORTS = (
     "taxi2_align_strings",
     "taxi2_ncd_pairs",
     "taxi2_zlib_lengths",
+    "taxi2_format_rows",
 )
 
 MODE_PREALIGNED = 0
@@ -87,6 +88,8 @@ _SIGNATURES = {
     "taxi2_align_strings": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _INT, _I32, _P, _P, _P]),
     "taxi2_ncd_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P, _INT, _P]),
     "taxi2_zlib_lengths": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P]),
+    "taxi2_format_rows": (_INT, [_P, _INT, _P, _I64, _I64, _INT, _P, _P, _P, _P, _INT, _P, _I32, _P, _I64,
+                                 ctypes.POINTER(_I64)]),
 }
 
 _lib = None
@@ -413,6 +416,51 @@ class Engine:
                     "taxi2_zlib_lengths",
                 )
         return out
+
+    def format_rows(self, vals: np.ndarray, row_pre, col_pre=None, *, decimals: int = 4,
+                    missing: str = "NA") -> bytes:
+        """Writer text (taxi2_format_rows): ``vals`` (nrows, ncols, nm) -> linear rows
+        ``row_pre TAB col_pre (TAB value){nm} LF`` per cell; (nrows, ncols) with ``col_pre=None``
+        -> matrix rows ``row_pre (TAB value){ncols} LF``.  Values as Python "%.{decimals}f"."""
+        v = np.ascontiguousarray(vals, dtype=np.float64)
+        mode = 0 if col_pre is not None else 1
+        if mode == 1 and v.ndim == 2:
+            v = v[:, :, None]
+        if v.ndim != 3:
+            raise ValueError("vals must be (nrows, ncols, nm) (linear) or (nrows, ncols) (matrix)")
+        nrows, ncols, nm = v.shape
+
+        def pack(strings):
+            enc = [s.encode("utf-8") for s in strings]
+            offs = np.zeros(len(enc) + 1, dtype=np.int64)
+            if enc:
+                offs[1:] = np.cumsum([len(e) for e in enc])
+            return np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8), offs
+
+        rb, ro = pack(row_pre)
+        if len(ro) != nrows + 1:
+            raise ValueError("one row prefix per row")
+        cb, co = pack(col_pre) if mode == 0 else (None, None)
+        if mode == 0 and len(co) != ncols + 1:
+            raise ValueError("one column prefix per column")
+        miss = missing.encode("utf-8")
+        need = _I64(0)
+        cap = max(1, nrows * ncols * (nm * (decimals + 8) + 4) + int(ro[-1]) * ncols
+                  + (int(co[-1]) * nrows if mode == 0 else 0))
+        for _ in range(2):
+            out = np.empty(cap, dtype=np.uint8)
+            with self._lock:
+                rc = self._lib.taxi2_format_rows(
+                    self._ctx, mode, v.ctypes.data, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data,
+                    cb.ctypes.data if cb is not None else None, co.ctypes.data if co is not None else None,
+                    int(decimals), miss, len(miss), out.ctypes.data, cap, ctypes.byref(need),
+                )
+            if rc == 1:
+                cap = int(need.value)
+                continue
+            self._check(rc, "taxi2_format_rows")
+            return out[: need.value].tobytes()
+        raise NativeError("taxi2_format_rows: output size changed between calls")
 
     def align_strings(self, x: SeqSet, y: SeqSet, xs, ys, scores=None, *, both: bool = False):
         """Gapped alignment strings: list of (ax, ay) per pair, plus the (y, x) alignment written

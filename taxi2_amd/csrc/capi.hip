@@ -16,6 +16,7 @@
 #include "align1_kernel.hpp"
 #include "align_kernel.hpp"
 #include "ncd_kernels.hpp"
+#include "format_kernels.hpp"
 #include "common.hpp"
 #include "pack_kernels.hpp"
 #include "prealigned_kernel.hpp"
@@ -53,6 +54,8 @@ struct taxi2_ctx {
     size_t d_aux_bytes = 0;
     void* d_work = nullptr;  // single-orientation aligner: [count][worklist...]
     size_t d_work_bytes = 0;
+    void* d_fmt = nullptr;  // text formatter staging
+    size_t d_fmt_bytes = 0;
     void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
     void* d_zslabs = nullptr;
     int64_t z_threads = 0;
@@ -465,7 +468,8 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out) 
     const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 64);
     const int64_t threads = (want + 63) / 64 * 64;
     if (ctx->z_threads < threads) {
-        if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
+        if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
+    if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
         if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
         ctx->d_zheads = nullptr;
         ctx->d_zslabs = nullptr;
@@ -526,6 +530,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
+    if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
     if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
     if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -900,6 +905,77 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
         HIP_TRY(ctx, hipMemcpyAsync(out + c0, d_c, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
+    return 0;
+}
+
+int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
+                      const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                      const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                      uint8_t* out, int64_t cap, int64_t* out_len) {
+    if (!ctx) return -1;
+    if (!out_len || (nrows > 0 && (!vals || !row_pre || !row_offs))) return fail(ctx, "null argument");
+    if (mode != 0 && mode != 1) return fail(ctx, "mode must be 0 (linear) or 1 (matrix)");
+    if (mode == 1 && nm != 1) return fail(ctx, "matrix mode formats one metric");
+    if (mode == 0 && (!col_pre || !col_offs)) return fail(ctx, "linear mode needs column prefixes");
+    if (decimals < 0 || decimals > FMT_MAX_DECIMALS) return fail(ctx, "decimals must be in [0, %d]", FMT_MAX_DECIMALS);
+    if (nrows < 0 || ncols < 0 || nm < 1 || missing_len < 0) return fail(ctx, "bad shape");
+    *out_len = 0;
+    if (nrows == 0 || ncols == 0) return 0;
+    const int64_t nv = nrows * ncols * nm;
+    const double lim = std::ldexp(1.0, 63) / (double)pow10_u64(decimals);
+    for (int64_t k = 0; k < nv; ++k)
+        if (std::isfinite(vals[k]) && !(std::fabs(vals[k]) < lim))
+            return fail(ctx, "value %g too large for fixed-point text with %d decimals", vals[k], decimals);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int64_t rp = row_offs[nrows] - row_offs[0];
+    const int64_t cp = mode == 0 ? col_offs[ncols] - col_offs[0] : 0;
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_vals = al(nv * 8), b_roffs = al((nrows + 1) * 8), b_coffs = al((ncols + 1) * 8),
+                 b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nrows * 8);
+    const size_t fixed = b_vals + b_roffs + b_coffs + b_rpre + b_cpre + b_miss + 2 * b_len;
+    if (ensure(ctx, &ctx->d_fmt, &ctx->d_fmt_bytes, fixed)) return -1;
+    char* base = (char*)ctx->d_fmt;
+    double* d_vals = (double*)base;
+    int64_t* d_roffs = (int64_t*)(base + b_vals);
+    int64_t* d_coffs = (int64_t*)((char*)d_roffs + b_roffs);
+    uint8_t* d_rpre = (uint8_t*)d_coffs + b_coffs;
+    uint8_t* d_cpre = d_rpre + b_rpre;
+    uint8_t* d_miss = d_cpre + b_cpre;
+    int64_t* d_rlen = (int64_t*)(d_miss + b_miss);
+    int64_t* d_rbase = (int64_t*)((char*)d_rlen + b_len);
+    std::vector<int64_t> roffs(nrows + 1), coffs(mode == 0 ? ncols + 1 : 1, 0);
+    for (int64_t r = 0; r <= nrows; ++r) roffs[r] = row_offs[r] - row_offs[0];
+    if (mode == 0)
+        for (int64_t c = 0; c <= ncols; ++c) coffs[c] = col_offs[c] - col_offs[0];
+    HIP_TRY(ctx, hipMemcpyAsync(d_vals, vals, nv * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_roffs, roffs.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (rp) HIP_TRY(ctx, hipMemcpyAsync(d_rpre, row_pre + row_offs[0], rp, hipMemcpyHostToDevice, ctx->stream));
+    if (mode == 0) {
+        HIP_TRY(ctx, hipMemcpyAsync(d_coffs, coffs.data(), (ncols + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (cp) HIP_TRY(ctx, hipMemcpyAsync(d_cpre, col_pre + col_offs[0], cp, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (missing_len) HIP_TRY(ctx, hipMemcpyAsync(d_miss, missing, missing_len, hipMemcpyHostToDevice, ctx->stream));
+    FmtArgs a{mode, d_vals, nrows, ncols, nm, decimals, d_rpre, d_roffs, d_cpre, d_coffs, d_miss, missing_len};
+    hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, ctx->stream, a, d_rlen);
+    HIP_TRY(ctx, hipGetLastError());
+    std::vector<int64_t> rlen(nrows), rbase(nrows);
+    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nrows * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int64_t total = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+        rbase[r] = total;
+        total += rlen[r];
+    }
+    *out_len = total;
+    if (total > cap) return 1;  // caller retries with a buffer of *out_len bytes
+    if (!out) return fail(ctx, "null output buffer");
+    if (ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 1)) return -1;
+    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nrows * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_fmt_rows, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, ctx->stream, a, d_rbase,
+                       (char*)ctx->d_out);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }
 

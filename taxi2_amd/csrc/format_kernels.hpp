@@ -1,0 +1,177 @@
+// Text for the distance writers (TaxI2 distances.py:59-279 DistanceHandler.Linear / .WithExtras /
+// .Matrix, fed by versus_all.py:564-603 and versus_reference.py:131-178): every value is
+// formatter.format(d) with formatter "{:.Nf}" (params.format.float = "{:.4f}", handler default
+// "{:f}" = 6 decimals), None -> params.format.missing.
+//
+// fmt_fixed reproduces Python's '%.Nf' exactly: the decimal rounding is decided on the exact binary
+// value (m * 2^e * 10^N, 128-bit integer arithmetic), ties to even, sign kept for -0.0 and for
+// negatives that round to zero ("-0.0000").  Valid for |x| * 10^N < 2^63 (the host checks).
+//
+// Layout of one chunk of rows: one workgroup per row, tokens = the row's columns; token lengths
+// are block-scanned in LDS and each thread writes its token at the row base + its offset.
+//   linear: token (r, c) = row_pre[r] '\t' col_pre[c] ('\t' value(r, c, m)){nm} '\n'
+//   matrix: token (r, c) = [row_pre[r] if c == 0] '\t' value(r, c) ['\n' if c == ncols-1]
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#endif
+
+namespace taxi2 {
+
+constexpr int FMT_MAX_DECIMALS = 17;
+
+__host__ __device__ __forceinline__ uint64_t pow10_u64(int n) {
+    uint64_t p = 1;
+    for (int i = 0; i < n; ++i) p *= 10u;
+    return p;
+}
+
+// Python "%.{N}f" % x for finite x; writes to dst (nullable: length only); returns the length.
+__host__ __device__ inline int fmt_fixed(double x, int N, char* dst) {
+    uint64_t bits;
+    __builtin_memcpy(&bits, &x, 8);
+    const bool neg = (bits >> 63) != 0;
+    const int bexp = (int)((bits >> 52) & 0x7FF);
+    const uint64_t frac = bits & ((1ull << 52) - 1);
+    const uint64_t m = bexp ? (frac | (1ull << 52)) : frac;
+    const int e = bexp ? bexp - 1075 : -1074;
+    const unsigned __int128 P = (unsigned __int128)m * pow10_u64(N);
+    uint64_t q;
+    if (e >= 0) {
+        q = (uint64_t)(P << e);
+    } else {
+        const int s = -e;
+        if (s >= 128) {
+            q = 0;  // P < 2^110 < 2^(s-1): rounds to 0
+        } else {
+            q = (uint64_t)(P >> s);
+            const unsigned __int128 rem = P & ((((unsigned __int128)1) << s) - 1);
+            const unsigned __int128 half = ((unsigned __int128)1) << (s - 1);
+            if (rem > half || (rem == half && (q & 1u))) ++q;
+        }
+    }
+    const uint64_t p10 = pow10_u64(N);
+    uint64_t ip = q / p10;
+    const uint64_t fp = q - ip * p10;
+    char tmp[24];
+    int nd = 0;
+    do {
+        tmp[nd++] = (char)('0' + ip % 10u);
+        ip /= 10u;
+    } while (ip);
+    const int len = (neg ? 1 : 0) + nd + (N > 0 ? 1 + N : 0);
+    if (dst) {
+        int o = 0;
+        if (neg) dst[o++] = '-';
+        while (nd) dst[o++] = tmp[--nd];
+        if (N > 0) {
+            dst[o++] = '.';
+            uint64_t f = fp;
+            for (int k = N - 1; k >= 0; --k) {
+                dst[o + k] = (char)('0' + f % 10u);
+                f /= 10u;
+            }
+        }
+    }
+    return len;
+}
+
+#ifdef __HIPCC__
+struct FmtArgs {
+    int mode;  // 0 linear, 1 matrix
+    const double* vals;  // [nrows][ncols][nm]
+    int64_t nrows, ncols;
+    int nm, decimals;
+    const uint8_t* row_pre;
+    const int64_t* row_offs;  // [nrows + 1] relative to the chunk
+    const uint8_t* col_pre;
+    const int64_t* col_offs;  // [ncols + 1]
+    const uint8_t* missing;
+    int missing_len;
+};
+
+__device__ __forceinline__ bool fmt_defined(double v) { return __builtin_isfinite(v); }
+
+__device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, int64_t c) {
+    const double* v = a.vals + (r * a.ncols + c) * a.nm;
+    int64_t len = 0;
+    if (a.mode == 0) {
+        len = (a.row_offs[r + 1] - a.row_offs[r]) + 1 + (a.col_offs[c + 1] - a.col_offs[c]) + 1;  // + '\n'
+        for (int m = 0; m < a.nm; ++m) len += 1 + (fmt_defined(v[m]) ? fmt_fixed(v[m], a.decimals, nullptr) : a.missing_len);
+    } else {
+        if (c == 0) len += a.row_offs[r + 1] - a.row_offs[r];
+        len += 1 + (fmt_defined(v[0]) ? fmt_fixed(v[0], a.decimals, nullptr) : a.missing_len);
+        if (c == a.ncols - 1) len += 1;
+    }
+    return len;
+}
+
+__device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int64_t c, char* o) {
+    const double* v = a.vals + (r * a.ncols + c) * a.nm;
+    auto put = [&](const uint8_t* s, int64_t n) {
+        for (int64_t k = 0; k < n; ++k) *o++ = (char)s[k];
+    };
+    auto value = [&](double x) {
+        *o++ = '\t';
+        if (fmt_defined(x)) o += fmt_fixed(x, a.decimals, o);
+        else put(a.missing, a.missing_len);
+    };
+    if (a.mode == 0) {
+        put(a.row_pre + a.row_offs[r], a.row_offs[r + 1] - a.row_offs[r]);
+        *o++ = '\t';
+        put(a.col_pre + a.col_offs[c], a.col_offs[c + 1] - a.col_offs[c]);
+        for (int m = 0; m < a.nm; ++m) value(v[m]);
+        *o++ = '\n';
+    } else {
+        if (c == 0) put(a.row_pre + a.row_offs[r], a.row_offs[r + 1] - a.row_offs[r]);
+        value(v[0]);
+        if (c == a.ncols - 1) *o++ = '\n';
+    }
+}
+
+constexpr int FMT_BLOCK = 256;
+
+// Pass 1: total text length of each row.
+__global__ void __launch_bounds__(FMT_BLOCK) k_fmt_row_len(FmtArgs a, int64_t* __restrict__ row_len) {
+    __shared__ int64_t red[FMT_BLOCK];
+    const int64_t r = blockIdx.x;
+    int64_t s = 0;
+    for (int64_t c = threadIdx.x; c < a.ncols; c += FMT_BLOCK) s += fmt_token_len(a, r, c);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = FMT_BLOCK / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) row_len[r] = red[0];
+}
+
+// Pass 2: write; row_base[r] = byte offset of row r in `out`.
+__global__ void __launch_bounds__(FMT_BLOCK)
+k_fmt_rows(FmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out) {
+    __shared__ int64_t scan[FMT_BLOCK];
+    const int64_t r = blockIdx.x;
+    int64_t base = row_base[r];
+    for (int64_t c0 = 0; c0 < a.ncols; c0 += FMT_BLOCK) {
+        const int64_t c = c0 + threadIdx.x;
+        const int64_t len = c < a.ncols ? fmt_token_len(a, r, c) : 0;
+        scan[threadIdx.x] = len;
+        __syncthreads();
+        for (int w = 1; w < FMT_BLOCK; w <<= 1) {  // inclusive Hillis-Steele scan
+            const int64_t add = threadIdx.x >= w ? scan[threadIdx.x - w] : 0;
+            __syncthreads();
+            scan[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (c < a.ncols) fmt_token_write(a, r, c, out + base + scan[threadIdx.x] - len);
+        base += scan[FMT_BLOCK - 1];
+        __syncthreads();
+    }
+}
+#endif
+
+}  // namespace taxi2

@@ -44,6 +44,36 @@ def format_values(vals: np.ndarray, fmt: str, missing: str) -> np.ndarray:
     return out
 
 
+def fixed_decimals(fmt: str) -> int | None:
+    """N for a "{:.Nf}" / "{:f}" formatter (the forms the GPU text formatter reproduces)."""
+    import re
+
+    m = re.fullmatch(r"\{:(?:\.(\d+))?f\}", fmt)
+    if not m:
+        return None
+    n = int(m.group(1)) if m.group(1) is not None else 6
+    return n if n <= 17 else None
+
+
+def gpu_text_ok(vals: np.ndarray, decimals: int | None) -> bool:
+    """True when taxi2_format_rows can format every finite value exactly."""
+    if decimals is None:
+        return False
+    fin = vals[np.isfinite(vals)]
+    return fin.size == 0 or float(np.max(np.abs(fin))) * 10.0 ** decimals < 2.0 ** 62
+
+
+def write_rows_gpu(fh, eng, vals: np.ndarray, row_pre: list, col_pre, decimals: int, missing: str,
+                   max_values: int = 1 << 23) -> None:
+    """Stream writer text (linear when col_pre is given, matrix otherwise) to the binary file
+    ``fh`` in row chunks of about ``max_values`` values."""
+    per_row = max(1, int(np.prod(vals.shape[1:])))
+    step = max(1, max_values // per_row)
+    for r0 in range(0, vals.shape[0], step):
+        r1 = min(vals.shape[0], r0 + step)
+        fh.write(eng.format_rows(vals[r0:r1], row_pre[r0:r1], col_pre, decimals=decimals, missing=missing))
+
+
 def _brace_to_percent(fmt: str) -> str | None:
     import re
 

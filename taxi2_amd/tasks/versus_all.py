@@ -32,7 +32,8 @@ from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric
 from ..pairs import SequencePair, SequencePairHandler
 from ..sequences import Sequences
 from ..types import AttrDict
-from .common import Results, console_report, create_parents, format_values, report, seq_key
+from .common import (Results, console_report, create_parents, fixed_decimals, format_values, gpu_text_ok,
+                     report, seq_key, write_rows_gpu)
 
 
 class VersusAll:
@@ -239,11 +240,17 @@ class VersusAll:
         if n == 0:
             open(self.paths.distances_linear, "w").close()
             return
-        text = format_values(D, fmt, missing)
         ex0 = list(seqs[0].extras.keys())
         head = ["seqid (query)", *[k + " (query)" for k in ex0], "seqid (reference)",
                 *[k + " (reference)" for k in ex0], *[str(m) for m in metrics]]
         pre = ["\t".join([s.id, *[v if v is not None else missing for v in s.extras.values()]]) for s in seqs]
+        dec = fixed_decimals(fmt)
+        if gpu_text_ok(D, dec):  # text formatted on the GPU (taxi2_format_rows)
+            with open(self.paths.distances_linear, "wb") as fh:
+                fh.write(("\t".join(head) + "\n").encode("utf-8"))
+                write_rows_gpu(fh, self._engine(), D, pre, pre, dec, missing)
+            return
+        text = format_values(D, fmt, missing)
         with open(self.paths.distances_linear, "w") as fh:
             fh.write("\t".join(head) + "\n")
             for i in range(n):
@@ -264,6 +271,14 @@ class VersusAll:
                         for j, y in enumerate(seqs):
                             v = D[i, j, m]
                             fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+                continue
+            dec = fixed_decimals(fmt)
+            if gpu_text_ok(D[:, :, m], dec):
+                with open(path, "wb") as fh:
+                    if seqs:
+                        fh.write(("\t".join(["", *ids]) + "\n").encode("utf-8"))
+                        write_rows_gpu(fh, self._engine(), np.ascontiguousarray(D[:, :, m]), ids, None, dec,
+                                       missing)
                 continue
             text = format_values(D[:, :, m], fmt, missing)
             with open(path, "w") as fh:

@@ -26,7 +26,8 @@ from ..align import PairwiseAligner, Scores
 from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric, check_ncd_strings
 from ..pairs import SequencePair, SequencePairHandler
 from ..types import AttrDict
-from .common import Results, console_report, create_parents, format_values, report
+from .common import (Results, console_report, create_parents, fixed_decimals, format_values, gpu_text_ok,
+                     report, write_rows_gpu)
 
 
 def first_minimum(block: np.ndarray, scale: float) -> tuple[np.ndarray, np.ndarray]:
@@ -227,6 +228,24 @@ class VersusReference:
         create_parents(self.paths.distances_linear)
         fmt, missing = self.params.format.float, self.params.format.missing
         metric = self.params.distances.metric
+        dec = fixed_decimals(fmt)
+        qids, rids = [s.id for s in data], [s.id for s in refs]
+        if (data and refs and gpu_text_ok(A, dec) and len(set(qids)) == len(qids) and len(set(rids)) == len(rids)
+                and all(list(s.extras) == list(data[0].extras) for s in data)
+                and all(list(s.extras) == list(refs[0].extras) for s in refs)):
+            # same text as DistanceHandler.Linear.WithExtras (one metric, no line merging), GPU-formatted
+            exq, exr = list(data[0].extras), list(refs[0].extras)
+            head = ["seqid (query)", *[k + " (query)" for k in exq], "seqid (reference)",
+                    *[k + " (reference)" for k in exr], str(metric)]
+
+            def pre(s):
+                return "\t".join([s.id, *[v if v is not None else missing for v in s.extras.values()]])
+
+            with open(self.paths.distances_linear, "wb") as fh:
+                fh.write(("\t".join(head) + "\n").encode("utf-8"))
+                write_rows_gpu(fh, self._engine(), np.ascontiguousarray(A)[:, :, None], [pre(s) for s in data],
+                               [pre(s) for s in refs], dec, missing)
+            return
         with DistanceHandler.Linear.WithExtras(self.paths.distances_linear, "w", missing=missing,
                                                formatter=fmt) as fh:
             for i, x in enumerate(data):
@@ -247,6 +266,12 @@ class VersusReference:
                     for j, y in enumerate(refs):
                         v = A[i, j]
                         fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+            return
+        dec = fixed_decimals(fmt)
+        if data and refs and gpu_text_ok(A, dec):
+            with open(self.paths.distances_matricial, "wb") as fh:
+                fh.write(("\t".join(["", *[s.id for s in refs]]) + "\n").encode("utf-8"))
+                write_rows_gpu(fh, self._engine(), np.ascontiguousarray(A), ids, None, dec, missing)
             return
         text = format_values(A, fmt, missing)
         with open(self.paths.distances_matricial, "w") as fh:
