@@ -1,4 +1,4 @@
-// Single-orientation aligner with a divergence flag (sequences <= 1023, Gotoh scores).
+// Single-orientation aligner with a divergence flag (Gotoh scores, sequences <= 4095).
 //
 // Same fill as align_kernel.hpp (Biopython first-path Gotoh, forward-carried counters,
 // systolic lanes, tie-tagged doubled scores) but each state carries the counters of ONE
@@ -14,10 +14,12 @@
 // are bit-exact; pass 2 typically sees a few percent of the pairs (0 % on the reference's
 // sample files, ~10 % on highly similar synthetic families).
 //
-// Per cell this halves the counter work of the two-orientation kernel (5 selects x 2 words,
+// Per cell this halves the counter work of the two-orientation kernel (5 selects x NW words,
 // one add per move), and the divergent-tie count rides the gap add as the carry-in of one
-// v_addc.  Counter words (lengths <= 1023):  w0 = valid | ts << 10 | tv << 20,
-// w1 = divergent ties | gap << 14 (both <= nA + nB + 1 <= 2047).
+// v_addc.  Counter words, NW = 2 (lengths <= 1023):  w0 = valid | ts << 10 | tv << 20,
+// w1 = divergent ties | gap << 14 (both <= nA + nB + 1 <= 2047).  NW = 3 (lengths <= 4095):
+// w0 = valid | ts << 16, w1 = ties | gap << 14 (<= 8191 each), w2 = tv << 20 (so the row-base LUT
+// bit for tv is already in place: one AND, no shift).
 //
 // The M score uses an equality field instead of a byte compare: per lane, eqp[r] holds for
 // each of its K columns a 3-bit field = 4 where the column byte is "ACGT"[r], so for the usual
@@ -29,112 +31,147 @@
 namespace taxi2 {
 
 constexpr uint32_t A1_GAP = 1u << 14;          // gap unit in w1 (= the x-gap flag bit of the LUT)
-constexpr uint32_t A1_INC_MASK = 0x00100401u;  // valid / ts / tv units in w0
-constexpr int A1_MAX_LEN = 1023;
+constexpr int A1_MAX_LEN = 1023;               // NW = 2 counters
+constexpr int A1_MAX_LEN_LONG = 4095;          // NW = 3 counters
 constexpr int A1_MAX_K = 10;                   // 3-bit equality fields in one word
 
+// Counter words of one orientation; layout per NW above.
+template <int NW>
+struct Cnt {
+    uint32_t w[NW];
+};
+template <int NW>
+__device__ __forceinline__ Cnt<NW> cselw(bool c, const Cnt<NW>& a, const Cnt<NW>& b) {
+    Cnt<NW> r;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) r.w[k] = c ? a.w[k] : b.w[k];
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ Cnt<NW> cnt_zero() {
+    Cnt<NW> r;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) r.w[k] = 0u;
+    return r;
+}
+// w0 units of a diagonal nucleotide column, shifted into place by the row base (LUT bits r, +ts, +tv)
+template <int NW> constexpr uint32_t a1_inc0_mask() { return NW == 2 ? 0x00100401u : 0x00010001u; }
+template <int NW> constexpr int a1_ts_bit() { return NW == 2 ? 10 : 16; }
+
+template <int NW>
 struct S1Col {
     int G;  // 2 * max(M, Iy) + (M won)
-    C2 g;
+    Cnt<NW> g;
     int X;  // 2 * Ix
-    C2 x;
+    Cnt<NW> x;
 };
+template <int NW>
 struct S1Left {
     int F;  // 2 * max(M, Ix) + (M won)
-    C2 f;
+    Cnt<NW> f;
     int Y;  // 2 * Iy
-    C2 y;
+    Cnt<NW> y;
 };
+template <int NW>
 struct S1Best {
     int h;
-    C2 c;
+    Cnt<NW> c;
 };
 
 // Best of a column state (the diagonal successor's source / the final cell).
 // A: G wins iff G > X (tagged);  B: G wins iff G >= X.  Divergent iff G == X.
-template <bool B, bool TRACK>
-__device__ __forceinline__ S1Best s1_best_col(const S1Col& u) {
+template <bool B, bool TRACK, int NW>
+__device__ __forceinline__ S1Best<NW> s1_best_col(const S1Col<NW>& u) {
     const bool take = B ? (u.G >= u.X) : (u.G > u.X);
-    S1Best r{max(u.G, u.X), csel(take, u.g, u.x)};
-    if (TRACK) r.c.w1 += (u.G == u.X) ? 1u : 0u;
+    S1Best<NW> r{max(u.G, u.X), cselw(take, u.g, u.x)};
+    if (TRACK) r.c.w[1] += (u.G == u.X) ? 1u : 0u;
     return r;
 }
 // Best of a left payload.  A: F wins iff F >= Y;  B: iff F > Y.  Divergent iff F == Y.
-template <bool B, bool TRACK>
-__device__ __forceinline__ S1Best s1_best_left(const S1Left& l) {
+template <bool B, bool TRACK, int NW>
+__device__ __forceinline__ S1Best<NW> s1_best_left(const S1Left<NW>& l) {
     const bool take = B ? (l.F > l.Y) : (l.F >= l.Y);
-    S1Best r{max(l.F, l.Y), csel(take, l.f, l.y)};
-    if (TRACK) r.c.w1 += (l.F == l.Y) ? 1u : 0u;
+    S1Best<NW> r{max(l.F, l.Y), cselw(take, l.f, l.y)};
+    if (TRACK) r.c.w[1] += (l.F == l.Y) ? 1u : 0u;
     return r;
 }
 
 // Row 0 / column 0 boundaries on doubled scores d (see g_col_row0 / g_left_row0).
-__device__ __forceinline__ S1Col s1_col_row0(int j, const KScores& d) {
-    S1Col c;
+template <int NW>
+__device__ __forceinline__ S1Col<NW> s1_col_row0(int j, const KScores& d) {
+    S1Col<NW> c;
     c.G = (j == 0) ? 1 : d.eo + d.ee * (j - 1);
     c.X = NEG_INF;
-    c.g = c.x = C2{0u, 0u};
+    c.g = c.x = cnt_zero<NW>();
     return c;
 }
-__device__ __forceinline__ S1Left s1_left_row0(int j, const KScores& d) {
-    S1Left l;
+template <int NW>
+__device__ __forceinline__ S1Left<NW> s1_left_row0(int j, const KScores& d) {
+    S1Left<NW> l;
     l.F = (j == 0) ? 1 : NEG_INF;
     l.Y = (j == 0) ? NEG_INF : d.eo + d.ee * (j - 1);
-    l.f = l.y = C2{0u, 0u};
+    l.f = l.y = cnt_zero<NW>();
     return l;
 }
-__device__ __forceinline__ S1Left s1_shr_first(const S1Left& v, int i, const KScores& d) {
-    S1Left r;
+template <int NW>
+__device__ __forceinline__ S1Left<NW> s1_shr_first(const S1Left<NW>& v, int i, const KScores& d) {
+    S1Left<NW> r;
     r.F = (int)shr_old((uint32_t)v.F, (uint32_t)(d.eo + d.ee * (i - 1)));
     r.Y = (int)shr_old((uint32_t)v.Y, (uint32_t)NEG_INF);
-    r.f.w0 = shr_zero(v.f.w0);
-    r.f.w1 = shr_zero(v.f.w1);
-    r.y.w0 = shr_zero(v.y.w0);
-    r.y.w1 = shr_zero(v.y.w1);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        r.f.w[k] = shr_zero(v.f.w[k]);
+        r.y.w[k] = shr_zero(v.y.w[k]);
+    }
     return r;
 }
-__device__ __forceinline__ S1Left s1_shr_old(const S1Left& v, const S1Left& o) {
-    S1Left r;
+template <int NW>
+__device__ __forceinline__ S1Left<NW> s1_shr_old(const S1Left<NW>& v, const S1Left<NW>& o) {
+    S1Left<NW> r;
     r.F = (int)shr_old((uint32_t)v.F, (uint32_t)o.F);
     r.Y = (int)shr_old((uint32_t)v.Y, (uint32_t)o.Y);
-    r.f.w0 = shr_old(v.f.w0, o.f.w0);
-    r.f.w1 = shr_old(v.f.w1, o.f.w1);
-    r.y.w0 = shr_old(v.y.w0, o.y.w0);
-    r.y.w1 = shr_old(v.y.w1, o.y.w1);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        r.f.w[k] = shr_old(v.f.w[k], o.f.w[k]);
+        r.y.w[k] = shr_old(v.y.w[k], o.y.w[k]);
+    }
     return r;
 }
 
-// One cell in place (see g_cell for the state algebra); inc = valid/ts/tv units of the M move,
-// gx / gy = gap units of the Ix / Iy moves, sM = doubled substitution score.
-template <bool B, bool TRACK>
-__device__ __forceinline__ S1Best s1_cell(const S1Best& d, S1Col& u, S1Left& l, int sM, uint32_t inc,
-                                          uint32_t gx, uint32_t gy, int ox, int ex, int oy, int ey) {
-    const S1Best nd = s1_best_col<B, TRACK>(u);
+// One cell in place (see g_cell for the state algebra); inc0 / inc2 = valid/ts(/tv) units of the
+// M move in w0 / w2 (NW = 3), gx / gy = gap units of the Ix / Iy moves, sM = doubled substitution.
+template <bool B, bool TRACK, int NW>
+__device__ __forceinline__ S1Best<NW> s1_cell(const S1Best<NW>& d, S1Col<NW>& u, S1Left<NW>& l, int sM,
+                                              uint32_t inc0, uint32_t inc2, uint32_t gx, uint32_t gy, int ox,
+                                              int ex, int oy, int ey) {
+    const S1Best<NW> nd = s1_best_col<B, TRACK>(u);
     const int M = (d.h | 1) + sM;
-    const C2 m{d.c.w0 + inc, d.c.w1};
+    Cnt<NW> m = d.c;
+    m.w[0] += inc0;
+    if constexpr (NW == 3) m.w[2] += inc2;
     // Ix from above. A: G-path iff cg > cx;  B: iff cg >= cx.
     const int cg = u.G + ox, cx = u.X + ex;
     const int X = max(cg, cx) & ~1;
-    C2 x = csel(B ? (cg >= cx) : (cg > cx), u.g, u.x);
+    Cnt<NW> x = cselw(B ? (cg >= cx) : (cg > cx), u.g, u.x);
     asm volatile("" : "+v"(gx));  // opaque: keeps "w1 + gap unit + tie" one v_addc
-    x.w1 += gx;
-    if (TRACK) x.w1 += (cg == cx) ? 1u : 0u;
+    x.w[1] += gx;
+    if (TRACK) x.w[1] += (cg == cx) ? 1u : 0u;
     // Iy from the left. A: F-path iff cf >= cy;  B: iff cf > cy.
     const int cf = l.F + oy, cy = l.Y + ey;
     const int Y = max(cf, cy) & ~1;
-    C2 y = csel(B ? (cf > cy) : (cf >= cy), l.f, l.y);
+    Cnt<NW> y = cselw(B ? (cf > cy) : (cf >= cy), l.f, l.y);
     asm volatile("" : "+v"(gy));
-    y.w1 += gy;
-    if (TRACK) y.w1 += (cf == cy) ? 1u : 0u;
+    y.w[1] += gy;
+    if (TRACK) y.w[1] += (cf == cy) ? 1u : 0u;
     // M wins ties against Iy and Ix under both priorities (M odd, X / Y even)
     const bool gs = M > Y;
     u.G = max(M, Y);
-    u.g = csel(gs, m, y);
+    u.g = cselw(gs, m, y);
     u.X = X;
     u.x = x;
     const bool fs = M > X;
     l.F = max(M, X);
-    l.f = csel(fs, m, x);
+    l.f = cselw(fs, m, x);
     l.Y = Y;
     l.y = y;
     return nd;
@@ -143,18 +180,36 @@ __device__ __forceinline__ S1Best s1_cell(const S1Best& d, S1Col& u, S1Left& l, 
 struct RingEntry1 {
     uint4 q[2];
 };
-__device__ __forceinline__ void ring_put(RingEntry1* e, const S1Left& s) {
-    e->q[0] = make_uint4((uint32_t)s.F, s.f.w0, s.f.w1, (uint32_t)s.Y);
-    e->q[1] = make_uint4(s.y.w0, s.y.w1, 0u, 0u);
+template <int NW>
+__device__ __forceinline__ void ring_put(RingEntry1* e, const S1Left<NW>& s) {
+    if constexpr (NW == 2) {
+        e->q[0] = make_uint4((uint32_t)s.F, s.f.w[0], s.f.w[1], (uint32_t)s.Y);
+        e->q[1] = make_uint4(s.y.w[0], s.y.w[1], 0u, 0u);
+    } else {
+        e->q[0] = make_uint4((uint32_t)s.F, s.f.w[0], s.f.w[1], s.f.w[2]);
+        e->q[1] = make_uint4((uint32_t)s.Y, s.y.w[0], s.y.w[1], s.y.w[2]);
+    }
 }
-__device__ __forceinline__ void ring_get(const RingEntry1* e, S1Left& s) {
+template <int NW>
+__device__ __forceinline__ void ring_get(const RingEntry1* e, S1Left<NW>& s) {
     const uint4 a = e->q[0], b = e->q[1];
-    s.F = (int)a.x;
-    s.f.w0 = a.y;
-    s.f.w1 = a.z;
-    s.Y = (int)a.w;
-    s.y.w0 = b.x;
-    s.y.w1 = b.y;
+    if constexpr (NW == 2) {
+        s.F = (int)a.x;
+        s.f.w[0] = a.y;
+        s.f.w[1] = a.z;
+        s.Y = (int)a.w;
+        s.y.w[0] = b.x;
+        s.y.w[1] = b.y;
+    } else {
+        s.F = (int)a.x;
+        s.f.w[0] = a.y;
+        s.f.w[1] = a.z;
+        s.f.w[2] = a.w;
+        s.Y = (int)b.x;
+        s.y.w[0] = b.y;
+        s.y.w[1] = b.z;
+        s.y.w[2] = b.w;
+    }
 }
 
 // Per-lane column constants.  The LUT (two uses per cell) and the equality fields stay in
@@ -163,7 +218,7 @@ __device__ __forceinline__ void ring_get(const RingEntry1* e, S1Left& s) {
 // (saturated) VALU.
 template <int K>
 struct LaneCols1 {
-    uint32_t lut[K];  // w0 units by row base: valid bit r, ts bit 10+r, tv bit 20+r;
+    uint32_t lut[K];  // w0 units by row base r: valid bit r, ts bit a1_ts_bit + r, tv bit 20 + r;
                       // bit 14 (= A1_GAP): an x-gap in column j lies in y's nucleotide span;
                       // column byte << 24
     uint32_t eqp0, eqp1, eqp2, eqp3;  // 3-bit field per column: 4 where the byte is "ACGT"[r]
@@ -192,18 +247,18 @@ __device__ __forceinline__ uint32_t a1_xinfo(uint32_t c, int i, int fx, int lx) 
     return c | (bc << 8) | (ec << 11) | (riy << 14) | ((bc < 4u ? 1u : 0u) << 15);
 }
 
-template <int K, int W, bool DEF, bool B, bool FIRST>
-__device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col (&st)[K], S1Left& pay, S1Best& carry,
-                                         const LaneCols1<K>& lc, const ColC* __restrict__ colc,
+template <int K, int W, bool DEF, bool B, bool FIRST, int NW>
+__device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col<NW> (&st)[K], S1Left<NW>& pay,
+                                         S1Best<NW>& carry, const LaneCols1<K>& lc, const ColC* __restrict__ colc,
                                          const int* __restrict__ colex, const uint32_t* __restrict__ xinfo,
                                          const RingEntry1* __restrict__ ring_in, RingEntry1* __restrict__ ring_out,
                                          const KScores& sc) {
     constexpr bool TRACK = !B;
-    S1Left in;
+    S1Left<NW> in;
     if constexpr (FIRST) {
         in = s1_shr_first(pay, s + 1, sc);
     } else {
-        S1Left old;
+        S1Left<NW> old;
         ring_get(ring_in + ((s + 1) & (RING - 1)), old);
         in = s1_shr_old(pay, old);
     }
@@ -212,7 +267,8 @@ __device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col (&st)[K]
         const uint32_t xi = xinfo[i - 1];
         const bool nuc = (xi >> 15) & 1u;
         const uint32_t xsh = (xi >> 8) & 3u;
-        const uint32_t incm = nuc ? A1_INC_MASK : 0u;
+        const uint32_t incm0 = nuc ? a1_inc0_mask<NW>() : 0u;
+        const uint32_t incm2 = nuc ? (1u << 20) : 0u;
         const uint32_t gxrow = nuc ? A1_GAP : 0u;
         const uint32_t gyrow = ((xi >> 14) & 1u) ? ~0u : 0u;
         const uint32_t ec = (xi >> 11) & 7u;
@@ -228,16 +284,17 @@ __device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col (&st)[K]
         const bool lastrow = (i == nA);
         const int oy = lastrow ? sc.eo : sc.io;
         const int ey = lastrow ? sc.ee : sc.ie;
-        S1Best d = carry;
-        S1Left l = in;
+        S1Best<NW> d = carry;
+        S1Left<NW> l = in;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t e = (eq >> (3 * k)) & 7u;
             const int sM = DEF ? sc.mi + (int)e : (e ? sc.ma : sc.mi);
-            const uint32_t inc = (lc.lut[k] >> xsh) & incm;
+            const uint32_t t = lc.lut[k] >> xsh;
             const ColC cc = colc[k * 64 * W];
             const int ex = DEF ? sc.ie : colex[k * 64 * W];
-            d = s1_cell<B, TRACK>(d, st[k], l, sM, inc, lc.lut[k] & gxrow, cc.yn & gyrow, cc.ox, ex, oy, ey);
+            d = s1_cell<B, TRACK>(d, st[k], l, sM, t & incm0, t & incm2, lc.lut[k] & gxrow, cc.yn & gyrow, cc.ox,
+                                  ex, oy, ey);
         }
         pay = l;
         if (W > 1 && ring_out != nullptr && lane == 63) ring_put(ring_out + (i & (RING - 1)), pay);
@@ -245,16 +302,27 @@ __device__ __forceinline__ void dp_step1(int s, int lane, int nA, S1Col (&st)[K]
     carry = s1_best_left<B, TRACK>(in);
 }
 
-__device__ __forceinline__ void a1_write(double* o, const MetricSpec& ms, C2 c) {
-    const uint32_t valid = c.w0 & 0x3FFu, ts = (c.w0 >> 10) & 0x3FFu, tv = (c.w0 >> 20) & 0x3FFu;
-    const uint32_t gap = (c.w1 >> 14) & 0xFFFu;
+template <int NW>
+__device__ __forceinline__ void a1_write(double* o, const MetricSpec& ms, const Cnt<NW>& c) {
+    uint32_t valid, ts, tv, gap;
+    if constexpr (NW == 2) {
+        valid = c.w[0] & 0x3FFu;
+        ts = (c.w[0] >> 10) & 0x3FFu;
+        tv = (c.w[0] >> 20) & 0x3FFu;
+        gap = (c.w[1] >> 14) & 0xFFFu;
+    } else {
+        valid = c.w[0] & 0xFFFFu;
+        ts = c.w[0] >> 16;
+        tv = c.w[2] >> 20;
+        gap = c.w[1] >> 14;
+    }
     for (int m = 0; m < ms.n; ++m) o[m] = metric_value(ms.code[m], valid, ts, tv, gap);
 }
 
 // Pass 1 (B = false): every pair of `ps` in orientation A (rows = the shorter sequence);
 // writes A's slot, and B's slot too when A's path has no divergent tie, else appends the pair
 // to wlist.  Pass 2 (B = true): the pairs of wlist[0, *wcount) in orientation B, B's slot.
-template <int K, int W, bool DEF, int OCC, bool B>
+template <int K, int W, bool DEF, int OCC, bool B, int NW>
 __global__ void __launch_bounds__(64 * W, OCC)
 k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xcap, int out_mode,
          double* __restrict__ out, int32_t* __restrict__ sout, uint32_t* __restrict__ wlist,
@@ -340,7 +408,7 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
                     for (int xb = 0; xb < 4; ++xb) {
                         const int dd = xb ^ yb;
                         l |= 1u << xb;                      // valid
-                        if (dd == 2) l |= 1u << (10 + xb);  // transition
+                        if (dd == 2) l |= 1u << (a1_ts_bit<NW>() + xb);  // transition
                         else if (dd) l |= 1u << (20 + xb);  // transversion
                     }
                     yn = A1_GAP;
@@ -357,11 +425,11 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
             if (!DEF) colex[k * 64 * W] = (j == nB) ? sc.ee : sc.ie;
         }
 
-        S1Col st[K];
+        S1Col<NW> st[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) st[k] = s1_col_row0(j0 + k, sc);
-        S1Left pay = s1_left_row0(j0 + K - 1, sc);
-        S1Best carry = s1_best_col<B, false>(s1_col_row0(j0 - 1, sc));
+        for (int k = 0; k < K; ++k) st[k] = s1_col_row0<NW>(j0 + k, sc);
+        S1Left<NW> pay = s1_left_row0<NW>(j0 + K - 1, sc);
+        S1Best<NW> carry = s1_best_col<B, false>(s1_col_row0<NW>(j0 - 1, sc));
 
         const RingEntry1* ring_in = (w > 0) ? rings + (size_t)(w - 1) * RING : nullptr;
         RingEntry1* ring_out = (w < W - 1) ? rings + (size_t)w * RING : nullptr;
@@ -376,10 +444,10 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
             if (W == 1 || (blk >= 0 && blk < nblk)) {
                 if (w == 0) {
                     for (int s = s0; s < s1; ++s)
-                        dp_step1<K, W, DEF, B, true>(s, lane, nA, st, pay, carry, lc, colc, colex, xinfo, ring_in, ring_out, sc);
+                        dp_step1<K, W, DEF, B, true, NW>(s, lane, nA, st, pay, carry, lc, colc, colex, xinfo, ring_in, ring_out, sc);
                 } else {
                     for (int s = s0; s < s1; ++s)
-                        dp_step1<K, W, DEF, B, false>(s, lane, nA, st, pay, carry, lc, colc, colex, xinfo, ring_in, ring_out, sc);
+                        dp_step1<K, W, DEF, B, false, NW>(s, lane, nA, st, pay, carry, lc, colc, colex, xinfo, ring_in, ring_out, sc);
                 }
             }
             if (W > 1) __syncthreads();
@@ -388,15 +456,15 @@ k_align1(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xc
         const int jl = nB - 1;
         if (w == jl / (64 * K) && lane == ((jl / K) & 63)) {
             const int kk = jl % K;
-            S1Col e = st[0];
+            S1Col<NW> e = st[0];
 #pragma unroll
             for (int k = 1; k < K; ++k)
                 if (k == kk) e = st[k];
-            const S1Best fin = s1_best_col<B, !B>(e);
+            const S1Best<NW> fin = s1_best_col<B, !B>(e);
             if (B) {
                 a1_write(slot_b, ms, fin.c);
             } else {
-                const bool diverges = (fin.c.w1 & 0x3FFFu) != 0u;
+                const bool diverges = (fin.c.w[1] & 0x3FFFu) != 0u;
                 if (slot_a) a1_write(slot_a, ms, fin.c);
                 if (slot_b) {
                     if (!diverges) a1_write(slot_b, ms, fin.c);

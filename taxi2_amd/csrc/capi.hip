@@ -207,35 +207,46 @@ size_t align_lds_bytes(const Variant& v, int xcap) {
 struct Variant1 {
     int K, W, occ;
     bool def;
+    int nw;  // counter words: 2 (<= 1023 bp), 3 (<= 4095 bp)
     const void* fn[2];  // pass 1 (orientation A + divergence flag), pass 2 (orientation B)
     void (*launch[2])(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int,
                       int, double*, int32_t*, uint32_t*, uint32_t*, unsigned long long*);
 };
 
-template <int K, int W, bool DEF, int OCC, bool B>
+template <int K, int W, bool DEF, int OCC, bool B, int NW>
 void launch_align1(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc,
                    MetricSpec ms, int xcap, int om, double* out, int32_t* so, uint32_t* wl, uint32_t* wc,
                    unsigned long long* nx) {
-    hipLaunchKernelGGL((k_align1<K, W, DEF, OCC, B>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so, wl, wc, nx);
+    hipLaunchKernelGGL((k_align1<K, W, DEF, OCC, B, NW>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so, wl, wc,
+                       nx);
 }
 
-#define T2_VARIANT1(K, W, DEF, OCC)                                                                   \
-    Variant1{K, W, OCC, DEF,                                                                         \
-             {(const void*)&k_align1<K, W, DEF, OCC, false>, (const void*)&k_align1<K, W, DEF, OCC, true>}, \
-             {&launch_align1<K, W, DEF, OCC, false>, &launch_align1<K, W, DEF, OCC, true>}}
+#define T2_VARIANT1N(K, W, DEF, OCC, NW)                                                                 \
+    Variant1{K, W, OCC, DEF, NW,                                                                          \
+             {(const void*)&k_align1<K, W, DEF, OCC, false, NW>, (const void*)&k_align1<K, W, DEF, OCC, true, NW>}, \
+             {&launch_align1<K, W, DEF, OCC, false, NW>, &launch_align1<K, W, DEF, OCC, true, NW>}}
+#define T2_VARIANT1(K, W, DEF, OCC) T2_VARIANT1N(K, W, DEF, OCC, 2)
 
-// Ordered by column capacity 64 * K * W (max 1023 = A1_MAX_LEN).
+// Ordered by column capacity 64 * K * W.  Two-word counters up to A1_MAX_LEN, three-word counters
+// up to A1_MAX_LEN_LONG.
 const Variant1 kAlign1Def[] = {
-    T2_VARIANT1(4, 1, true, 4), T2_VARIANT1(8, 1, true, 4), T2_VARIANT1(6, 2, true, 4), T2_VARIANT1(8, 2, true, 4),
+    T2_VARIANT1(4, 1, true, 4),      T2_VARIANT1(8, 1, true, 4),      T2_VARIANT1(6, 2, true, 4),
+    T2_VARIANT1(8, 2, true, 4),      T2_VARIANT1N(10, 2, true, 3, 3), T2_VARIANT1N(6, 4, true, 3, 3),
+    T2_VARIANT1N(8, 4, true, 3, 3),  T2_VARIANT1N(10, 4, true, 2, 3), T2_VARIANT1N(6, 8, true, 2, 3),
+    T2_VARIANT1N(8, 8, true, 2, 3),
 };
 const Variant1 kAlign1[] = {
-    T2_VARIANT1(4, 1, false, 4), T2_VARIANT1(8, 1, false, 4), T2_VARIANT1(6, 2, false, 4),
-    T2_VARIANT1(8, 2, false, 4),
+    T2_VARIANT1(4, 1, false, 4),      T2_VARIANT1(8, 1, false, 4),      T2_VARIANT1(6, 2, false, 4),
+    T2_VARIANT1(8, 2, false, 4),      T2_VARIANT1N(10, 2, false, 3, 3), T2_VARIANT1N(6, 4, false, 3, 3),
+    T2_VARIANT1N(8, 4, false, 3, 3),  T2_VARIANT1N(10, 4, false, 2, 3), T2_VARIANT1N(6, 8, false, 2, 3),
+    T2_VARIANT1N(8, 8, false, 2, 3),
 };
 // Tuning shapes (TAXI2_VARIANT1="K,W,OCC").
 const Variant1 kAlign1Sweep[] = {
     T2_VARIANT1(8, 2, true, 3), T2_VARIANT1(8, 2, true, 5), T2_VARIANT1(4, 4, true, 4), T2_VARIANT1(4, 4, true, 6),
-    T2_VARIANT1(10, 2, true, 3), T2_VARIANT1(10, 2, true, 4),
+    T2_VARIANT1(10, 2, true, 3), T2_VARIANT1(10, 2, true, 4), T2_VARIANT1N(8, 4, true, 4, 3),
+    T2_VARIANT1N(8, 4, true, 2, 3), T2_VARIANT1N(10, 2, true, 2, 3), T2_VARIANT1N(6, 4, true, 2, 3),
+    T2_VARIANT1N(10, 4, true, 3, 3), T2_VARIANT1N(6, 8, true, 3, 3),
 };
 
 const Variant1* pick_variant1(const KScores& k, int max_len) {
@@ -248,14 +259,17 @@ const Variant1* pick_variant1(const KScores& k, int max_len) {
                                  : tab == kAlign1Def ? sizeof kAlign1Def / sizeof kAlign1Def[0]
                                                      : sizeof kAlign1 / sizeof kAlign1[0];
                 for (size_t i = 0; i < n; ++i)
-                    if (tab[i].K == K && tab[i].W == W && tab[i].occ == occ && tab[i].def == def) return &tab[i];
+                    if (tab[i].K == K && tab[i].W == W && tab[i].occ == occ && tab[i].def == def &&
+                        (tab[i].nw == 2) == (max_len <= A1_MAX_LEN))
+                        return &tab[i];
             }
         }
     }
     const Variant1* tab = def ? kAlign1Def : kAlign1;
     const int n = (int)(def ? sizeof kAlign1Def / sizeof kAlign1Def[0] : sizeof kAlign1 / sizeof kAlign1[0]);
+    const int nw = max_len <= A1_MAX_LEN ? 2 : 3;
     for (int i = 0; i < n; ++i)
-        if (64 * tab[i].K * tab[i].W >= max_len) return &tab[i];
+        if (tab[i].nw == nw && 64 * tab[i].K * tab[i].W >= max_len) return &tab[i];
     return nullptr;
 }
 
@@ -307,7 +321,7 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (mag * (2LL * max_len + 2) >= (1LL << 26))
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
-    if (!is_linear(k) && max_len <= A1_MAX_LEN && !getenv("TAXI2_NO_ALIGN1")) {
+    if (!is_linear(k) && max_len <= A1_MAX_LEN_LONG && !getenv("TAXI2_NO_ALIGN1")) {
         if (ps.count <= 0) return 0;
         const Variant1* v1 = pick_variant1(k, max_len);
         if (v1) return launch_align1_pairs(ctx, *v1, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, xcap);

@@ -293,3 +293,30 @@ def test_single_orientation_divergent_pairs(engine, oracle_c):
     assert_metrics_equal(got, exp[:, 0, :])
     for s in (st, qs, rs):
         s.free()
+
+
+def test_single_orientation_long_counters(engine, oracle_c):
+    """1 024-4 095 bp run the three-word-counter variant (NW = 3): a tie-heavy 1 500 bp family
+    with ragged ends and IUPAC bytes against the oracle and the two-orientation kernel."""
+    from taxi2_amd._native import tri_pairs
+
+    fam = family_sequences(10, 1500, 0x52, ancestors=2, max_sub=0.05, indel_rate=0.02)
+    rng = np.random.default_rng(6)
+    seqs = []
+    for k, s in enumerate(fam):
+        s = s[: 1100 + int(rng.integers(0, 400))]
+        if k % 3 == 1:
+            b = bytearray(s.encode())
+            for pos in rng.integers(0, len(b), 5):
+                b[pos] = ord("NRY"[int(rng.integers(0, 3))])
+            s = b.decode()
+        seqs.append(s)
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    got, gsc = engine.all_pairs(st, 0, len(a), METRICS, None, with_scores=True)
+    two = _with_env("TAXI2_NO_ALIGN1", "1", lambda: engine.all_pairs(st, 0, len(a), METRICS, None))
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=SCORE_SETS["default"])
+    assert np.array_equal(gsc, esc)
+    assert_metrics_equal(got, exp)
+    assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(two, nan=9.0))
+    st.free()
