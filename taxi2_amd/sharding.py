@@ -1,10 +1,11 @@
-"""Pair-space sharding across GPUs (one process per GPU, torch.distributed).
+"""Pair-space and query sharding across GPUs (one process per GPU, torch.distributed).
 
 versusAll's unordered pairs are the row-major upper triangle of the N x N product; row a holds
 N-1-a pairs.  Ranks take contiguous row blocks balanced by pair count; the
 pair blocks are independent, so the only exchange is the final gather of each rank's results
 (RCCL all-gather over xGMI on GPUs, gloo on CPU for tests).  RCCL has no all-gather-v, so
-blocks are padded to the largest one.
+blocks are padded to the largest one.  versusReference shards its queries the same way
+(contiguous equal blocks, references replicated on every rank).
 """
 
 from __future__ import annotations
@@ -79,3 +80,32 @@ def distributed_all_pairs(n: int, compute: Callable[[int, int], np.ndarray], gro
     k0, cnt = blocks[rank]
     local = compute(k0, cnt)
     return gather_blocks(local, [c for _, c in blocks], group=group, device=device)
+
+
+def shard_range(n: int, world: int) -> list[tuple[int, int]]:
+    """Contiguous, nearly equal [lo, hi) blocks of n rows (versusReference queries)."""
+    return [(n * r // world, n * (r + 1) // world) for r in range(world)]
+
+
+def distributed_rows(n: int, compute: Callable[[int, int], np.ndarray], group=None, device=None) -> np.ndarray:
+    """Every rank computes ``compute(q0, q1)`` (rows [q0, q1), shape (q1 - q0, ...)) for its
+    block and receives every block: the full (n, ...) result on every rank."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    blocks = shard_range(n, world)
+    q0, q1 = blocks[rank]
+    return gather_blocks(compute(q0, q1), [hi - lo for lo, hi in blocks], group=group, device=device)
+
+
+def world_info() -> tuple[bool, int]:
+    """(distributed run with more than one rank, rank)."""
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return True, dist.get_rank()
+    except Exception:
+        pass
+    return False, 0

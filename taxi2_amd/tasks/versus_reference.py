@@ -26,6 +26,7 @@ from ..align import PairwiseAligner, Scores
 from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric, check_ncd_strings
 from ..pairs import SequencePair, SequencePairHandler
 from ..types import AttrDict
+from ..sharding import distributed_rows, world_info
 from .common import (Results, console_report, create_parents, fixed_decimals, format_values, gpu_text_ok,
                      report, write_rows_gpu)
 
@@ -132,49 +133,70 @@ class VersusReference:
             check_ncd_strings(s.seq for s in refs)
         qs = eng.upload([s.seq for s in data], align=align)
         rs = eng.upload([s.seq for s in refs], align=align)
-        try:
-            idx = np.full(Q, -1, dtype=np.int64)
-            dmin = np.full(Q, np.nan)
-            ext = np.full((Q, len(extras)), np.nan)
-            mat = np.full((Q, R), np.nan) if want_matrix else None
+        E = len(extras)
+        scale = 100.0 if pct else 1.0
+
+        def block(qa: int, qb: int) -> np.ndarray:
+            """Queries [qa, qb) -> rows [idx, dmin, extras (E), primary row (R if want_matrix)]."""
+            width = 2 + E + (R if want_matrix else 0)
+            res = np.full((qb - qa, width), np.nan)
             step = max(1, (1 << 22) // max(R, 1))
             if ncd_primary:
                 step = max(1, (1 << 16) // max(R, 1))
-            for q0 in range(0, Q, step):
-                q1 = min(Q, q0 + step)
+            for q0 in range(qa, qb, step):
+                q1 = min(qb, q0 + step)
+                rows = res[q0 - qa : q1 - qa]
+                rows[:, 0] = -1
                 if R and not ncd_primary:
                     cx = [str(extras[k]) for k in cextra]
-                    i, d, e, m = eng.closest(qs, rs, q0, q1, str(primary), cx, scores,
-                                             scale=100.0 if pct else 1.0, want_matrix=want_matrix)
-                    idx[q0:q1], dmin[q0:q1] = i, d
+                    i, d, e, m = eng.closest(qs, rs, q0, q1, str(primary), cx, scores, scale=scale,
+                                             want_matrix=want_matrix)
+                    rows[:, 0], rows[:, 1] = i, d
                     if e is not None:
-                        ext[q0:q1, cextra] = e
+                        rows[:, [2 + k for k in cextra]] = e
                     if m is not None:
-                        mat[q0:q1] = m
+                        rows[:, 2 + E :] = m
                 elif R:
                     nq = q1 - q0
-                    qa = np.repeat(np.arange(q0, q1, dtype=np.int64), R)
-                    ra = np.tile(np.arange(R, dtype=np.int64), nq)
-                    block = eng.ncd_pairs(qs, rs, qa, ra, scores, aligned=align, both=False).reshape(nq, R)
-                    i, d = first_minimum(block, 100.0 if pct else 1.0)
-                    idx[q0:q1], dmin[q0:q1] = i, d
-                    if mat is not None:
-                        mat[q0:q1] = block
+                    qv = np.repeat(np.arange(q0, q1, dtype=np.int64), R)
+                    rv = np.tile(np.arange(R, dtype=np.int64), nq)
+                    mat_b = eng.ncd_pairs(qs, rs, qv, rv, scores, aligned=align, both=False).reshape(nq, R)
+                    i, d = first_minimum(mat_b, scale)
+                    rows[:, 0], rows[:, 1] = i, d
+                    if want_matrix:
+                        rows[:, 2 + E :] = mat_b
                     if cextra:
                         ok = np.nonzero(i >= 0)[0]
                         if len(ok):
                             e = eng.list_pairs(qs, rs, ok + q0, i[ok], [str(extras[k]) for k in cextra], scores)
-                            ext[(ok + q0)[:, None], np.array(cextra)[None, :]] = e[:, 0, :] if align else e
+                            rows[ok[:, None], np.array([2 + k for k in cextra])[None, :]] = e[:, 0, :] if align else e
+                if ncd_extra:
+                    idxb = rows[:, 0].astype(np.int64)
+                    ok = np.nonzero(idxb >= 0)[0]
+                    if len(ok):
+                        v = eng.ncd_pairs(qs, rs, ok + q0, idxb[ok], scores, aligned=align, both=False)
+                        for k in ncd_extra:
+                            rows[ok, 2 + k] = v
                 report(self.progress_handler, "distance.x.id", q1 * R, total)
-            if ncd_extra:
-                ok = np.nonzero(idx >= 0)[0]
-                if len(ok):
-                    v = eng.ncd_pairs(qs, rs, ok, idx[ok], scores, aligned=align, both=False)
-                    for k in ncd_extra:
-                        ext[ok, k] = v
+            return res
+
+        try:
+            distributed, rank = world_info()
+            if distributed:  # queries sharded across ranks, references replicated (SURVEY.md §8(e))
+                import torch
+                import torch.distributed as dist
+
+                device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else None
+                res = distributed_rows(Q, block, device=device)
+            else:
+                res = block(0, Q)
         finally:
             qs.free()
             rs.free()
+        idx = res[:, 0].astype(np.int64)
+        dmin = res[:, 1]
+        ext = res[:, 2 : 2 + E]
+        mat = res[:, 2 + E :] if want_matrix else None
 
         # groupby(x.id) over consecutive queries, first minimum wins (versus_reference.py:184-188)
         groups = []
@@ -198,13 +220,14 @@ class VersusReference:
             closest.append((q, int(idx[q]), float(dmin[q]), ext[q].copy()))
         self.closest = closest
 
-        if self.params.pairs.write:
-            self.write_pairs(data, refs)
-        if mat is not None:
-            A = mat * 100.0 if pct else mat
-            self.write_distances_linear(data, refs, A)
-            self.write_distances_matrix(data, refs, A)
-        self.write_closest(data, refs, closest)
+        if world_info()[1] == 0:  # rank 0 writes (every rank holds the gathered results)
+            if self.params.pairs.write:
+                self.write_pairs(data, refs)
+            if mat is not None:
+                A = mat * 100.0 if pct else mat
+                self.write_distances_linear(data, refs, A)
+                self.write_distances_matrix(data, refs, A)
+            self.write_closest(data, refs, closest)
         report(self.progress_handler, "Finalizing...", total, total)
         return Results(self.work_dir, perf_counter() - ts)
 

@@ -72,3 +72,47 @@ def test_two_rank_gloo_all_pairs(tmp_path, oracle_c):
     for got in (r0, r1):
         assert got.shape == exp.shape
         assert np.array_equal(np.nan_to_num(got, nan=7.0), np.nan_to_num(exp, nan=7.0))
+
+
+ROWS_WORKER = textwrap.dedent(
+    """
+    import os, sys
+    import numpy as np
+    import torch.distributed as dist
+    sys.path.insert(0, {root!r})
+    from taxi2_amd.sharding import distributed_rows
+
+    dist.init_process_group("gloo")
+    def compute(q0, q1):
+        q = np.arange(q0, q1, dtype=np.float64)
+        return np.stack([q, q * q, -q], axis=1)
+    res = distributed_rows(37, compute)
+    np.save(os.environ["OUT"] + f".{{dist.get_rank()}}.npy", res)
+    dist.destroy_process_group()
+    """
+)
+
+
+def test_two_rank_gloo_query_rows(tmp_path):
+    """versusReference query sharding (contiguous blocks, all-gather): every rank gets all rows."""
+    script = tmp_path / "rows.py"
+    script.write_text(ROWS_WORKER.format(root=str(ROOT)))
+    out = tmp_path / "rows"
+    env = dict(os.environ, OUT=str(out), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    q = np.arange(37, dtype=np.float64)
+    exp = np.stack([q, q * q, -q], axis=1)
+    for k in range(2):
+        assert np.array_equal(np.load(str(out) + f".{k}.npy"), exp)
+
+
+def test_shard_range_covers():
+    from taxi2_amd.sharding import shard_range
+
+    for n in (0, 1, 7, 100):
+        for w in (1, 2, 3, 8):
+            b = shard_range(n, w)
+            assert b[0][0] == 0 and b[-1][1] == n and all(b[i][1] == b[i + 1][0] for i in range(w - 1))
