@@ -26,7 +26,9 @@
  *     context owns all device memory.  *_dev entry points take device pointers that the
  *     caller allocated on the context's device, plus an optional hipStream_t (void*).
  *   - Threading: one context per device; calls on one context are serialized by the
- *     caller (the Python layer holds one context per process / GPU).
+ *     caller (the Python layer holds one context per process / GPU).  A context's device
+ *     scratch (e.g. the aligner's re-run worklist) is reused by its next call, so *_dev calls
+ *     on one context must be stream-ordered (same stream, or synchronized in between).
  */
 #ifndef TAXI2_MI355X_H
 #define TAXI2_MI355X_H
