@@ -76,7 +76,7 @@ int fail(taxi2_ctx* ctx, const char* fmt, ...) {
 #define HIP_TRY(ctx, expr)                                                                    \
     do {                                                                                      \
         hipError_t e_ = (expr);                                                               \
-        if (e_ != hipSuccess) return fail(ctx, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) return fail(ctx, "%s failed (capi.hip:%d): %s", #expr, __LINE__, hipGetErrorString(e_)); \
     } while (0)
 
 int ensure(taxi2_ctx* ctx, void** p, size_t* cap, size_t need) {
@@ -482,8 +482,7 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out) 
     const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 64);
     const int64_t threads = (want + 63) / 64 * 64;
     if (ctx->z_threads < threads) {
-        if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
-    if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
+        if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
         if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
         ctx->d_zheads = nullptr;
         ctx->d_zslabs = nullptr;

@@ -1,4 +1,5 @@
-"""GPU-backed TaxI2 tasks: the versusAll / versusReference hot path."""
+"""GPU-backed TaxI2 tasks: versusAll / versusReference (the hot path) and Decontaminate (its rectangular caller)."""
 
 from .versus_all import VersusAll  # noqa: F401
 from .versus_reference import VersusReference  # noqa: F401
+from .decontaminate import Decontaminate  # noqa: F401

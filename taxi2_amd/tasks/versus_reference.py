@@ -22,27 +22,12 @@ from typing import Callable
 
 import numpy as np
 
-from ..align import PairwiseAligner, Scores
+from ..align import Scores
 from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric, check_ncd_strings
-from ..pairs import SequencePair, SequencePairHandler
 from ..types import AttrDict
 from ..sharding import distributed_rows, world_info
-from .common import (Results, console_report, create_parents, fixed_decimals, format_values, gpu_text_ok,
-                     report, write_rows_gpu)
-
-
-def first_minimum(block: np.ndarray, scale: float) -> tuple[np.ndarray, np.ndarray]:
-    """Per row: index of the first minimum of ``scale * v`` over finite values (the reference's
-    ``min`` over Distances after the x100 adjustment, versus_reference.py:184-188, 232) and the
-    unscaled value; -1 / NaN for rows without a defined value (same contract as taxi2_closest)."""
-    v = block * scale
-    ok = np.isfinite(v)
-    w = np.where(ok, v, np.inf)
-    i = np.argmin(w, axis=1) if block.shape[1] else np.zeros(block.shape[0], dtype=np.int64)
-    has = ok.any(axis=1)
-    idx = np.where(has, i, -1).astype(np.int64)
-    d = np.where(has, block[np.arange(block.shape[0]), np.maximum(idx, 0)], np.nan)
-    return idx, d
+from .common import Results, console_report, create_parents, report
+from .rect import closest_rows, first_minimum, write_rect_linear, write_rect_matrix, write_rect_pairs  # noqa: F401
 
 
 class VersusReference:
@@ -125,10 +110,7 @@ class VersusReference:
         want_matrix = bool(self.params.distances.write_linear or self.params.distances.write_matricial)
         total = Q * R
         eng = self._engine()
-        ncd_primary = str(primary) == "ncd"
-        ncd_extra = [k for k, m in enumerate(extras) if str(m) == "ncd"]
-        cextra = [k for k, m in enumerate(extras) if str(m) != "ncd"]
-        if ncd_primary or ncd_extra:
+        if str(primary) == "ncd" or any(str(m) == "ncd" for m in extras):
             check_ncd_strings(s.seq for s in data)
             check_ncd_strings(s.seq for s in refs)
         qs = eng.upload([s.seq for s in data], align=align)
@@ -137,48 +119,8 @@ class VersusReference:
         scale = 100.0 if pct else 1.0
 
         def block(qa: int, qb: int) -> np.ndarray:
-            """Queries [qa, qb) -> rows [idx, dmin, extras (E), primary row (R if want_matrix)]."""
-            width = 2 + E + (R if want_matrix else 0)
-            res = np.full((qb - qa, width), np.nan)
-            step = max(1, (1 << 22) // max(R, 1))
-            if ncd_primary:
-                step = max(1, (1 << 16) // max(R, 1))
-            for q0 in range(qa, qb, step):
-                q1 = min(qb, q0 + step)
-                rows = res[q0 - qa : q1 - qa]
-                rows[:, 0] = -1
-                if R and not ncd_primary:
-                    cx = [str(extras[k]) for k in cextra]
-                    i, d, e, m = eng.closest(qs, rs, q0, q1, str(primary), cx, scores, scale=scale,
-                                             want_matrix=want_matrix)
-                    rows[:, 0], rows[:, 1] = i, d
-                    if e is not None:
-                        rows[:, [2 + k for k in cextra]] = e
-                    if m is not None:
-                        rows[:, 2 + E :] = m
-                elif R:
-                    nq = q1 - q0
-                    qv = np.repeat(np.arange(q0, q1, dtype=np.int64), R)
-                    rv = np.tile(np.arange(R, dtype=np.int64), nq)
-                    mat_b = eng.ncd_pairs(qs, rs, qv, rv, scores, aligned=align, both=False).reshape(nq, R)
-                    i, d = first_minimum(mat_b, scale)
-                    rows[:, 0], rows[:, 1] = i, d
-                    if want_matrix:
-                        rows[:, 2 + E :] = mat_b
-                    if cextra:
-                        ok = np.nonzero(i >= 0)[0]
-                        if len(ok):
-                            e = eng.list_pairs(qs, rs, ok + q0, i[ok], [str(extras[k]) for k in cextra], scores)
-                            rows[ok[:, None], np.array([2 + k for k in cextra])[None, :]] = e[:, 0, :] if align else e
-                if ncd_extra:
-                    idxb = rows[:, 0].astype(np.int64)
-                    ok = np.nonzero(idxb >= 0)[0]
-                    if len(ok):
-                        v = eng.ncd_pairs(qs, rs, ok + q0, idxb[ok], scores, aligned=align, both=False)
-                        for k in ncd_extra:
-                            rows[ok, 2 + k] = v
-                report(self.progress_handler, "distance.x.id", q1 * R, total)
-            return res
+            return closest_rows(eng, qs, rs, qa, qb, primary, extras, scores, align, scale, want_matrix,
+                                lambda q1: report(self.progress_handler, "distance.x.id", q1 * R, total))
 
         try:
             distributed, rank = world_info()
@@ -233,76 +175,18 @@ class VersusReference:
 
     # ------------------------------------------------------------------ writers
     def write_pairs(self, data, refs):
-        create_parents(self.paths.aligned_pairs)
-        with SequencePairHandler.Formatted(self.paths.aligned_pairs, "w") as fh:
-            if not self.params.pairs.align:
-                for x in data:
-                    for y in refs:
-                        fh.write(SequencePair(x, y))
-                return
-            aligner = PairwiseAligner.Biopython(self.params.pairs.scores, engine=self._engine())
-            for x in data:
-                for pair in aligner.align_many([SequencePair(x, y) for y in refs]):
-                    fh.write(pair)
+        write_rect_pairs(self.paths.aligned_pairs, data, refs, self.params.pairs.align, self.params.pairs.scores,
+                         self._engine())
 
     def write_distances_linear(self, data, refs, A):
-        if not self.params.distances.write_linear:
-            return
-        create_parents(self.paths.distances_linear)
-        fmt, missing = self.params.format.float, self.params.format.missing
-        metric = self.params.distances.metric
-        dec = fixed_decimals(fmt)
-        qids, rids = [s.id for s in data], [s.id for s in refs]
-        if (data and refs and gpu_text_ok(A, dec) and len(set(qids)) == len(qids) and len(set(rids)) == len(rids)
-                and all(list(s.extras) == list(data[0].extras) for s in data)
-                and all(list(s.extras) == list(refs[0].extras) for s in refs)):
-            # same text as DistanceHandler.Linear.WithExtras (one metric, no line merging), GPU-formatted
-            exq, exr = list(data[0].extras), list(refs[0].extras)
-            head = ["seqid (query)", *[k + " (query)" for k in exq], "seqid (reference)",
-                    *[k + " (reference)" for k in exr], str(metric)]
-
-            def pre(s):
-                return "\t".join([s.id, *[v if v is not None else missing for v in s.extras.values()]])
-
-            with open(self.paths.distances_linear, "wb") as fh:
-                fh.write(("\t".join(head) + "\n").encode("utf-8"))
-                write_rows_gpu(fh, self._engine(), np.ascontiguousarray(A)[:, :, None], [pre(s) for s in data],
-                               [pre(s) for s in refs], dec, missing)
-            return
-        with DistanceHandler.Linear.WithExtras(self.paths.distances_linear, "w", missing=missing,
-                                               formatter=fmt) as fh:
-            for i, x in enumerate(data):
-                for j, y in enumerate(refs):
-                    v = A[i, j]
-                    fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
+        if self.params.distances.write_linear:
+            write_rect_linear(self.paths.distances_linear, data, refs, A, self.params.distances.metric,
+                              self.params.format.float, self.params.format.missing, self._engine())
 
     def write_distances_matrix(self, data, refs, A):
-        if not self.params.distances.write_matricial:
-            return
-        create_parents(self.paths.distances_matricial)
-        fmt, missing = self.params.format.float, self.params.format.missing
-        ids = [s.id for s in data]
-        if len(set(ids)) != len(ids):
-            metric = self.params.distances.metric
-            with DistanceHandler.Matrix(self.paths.distances_matricial, "w", missing=missing, formatter=fmt) as fh:
-                for i, x in enumerate(data):
-                    for j, y in enumerate(refs):
-                        v = A[i, j]
-                        fh.write(Distance(metric, x, y, float(v) if np.isfinite(v) else None))
-            return
-        dec = fixed_decimals(fmt)
-        if data and refs and gpu_text_ok(A, dec):
-            with open(self.paths.distances_matricial, "wb") as fh:
-                fh.write(("\t".join(["", *[s.id for s in refs]]) + "\n").encode("utf-8"))
-                write_rows_gpu(fh, self._engine(), np.ascontiguousarray(A), ids, None, dec, missing)
-            return
-        text = format_values(A, fmt, missing)
-        with open(self.paths.distances_matricial, "w") as fh:
-            if data and refs:
-                fh.write("\t".join(["", *[s.id for s in refs]]) + "\n")
-            for i, x in enumerate(data):
-                if refs:
-                    fh.write("\t".join((x.id, *text[i])) + "\n")
+        if self.params.distances.write_matricial:
+            write_rect_matrix(self.paths.distances_matricial, data, refs, A, self.params.distances.metric,
+                              self.params.format.float, self.params.format.missing, self._engine())
 
     def write_closest(self, data, refs, closest):
         create_parents(self.paths.closest)

@@ -155,3 +155,16 @@ def test_versus_reference_ncd_primary_and_extra(tmp_path, engine):
             for k, m in enumerate(task.params.distances.extra_metrics):
                 exp = R.ncd(ax, ay) if str(m) == "ncd" else R.metric(str(m), ax, ay)
                 assert (exp is None and np.isnan(ext[k])) or ext[k] == exp
+
+
+def test_scratch_regrowth_interleaved(engine):
+    """Context scratch regrows across entry points (formatter buffers, NCD slabs): interleaved calls
+    with growing sizes stay correct (regression: a regrowth once freed an unrelated buffer)."""
+    seqs = ["ACGT" * 50, "ACGA" * 60, "TTGCA" * 30]
+    st = engine.upload(seqs, align=False)
+    vals = np.array([[0.5, np.nan], [1.25, -0.0]])
+    for n in (1, 70, 300, 5000):
+        idx = np.arange(n) % 3
+        assert engine.zlib_lengths(st, idx).tolist() == [len(zlib.compress(seqs[i].encode())) for i in idx]
+        assert engine.format_rows(vals, ["a", "b"], None, decimals=2).decode() == "a\t0.50\tNA\nb\t1.25\t-0.00\n"
+    st.free()

@@ -242,3 +242,73 @@ def test_versus_reference(tmp_path, engine, oracle_c, align):
                 v = vals[qq, r, 0]
                 fh.write(Distance(metrics[0], wd[qq], wr[r], float(v) if np.isfinite(v) else None))
     assert (tmp_path / "out/distances/p.linear.tsv").read_text() == lin.read_text()
+
+
+@pytest.mark.parametrize("pct", [False, True])
+def test_decontaminate(tmp_path, engine, oracle_c, pct):
+    """decontaminate.py:336-371 on sample sequences: duplicate consecutive query ids (groupby +
+    zip pairing), an all-N query (every distance None -> the group's first distance), x100 before
+    the threshold; every output file against the oracle's distances."""
+    from taxi2_amd.distances import Distance, DistanceHandler, DistanceMetric
+    from taxi2_amd.handlers import FileHandler
+    from taxi2_amd.sequences import Sequence, SequenceHandler, Sequences
+    from taxi2_amd.tasks import Decontaminate
+
+    allseqs = read_tab("Taxi2test1_120.tab")
+    data = allseqs[:12]
+    data = data[:4] + [Sequence(data[3].id, data[8].seq, data[8].extras)] + data[4:]
+    data.append(Sequence("allN", "NNNNNNNNNN", dict(data[0].extras)))
+    outgroup = allseqs[40:48] + [Sequence("twin", data[1].seq, dict(data[1].extras))]
+    task = Decontaminate()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input = Sequences(data)
+    task.outgroup = Sequences(outgroup)
+    task.params.pairs.write = False
+    task.params.thresholds.similarity = 8.0 if pct else 0.08
+    task.params.format.percentage_multiply = pct
+    task.start()
+
+    dn = [s.normalize() for s in data]
+    on = [s.normalize() for s in outgroup]
+    Q, R = len(dn), len(on)
+    seqs = [s.seq for s in dn] + [s.seq for s in on]
+    pa = np.repeat(np.arange(Q), R)
+    pb = np.tile(np.arange(R), Q) + Q
+    out, _ = oracle_c.batch(seqs, pa, pb, align=True, scores=(1, -1, -8, -1, -1, -1), metrics=("p",))
+    A = out[:, 0, 0].reshape(Q, R) * (100.0 if pct else 1.0)
+    # groups of consecutive ids, min(key=d or inf)
+    minima, g0 = [], 0
+    for k in range(1, Q + 1):
+        if k == Q or dn[k].id != dn[g0].id:
+            best = None
+            for q in range(g0, k):
+                for r in range(R):
+                    v = A[q, r] if np.isfinite(A[q, r]) else np.inf
+                    if best is None or v < best[0]:
+                        best = (v, q, r)
+            v, q, r = best
+            minima.append((on[r].id, None if v == np.inf else float(v)))
+            g0 = k
+    verdicts = [(s, d is not None and d <= task.params.thresholds.similarity) for s, (_, d) in zip(data, minima)]
+    assert any(c for _, c in verdicts) and not all(c for _, c in verdicts)
+    exp_sum = tmp_path / "exp_summary.tsv"
+    with FileHandler.Tabfile(exp_sum, "w", columns=("query_id", "outgroup_id", "outgroup_distance", "contaminant")) as fh:
+        for (s, c), (oid, d) in zip(verdicts, minima):
+            fh.write((s.id, oid, "NA" if d is None else "{:.4f}".format(d), "Yes" if c else "No"))
+    assert (tmp_path / "out/summary.tsv").read_text() == exp_sum.read_text()
+    for name, want in (("decontaminated.tsv", False), ("contaminants.tsv", True)):
+        exp = tmp_path / f"exp_{name}"
+        with SequenceHandler.Tabfile(exp, "w", idHeader="seqid", seqHeader="sequence") as fh:
+            for s, c in verdicts:
+                if c == want:
+                    fh.write(s)
+        assert (tmp_path / "out" / name).read_text() == exp.read_text(), name
+    lin = tmp_path / "exp_lin.tsv"
+    with DistanceHandler.Linear.WithExtras(lin, "w", missing="NA", formatter="{:.4f}") as fh:
+        for q in range(Q):
+            for r in range(R):
+                v = A[q, r]
+                fh.write(Distance(DistanceMetric.Uncorrected(), dn[q], on[r], float(v) if np.isfinite(v) else None))
+    assert (tmp_path / "out/distances/p.linear.tsv").read_text() == lin.read_text()
