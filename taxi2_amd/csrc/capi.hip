@@ -475,11 +475,62 @@ struct Tracer {
     }
 };
 
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out);
+
+// Raw-mode NCD with C(x) computed once per set member (when the pairs outnumber the sequences).
+int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
+                   int64_t count, int both, double* out) {
+    const int no = both ? 2 : 1;
+    const bool same = &X == &Y;
+    const int64_t chunk = std::min<int64_t>(count, (int64_t)1 << 18);
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_single = al((size_t)X.n * 4) + (same ? 0 : al((size_t)Y.n * 4));
+    const size_t b_sst = al((size_t)std::max(X.n, Y.n) * sizeof(ZStream));
+    const size_t b_idx = al((size_t)chunk * 16);
+    const size_t b_cst = al((size_t)chunk * no * sizeof(ZStream)), b_c = al((size_t)chunk * no * 4);
+    const size_t b_v = al((size_t)chunk * no * 8);
+    if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, b_single + b_sst + b_idx + b_cst + b_c + b_v)) return -1;
+    char* base = (char*)ctx->d_aux;
+    int32_t* d_cx = (int32_t*)base;
+    int32_t* d_cy = same ? d_cx : (int32_t*)(base + al((size_t)X.n * 4));
+    ZStream* d_sst = (ZStream*)(base + b_single);
+    int64_t* d_idx = (int64_t*)((char*)d_sst + b_sst);
+    ZStream* d_cst = (ZStream*)((char*)d_idx + b_idx);
+    int32_t* d_c = (int32_t*)((char*)d_cst + b_cst);
+    double* d_v = (double*)((char*)d_c + b_c);
+    const DevSet* sets[2] = {&X, &Y};
+    int32_t* singles[2] = {d_cx, d_cy};
+    for (int k = 0; k < (same ? 1 : 2); ++k) {
+        const DevSet& S = *sets[k];
+        if (S.n == 0) continue;
+        hipLaunchKernelGGL(k_seq_streams, dim3((unsigned)((S.n + 255) / 256)), dim3(256), 0, ctx->stream, view(S), S.n,
+                           d_sst);
+        HIP_TRY(ctx, hipGetLastError());
+        if (launch_zlen(ctx, d_sst, S.n, singles[k])) return -1;
+    }
+    for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+        const int64_t n = std::min(chunk, count - c0);
+        HIP_TRY(ctx, hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        const int64_t m = n * no;
+        hipLaunchKernelGGL(k_ncd_concat_streams, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, view(X),
+                           view(Y), d_idx, d_idx + chunk, n, both, d_cst);
+        HIP_TRY(ctx, hipGetLastError());
+        if (launch_zlen(ctx, d_cst, m, d_c)) return -1;
+        hipLaunchKernelGGL(k_ncd_finish_cached, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, d_c, d_cx,
+                           d_cy, d_idx, d_idx + chunk, n, both, d_v);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipMemcpyAsync(out + c0 * no, d_v, (size_t)m * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return 0;
+}
+
 // Compressed lengths of `n` device stream descriptors (persistent threads, per-thread scratch
 // slabs kept in the context; the head tables are zeroed once at allocation).
 int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out) {
     if (n <= 0) return 0;
-    const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 64);
+    const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 128);  // 2 waves / SIMD
     const int64_t threads = (want + 63) / 64 * 64;
     if (ctx->z_threads < threads) {
         if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
@@ -842,6 +893,7 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int no = both ? 2 : 1;
     const int cap = X->max_len + Y->max_len;
+    if (!aligned && X->n + (X == Y ? 0 : Y->n) <= count * no) return ncd_raw_cached(ctx, *X, *Y, xs, ys, count, both, out);
     Tracer tr;
     int64_t chunk = (int64_t)1 << 16;
     if (aligned) {

@@ -22,6 +22,9 @@
 #define __device__
 #define __forceinline__ inline
 #endif
+// The Huffman bookkeeping runs once per stream; keeping it out of line leaves the per-byte parse
+// loop its own small register set (higher occupancy for this latency-bound scalar code).
+#define ZL_COLD __attribute__((noinline))
 
 namespace taxi2 {
 namespace zl {
@@ -94,7 +97,7 @@ __host__ __device__ __forceinline__ bool smaller(const uint16_t* fc, const uint8
     return fc[n] < fc[m] || (fc[n] == fc[m] && depth[n] <= depth[m]);
 }
 
-__host__ __device__ inline void pqdownheap(Trees& t, const uint16_t* fc, int k) {
+__host__ __device__ ZL_COLD inline void pqdownheap(Trees& t, const uint16_t* fc, int k) {
     const int v = t.heap[k];
     int j = k << 1;
     while (j <= t.heap_len) {
@@ -107,7 +110,7 @@ __host__ __device__ inline void pqdownheap(Trees& t, const uint16_t* fc, int k) 
     t.heap[k] = (int16_t)v;
 }
 
-__host__ __device__ inline void gen_bitlen(Trees& t, int kind, uint16_t* fc, uint16_t* dl, int max_code) {
+__host__ __device__ ZL_COLD inline void gen_bitlen(Trees& t, int kind, uint16_t* fc, uint16_t* dl, int max_code) {
     const int max_length = kind == T_BL ? MAX_BL_BITS : MAX_BITS;
     for (int b = 0; b <= MAX_BITS; b++) t.bl_count[b] = 0;
     dl[t.heap[t.heap_max]] = 0;  // root
@@ -157,7 +160,7 @@ __host__ __device__ inline void gen_bitlen(Trees& t, int kind, uint16_t* fc, uin
 }
 
 // build_tree: returns max_code.
-__host__ __device__ inline int build_tree(Trees& t, int kind) {
+__host__ __device__ ZL_COLD inline int build_tree(Trees& t, int kind) {
     uint16_t* fc = kind == T_LIT ? t.lfc : kind == T_DIST ? t.dfc : t.bfc;
     uint16_t* dl = kind == T_LIT ? t.ldl : kind == T_DIST ? t.ddl : t.bdl;
     const int elems = kind == T_LIT ? L_CODES : kind == T_DIST ? D_CODES : BL_CODES;
@@ -201,7 +204,7 @@ __host__ __device__ inline int build_tree(Trees& t, int kind) {
     return max_code;
 }
 
-__host__ __device__ inline void scan_tree(Trees& t, uint16_t* dl, int max_code) {
+__host__ __device__ ZL_COLD inline void scan_tree(Trees& t, uint16_t* dl, int max_code) {
     int prevlen = -1, nextlen = dl[0], count = 0, max_count = 7, min_count = 4;
     if (nextlen == 0) max_count = 138, min_count = 3;
     dl[max_code + 1] = 0xffff;  // guard
@@ -229,7 +232,7 @@ __host__ __device__ inline void scan_tree(Trees& t, uint16_t* dl, int max_code) 
 }
 
 // Bytes of the final block (_tr_flush_block + bi_windup) for `stored_len` input bytes.
-__host__ __device__ inline int flush_block_bytes(Trees& t, int stored_len) {
+__host__ __device__ ZL_COLD inline int flush_block_bytes(Trees& t, int stored_len) {
     const int lmax = build_tree(t, T_LIT);
     const int dmax = build_tree(t, T_DIST);
     scan_tree(t, t.ldl, lmax);

@@ -26,7 +26,7 @@ constexpr size_t ZS_TREES = (sizeof(zl::Trees) + 255) / 256 * 256;
 constexpr size_t ZS_SLAB = ZS_WIN + ZS_PREV + ZS_TREES;
 constexpr size_t ZS_HEAD = (size_t)zl::HASH_SIZE * 2;
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, 4)
 k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, uint8_t* __restrict__ slabs,
        int32_t* __restrict__ out) {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -85,6 +85,42 @@ k_ncd_finish(const int32_t* __restrict__ c, int64_t m, double* __restrict__ out)
     const double c1 = c[t * 3], c2 = c[t * 3 + 1], c12 = c[t * 3 + 2];
     const double mn = c1 < c2 ? c1 : c2, mx = c1 < c2 ? c2 : c1;
     out[t] = (c12 - mn) / mx;
+}
+
+// Raw mode with per-sequence C(x): one stream per set member (C of the sequence alone) ...
+__global__ void __launch_bounds__(256) k_seq_streams(SetView S, int64_t n, ZStream* __restrict__ st) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    st[t] = ZStream{S.bytes + S.offs[t], nullptr, S.meta[t].x, 0};
+}
+
+// ... and one concatenation stream per (pair, orientation): x+y for (x, y), y+x for (y, x).
+__global__ void __launch_bounds__(256)
+k_ncd_concat_streams(SetView XS, SetView YS, const int64_t* __restrict__ xs, const int64_t* __restrict__ ys,
+                     int64_t n, int both, ZStream* __restrict__ st) {
+    const int no = both ? 2 : 1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * no) return;
+    const int64_t p = t / no;
+    const int o = (int)(t % no);
+    const int64_t a = xs[p], b = ys[p];
+    const uint8_t* sx = XS.bytes + XS.offs[a];
+    const uint8_t* sy = YS.bytes + YS.offs[b];
+    const int32_t lx = XS.meta[a].x, ly = YS.meta[b].x;
+    st[t] = o ? ZStream{sy, sx, ly, lx} : ZStream{sx, sy, lx, ly};
+}
+
+__global__ void __launch_bounds__(256)
+k_ncd_finish_cached(const int32_t* __restrict__ c12, const int32_t* __restrict__ cx, const int32_t* __restrict__ cy,
+                    const int64_t* __restrict__ xs, const int64_t* __restrict__ ys, int64_t n, int both,
+                    double* __restrict__ out) {
+    const int no = both ? 2 : 1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * no) return;
+    const int64_t p = t / no;
+    const double c1 = cx[xs[p]], c2 = cy[ys[p]], c = c12[t];
+    const double mn = c1 < c2 ? c1 : c2, mx = c1 < c2 ? c2 : c1;
+    out[t] = (c - mn) / mx;
 }
 
 // Raw-mode streams for taxi2_zlib_lengths: upper(x_a) (+ upper(y_b) when ys != nullptr).
