@@ -173,6 +173,36 @@ int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrow
                       const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
                       uint8_t* out, int64_t cap, int64_t* out_len);
 
+/* Same text for ragged rows (dereplicate.py:255-287 writers fed only the pairs that survive
+ * drop_excluded_pairs): row r holds tokens g in [row_start[r], row_start[r+1]) with column
+ * cols[g] in [0, ncols) and values vals[g][nm] (indices absolute, row_start[0] may be > 0).  Linear:
+ * row_pre[r] TAB col_pre[cols[g]] (TAB value){nm} LF per token; matrix: row_pre[r] (TAB value)* LF,
+ * nothing for an empty row. */
+int taxi2_format_ragged(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, const int64_t* row_start,
+                        const int32_t* cols, int64_t ncols, int nm, const uint8_t* row_pre, const int64_t* row_offs,
+                        const uint8_t* col_pre, const int64_t* col_offs, int decimals, const uint8_t* missing,
+                        int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len);
+
+/* ---- Dereplicate's greedy walk (dereplicate.py:180-196 drop_*_pairs, 289-337 find_replicates,
+ * 393-425 the lazily pulled chain that interleaves them) ------------------------------------ *
+ * Host-only (no context, no device): over precomputed distances d[n][n] of the ordered pairs of
+ * the length-filtered sequences (x100-adjusted; non-finite = None; diagonal unused), ids as codes
+ * id[n] in [0, n) (equal code <=> equal id) and unaligned lengths len[n].  Pairs are visited
+ * x-major; (i, j) is kept unless id[i] == id[j] or either id is excluded at that point; runs of
+ * kept pairs with equal x id form the groups of find_replicates.
+ *   row_kept[n]                   kept pairs per row;
+ *   kept_cols[kept_cap]           their columns, row-major (*n_kept in total);
+ *   line_idx[line_cap][3]         summary lines: (query row, included row, excluded row);
+ *   line_d[line_cap][2]           (included distance, excluded distance), NaN = None;
+ *   excluded[n]                   1 when the sequence's id ends up excluded.
+ * Returns 0; 1 when kept_cap < *n_kept or line_cap < *n_lines (outputs truncated; retry with
+ * those capacities); < 0 on bad arguments (-1 null pointer / negative n, -2 n > 2^31-1,
+ * -3 id code out of range). */
+int taxi2_dereplicate_walk(const double* d, int64_t n, const int64_t* id, const int64_t* len, double similarity,
+                           int64_t* row_kept, int32_t* kept_cols, int64_t kept_cap, int64_t* n_kept,
+                           int64_t* line_idx, double* line_d, int64_t line_cap, int64_t* n_lines,
+                           uint8_t* excluded);
+
 #ifdef __cplusplus
 }
 #endif

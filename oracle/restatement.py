@@ -280,3 +280,46 @@ def ncd(x: str, y: str) -> float:
     X, Y = x.upper(), y.upper()
     c1, c2, c12 = float(complexity(X)), float(complexity(Y)), float(complexity(X + Y))
     return (c12 - min(c1, c2)) / max(c1, c2)
+
+
+# --------------------------------------------------------------------------- A10
+class Replicate(NamedTuple):
+    query_id: str
+    query_length: int
+    included: tuple  # (id, length, distance)
+    excluded: tuple
+
+
+def dereplicate(items: list[tuple[str, int]], dist, similarity: float):
+    """Dereplicate's greedy walk (``tasks/dereplicate.py:180-196, 289-337, 393-425``), restated as
+    one explicit loop instead of the reference's lazily pulled generator chain.
+
+    ``items`` = (id, unaligned length) of the sequences that passed the length filter, in input
+    order; ``dist(i, j)`` = the (already x100-adjusted) distance of the ordered pair or None.
+    The reference pulls pair k of the x-major product only after every earlier pair has been
+    through ``find_replicates``, so each pair is tested against the exclusions made so far;
+    groups are runs of consecutive pairs with equal x id.  Returns (summary lines, the surviving
+    pairs in order, the final excluded set)."""
+    excluded: set[str] = set()
+    lines: list[Replicate] = []
+    kept: list[tuple[int, int]] = []
+    group = None  # [query id, query length, best (id, length, distance)]
+    for i, (xi, lx) in enumerate(items):
+        for j, (yj, ly) in enumerate(items):
+            if xi == yj or xi in excluded or yj in excluded:
+                continue
+            kept.append((i, j))
+            d = dist(i, j)
+            if group is None or group[0] != xi:
+                group = [xi, lx, (xi, lx, d)]  # the query, with its first pair's distance
+            if d is None or not d <= similarity:
+                continue
+            best = group[2]
+            if ly > best[1]:
+                inc, exc = (yj, ly, d), best
+                group[2] = inc
+            else:
+                inc, exc = best, (yj, ly, d)
+            excluded.add(exc[0])
+            lines.append(Replicate(group[0], group[1], inc, exc))
+    return lines, kept, excluded

@@ -14,7 +14,7 @@ import ctypes
 import os
 import threading
 from pathlib import Path
-from typing import Iterable, Sequence as Seq
+from typing import Iterable, NamedTuple, Sequence as Seq
 
 import numpy as np
 
@@ -41,6 +41,8 @@ EXPORTS = (
     "taxi2_ncd_pairs",
     "taxi2_zlib_lengths",
     "taxi2_format_rows",
+    "taxi2_format_ragged",
+    "taxi2_dereplicate_walk",
 )
 
 MODE_PREALIGNED = 0
@@ -90,6 +92,10 @@ _SIGNATURES = {
     "taxi2_zlib_lengths": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P]),
     "taxi2_format_rows": (_INT, [_P, _INT, _P, _I64, _I64, _INT, _P, _P, _P, _P, _INT, _P, _I32, _P, _I64,
                                  ctypes.POINTER(_I64)]),
+    "taxi2_format_ragged": (_INT, [_P, _INT, _P, _I64, _P, _P, _I64, _INT, _P, _P, _P, _P, _INT, _P, _I32, _P,
+                                   _I64, ctypes.POINTER(_I64)]),
+    "taxi2_dereplicate_walk": (_INT, [_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, ctypes.POINTER(_I64), _P,
+                                      _P, _I64, ctypes.POINTER(_I64), _P]),
 }
 
 _lib = None
@@ -429,7 +435,27 @@ class Engine:
         if v.ndim != 3:
             raise ValueError("vals must be (nrows, ncols, nm) (linear) or (nrows, ncols) (matrix)")
         nrows, ncols, nm = v.shape
+        return self._format(mode, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing)
 
+    def format_ragged(self, vals: np.ndarray, row_start, cols, row_pre, col_pre=None, *, ncols: int | None = None,
+                      decimals: int = 4, missing: str = "NA") -> bytes:
+        """Writer text for ragged rows (taxi2_format_ragged): row r formats tokens
+        [row_start[r], row_start[r+1]) of ``vals`` (ntok, nm) / (ntok,), token g at column cols[g];
+        linear with ``col_pre``, matrix rows otherwise (``ncols`` bounds cols then)."""
+        v = np.ascontiguousarray(vals, dtype=np.float64)
+        if v.ndim == 1:
+            v = v[:, None]
+        rs = np.ascontiguousarray(row_start, dtype=np.int64)
+        cs = np.ascontiguousarray(cols, dtype=np.int32)
+        nrows = len(rs) - 1
+        if nrows < 0 or len(cs) < rs[-1] or len(v) < rs[-1]:
+            raise ValueError("row_start must have nrows + 1 entries covering cols and vals")
+        mode = 0 if col_pre is not None else 1
+        if ncols is None:
+            ncols = len(col_pre) if col_pre is not None else (int(cs.max()) + 1 if len(cs) else 0)
+        return self._format(mode, v, nrows, rs, cs, ncols, v.shape[1], row_pre, col_pre, decimals, missing)
+
+    def _format(self, mode, v, nrows, rs, cs, ncols, nm, row_pre, col_pre, decimals, missing) -> bytes:
         def pack(strings):
             enc = [s.encode("utf-8") for s in strings]
             offs = np.zeros(len(enc) + 1, dtype=np.int64)
@@ -445,22 +471,32 @@ class Engine:
             raise ValueError("one column prefix per column")
         miss = missing.encode("utf-8")
         need = _I64(0)
-        cap = max(1, nrows * ncols * (nm * (decimals + 8) + 4) + int(ro[-1]) * ncols
-                  + (int(co[-1]) * nrows if mode == 0 else 0))
+        ntok = nrows * ncols if rs is None else int(rs[-1] - rs[0])
+        cap = max(1, ntok * (nm * (decimals + 8) + 4) + int(ro[-1]) * (ncols if rs is None else max(1, ntok))
+                  + (int(co[-1]) * nrows if mode == 0 and rs is None else 0)
+                  + (int(np.diff(co).max(initial=0)) * ntok if mode == 0 and rs is not None else 0))
+        name = "taxi2_format_rows" if rs is None else "taxi2_format_ragged"
         for _ in range(2):
             out = np.empty(cap, dtype=np.uint8)
+            cpre = (cb.ctypes.data if cb is not None else None, co.ctypes.data if co is not None else None)
             with self._lock:
-                rc = self._lib.taxi2_format_rows(
-                    self._ctx, mode, v.ctypes.data, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data,
-                    cb.ctypes.data if cb is not None else None, co.ctypes.data if co is not None else None,
-                    int(decimals), miss, len(miss), out.ctypes.data, cap, ctypes.byref(need),
-                )
+                if rs is None:
+                    rc = self._lib.taxi2_format_rows(
+                        self._ctx, mode, v.ctypes.data, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data, *cpre,
+                        int(decimals), miss, len(miss), out.ctypes.data, cap, ctypes.byref(need),
+                    )
+                else:
+                    rc = self._lib.taxi2_format_ragged(
+                        self._ctx, mode, v.ctypes.data, nrows, rs.ctypes.data, cs.ctypes.data, ncols, nm,
+                        rb.ctypes.data, ro.ctypes.data, *cpre, int(decimals), miss, len(miss), out.ctypes.data,
+                        cap, ctypes.byref(need),
+                    )
             if rc == 1:
                 cap = int(need.value)
                 continue
-            self._check(rc, "taxi2_format_rows")
+            self._check(rc, name)
             return out[: need.value].tobytes()
-        raise NativeError("taxi2_format_rows: output size changed between calls")
+        raise NativeError(f"{name}: output size changed between calls")
 
     def align_strings(self, x: SeqSet, y: SeqSet, xs, ys, scores=None, *, both: bool = False):
         """Gapped alignment strings: list of (ax, ay) per pair, plus the (y, x) alignment written
@@ -502,6 +538,51 @@ def tri_index(a: np.ndarray, b: np.ndarray, n: int) -> np.ndarray:
     a = np.asarray(a, dtype=np.int64)
     b = np.asarray(b, dtype=np.int64)
     return a * (2 * n - a - 1) // 2 + (b - a - 1)
+
+
+class Walk(NamedTuple):
+    """taxi2_dereplicate_walk result: kept pairs (row_kept per row, kept_cols row-major), summary
+    lines (query, included, excluded rows; their distances, NaN = None) and the excluded flags."""
+
+    row_kept: np.ndarray
+    kept_cols: np.ndarray
+    line_idx: np.ndarray
+    line_d: np.ndarray
+    excluded: np.ndarray
+
+
+def dereplicate_walk(d: np.ndarray, ids, lens, similarity: float) -> Walk:
+    """Dereplicate's greedy walk (taxi2_dereplicate_walk, host code in the engine library) over the
+    (n, n) adjusted distance matrix; ``ids`` = id codes (equal <=> equal id), ``lens`` = unaligned
+    lengths."""
+    lib = load_library()
+    d = np.ascontiguousarray(d, dtype=np.float64)
+    n = len(d)
+    if d.shape != (n, n):
+        raise ValueError("d must be square")
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    if len(ids) != n or len(lens) != n:
+        raise ValueError("one id code and one length per sequence")
+    row_kept = np.zeros(n, dtype=np.int64)
+    excluded = np.zeros(n, dtype=np.uint8)
+    kcap, lcap = max(1, min(n * max(n - 1, 0), 1 << 24)), max(1, n)
+    nk, nl = _I64(0), _I64(0)
+    for _ in range(2):
+        cols = np.empty(kcap, dtype=np.int32)
+        li = np.empty((lcap, 3), dtype=np.int64)
+        ld = np.empty((lcap, 2), dtype=np.float64)
+        rc = lib.taxi2_dereplicate_walk(d.ctypes.data, n, ids.ctypes.data, lens.ctypes.data, float(similarity),
+                                        row_kept.ctypes.data, cols.ctypes.data, kcap, ctypes.byref(nk),
+                                        li.ctypes.data, ld.ctypes.data, lcap, ctypes.byref(nl), excluded.ctypes.data)
+        if rc == 1:
+            kcap, lcap = max(kcap, int(nk.value)), max(lcap, int(nl.value))
+            continue
+        if rc != 0:
+            raise NativeError(f"taxi2_dereplicate_walk: bad arguments ({rc})")
+        k, m = int(nk.value), int(nl.value)
+        return Walk(row_kept, cols[:k], li[:m], ld[:m], excluded.astype(bool))
+    raise NativeError("taxi2_dereplicate_walk: result size changed between calls")
 
 
 def tri_pairs(n: int, k0: int = 0, count: int | None = None) -> tuple[np.ndarray, np.ndarray]:

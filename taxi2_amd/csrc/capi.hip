@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -973,10 +974,13 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
     return 0;
 }
 
-int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
-                      const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
-                      const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
-                      uint8_t* out, int64_t cap, int64_t* out_len) {
+}  // extern "C"
+
+// Shared by taxi2_format_rows (rectangular) and taxi2_format_ragged (rstart / cols non-null).
+static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
+                       const int64_t* rstart, const int32_t* cols, const uint8_t* row_pre, const int64_t* row_offs,
+                       const uint8_t* col_pre, const int64_t* col_offs, int decimals, const uint8_t* missing,
+                       int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len) {
     if (!ctx) return -1;
     if (!out_len || (nrows > 0 && (!vals || !row_pre || !row_offs))) return fail(ctx, "null argument");
     if (mode != 0 && mode != 1) return fail(ctx, "mode must be 0 (linear) or 1 (matrix)");
@@ -984,20 +988,33 @@ int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrow
     if (mode == 0 && (!col_pre || !col_offs)) return fail(ctx, "linear mode needs column prefixes");
     if (decimals < 0 || decimals > FMT_MAX_DECIMALS) return fail(ctx, "decimals must be in [0, %d]", FMT_MAX_DECIMALS);
     if (nrows < 0 || ncols < 0 || nm < 1 || missing_len < 0) return fail(ctx, "bad shape");
+    const bool ragged = rstart != nullptr;
     *out_len = 0;
-    if (nrows == 0 || ncols == 0) return 0;
-    const int64_t nv = nrows * ncols * nm;
+    if (nrows == 0) return 0;
+    int64_t ntok = nrows * ncols;
+    if (ragged) {
+        if (!cols) return fail(ctx, "ragged rows need a column list");
+        for (int64_t r = 0; r < nrows; ++r)
+            if (rstart[r + 1] < rstart[r]) return fail(ctx, "row starts must be non-decreasing");
+        ntok = rstart[nrows] - rstart[0];
+        for (int64_t g = rstart[0]; g < rstart[nrows]; ++g)
+            if (cols[g] < 0 || cols[g] >= ncols) return fail(ctx, "column %d out of range [0, %lld)", cols[g], (long long)ncols);
+    }
+    if (ntok == 0) return 0;
+    const double* v0 = ragged ? vals + rstart[0] * nm : vals;
+    const int64_t nv = ntok * nm;
     const double lim = std::ldexp(1.0, 63) / (double)pow10_u64(decimals);
     for (int64_t k = 0; k < nv; ++k)
-        if (std::isfinite(vals[k]) && !(std::fabs(vals[k]) < lim))
-            return fail(ctx, "value %g too large for fixed-point text with %d decimals", vals[k], decimals);
+        if (std::isfinite(v0[k]) && !(std::fabs(v0[k]) < lim))
+            return fail(ctx, "value %g too large for fixed-point text with %d decimals", v0[k], decimals);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int64_t rp = row_offs[nrows] - row_offs[0];
     const int64_t cp = mode == 0 ? col_offs[ncols] - col_offs[0] : 0;
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t b_vals = al(nv * 8), b_roffs = al((nrows + 1) * 8), b_coffs = al((ncols + 1) * 8),
-                 b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nrows * 8);
-    const size_t fixed = b_vals + b_roffs + b_coffs + b_rpre + b_cpre + b_miss + 2 * b_len;
+                 b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nrows * 8),
+                 b_rst = ragged ? al((nrows + 1) * 8) : 0, b_cols = ragged ? al(ntok * 4) : 0;
+    const size_t fixed = b_vals + b_roffs + b_coffs + b_rpre + b_cpre + b_miss + 2 * b_len + b_rst + b_cols;
     if (ensure(ctx, &ctx->d_fmt, &ctx->d_fmt_bytes, fixed)) return -1;
     char* base = (char*)ctx->d_fmt;
     double* d_vals = (double*)base;
@@ -1008,11 +1025,18 @@ int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrow
     uint8_t* d_miss = d_cpre + b_cpre;
     int64_t* d_rlen = (int64_t*)(d_miss + b_miss);
     int64_t* d_rbase = (int64_t*)((char*)d_rlen + b_len);
-    std::vector<int64_t> roffs(nrows + 1), coffs(mode == 0 ? ncols + 1 : 1, 0);
+    int64_t* d_rst = ragged ? (int64_t*)((char*)d_rbase + b_len) : nullptr;
+    int32_t* d_cols = ragged ? (int32_t*)((char*)d_rst + b_rst) : nullptr;
+    std::vector<int64_t> roffs(nrows + 1), coffs(mode == 0 ? ncols + 1 : 1, 0), rst(ragged ? nrows + 1 : 0);
     for (int64_t r = 0; r <= nrows; ++r) roffs[r] = row_offs[r] - row_offs[0];
     if (mode == 0)
         for (int64_t c = 0; c <= ncols; ++c) coffs[c] = col_offs[c] - col_offs[0];
-    HIP_TRY(ctx, hipMemcpyAsync(d_vals, vals, nv * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (ragged) {
+        for (int64_t r = 0; r <= nrows; ++r) rst[r] = rstart[r] - rstart[0];
+        HIP_TRY(ctx, hipMemcpyAsync(d_rst, rst.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_cols, cols + rstart[0], ntok * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(d_vals, v0, nv * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(d_roffs, roffs.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     if (rp) HIP_TRY(ctx, hipMemcpyAsync(d_rpre, row_pre + row_offs[0], rp, hipMemcpyHostToDevice, ctx->stream));
     if (mode == 0) {
@@ -1020,7 +1044,8 @@ int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrow
         if (cp) HIP_TRY(ctx, hipMemcpyAsync(d_cpre, col_pre + col_offs[0], cp, hipMemcpyHostToDevice, ctx->stream));
     }
     if (missing_len) HIP_TRY(ctx, hipMemcpyAsync(d_miss, missing, missing_len, hipMemcpyHostToDevice, ctx->stream));
-    FmtArgs a{mode, d_vals, nrows, ncols, nm, decimals, d_rpre, d_roffs, d_cpre, d_coffs, d_miss, missing_len};
+    FmtArgs a{mode, d_vals, nrows, ncols, nm, decimals, d_rpre, d_roffs, d_cpre, d_coffs, d_miss, missing_len,
+              d_rst, d_cols};
     hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, ctx->stream, a, d_rlen);
     HIP_TRY(ctx, hipGetLastError());
     std::vector<int64_t> rlen(nrows), rbase(nrows);
@@ -1042,6 +1067,81 @@ int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrow
     HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
+}
+
+extern "C" {
+
+int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
+                      const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                      const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                      uint8_t* out, int64_t cap, int64_t* out_len) {
+    return format_impl(ctx, mode, vals, nrows, ncols, nm, nullptr, nullptr, row_pre, row_offs, col_pre, col_offs,
+                       decimals, missing, missing_len, out, cap, out_len);
+}
+
+int taxi2_format_ragged(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, const int64_t* row_start,
+                        const int32_t* cols, int64_t ncols, int nm, const uint8_t* row_pre, const int64_t* row_offs,
+                        const uint8_t* col_pre, const int64_t* col_offs, int decimals, const uint8_t* missing,
+                        int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len) {
+    if (ctx && nrows > 0 && !row_start) return fail(ctx, "null row starts");
+    return format_impl(ctx, mode, vals, nrows, ncols, nm, row_start, cols, row_pre, row_offs, col_pre, col_offs,
+                       decimals, missing, missing_len, out, cap, out_len);
+}
+
+int taxi2_dereplicate_walk(const double* d, int64_t n, const int64_t* id, const int64_t* len, double similarity,
+                           int64_t* row_kept, int32_t* kept_cols, int64_t kept_cap, int64_t* n_kept,
+                           int64_t* line_idx, double* line_d, int64_t line_cap, int64_t* n_lines,
+                           uint8_t* excluded) {
+    if (n < 0 || !n_kept || !n_lines || (n > 0 && (!d || !id || !len || !row_kept || !excluded))) return -1;
+    if (n > INT32_MAX) return -2;
+    for (int64_t i = 0; i < n; ++i)
+        if (id[i] < 0 || id[i] >= n) return -3;
+    std::vector<uint8_t> ex((size_t)n, 0);  // by id code
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    int64_t nk = 0, nl = 0;
+    int64_t gcode = -1, gq = -1, best = -1;  // current group: id code, query row, longest member
+    double bestd = nan;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t xi = id[i];
+        int64_t kept_i = 0;
+        for (int64_t j = 0; j < n && !ex[xi]; ++j) {  // an excluded x drops the rest of its row
+            const int64_t yj = id[j];
+            if (yj == xi || ex[yj]) continue;
+            if (nk < kept_cap) kept_cols[nk] = (int32_t)j;
+            ++nk;
+            ++kept_i;
+            const double v = d[i * n + j];
+            const bool defined = std::isfinite(v);
+            if (gq < 0 || gcode != xi) {  // groupby(id_x): a new run of equal query ids
+                gcode = xi;
+                gq = i;
+                best = i;
+                bestd = defined ? v : nan;
+            }
+            if (!(defined && v <= similarity)) continue;
+            const bool longer = len[j] > len[best];
+            const int64_t inc = longer ? j : best, exc = longer ? best : j;
+            const double incd = longer ? v : bestd, excd = longer ? bestd : v;
+            ex[id[exc]] = 1;
+            if (nl < line_cap) {
+                line_idx[nl * 3] = gq;
+                line_idx[nl * 3 + 1] = inc;
+                line_idx[nl * 3 + 2] = exc;
+                line_d[nl * 2] = incd;
+                line_d[nl * 2 + 1] = excd;
+            }
+            ++nl;
+            if (longer) {
+                best = j;
+                bestd = v;
+            }
+        }
+        row_kept[i] = kept_i;
+    }
+    for (int64_t i = 0; i < n; ++i) excluded[i] = ex[id[i]];
+    *n_kept = nk;
+    *n_lines = nl;
+    return (nk > kept_cap || nl > line_cap) ? 1 : 0;
 }
 
 }  // extern "C"

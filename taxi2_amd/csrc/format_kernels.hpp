@@ -11,6 +11,8 @@
 // are block-scanned in LDS and each thread writes its token at the row base + its offset.
 //   linear: token (r, c) = row_pre[r] '\t' col_pre[c] ('\t' value(r, c, m)){nm} '\n'
 //   matrix: token (r, c) = [row_pre[r] if c == 0] '\t' value(r, c) ['\n' if c == ncols-1]
+// Ragged rows (taxi2_format_ragged, Dereplicate's surviving pairs): row r's tokens are an explicit
+// column list instead of every column.
 #pragma once
 #include <stdint.h>
 
@@ -83,7 +85,7 @@ __host__ __device__ inline int fmt_fixed(double x, int N, char* dst) {
 #ifdef __HIPCC__
 struct FmtArgs {
     int mode;  // 0 linear, 1 matrix
-    const double* vals;  // [nrows][ncols][nm]
+    const double* vals;  // [nrows][ncols][nm], or [rstart[nrows]][nm] when ragged
     int64_t nrows, ncols;
     int nm, decimals;
     const uint8_t* row_pre;
@@ -92,26 +94,49 @@ struct FmtArgs {
     const int64_t* col_offs;  // [ncols + 1]
     const uint8_t* missing;
     int missing_len;
+    // ragged rows (nullable): row r holds tokens g in [rstart[r], rstart[r+1]) (relative to the
+    // chunk), column cols[g]; rectangular otherwise (token t of row r = column t)
+    const int64_t* rstart;
+    const int32_t* cols;
 };
 
 __device__ __forceinline__ bool fmt_defined(double v) { return __builtin_isfinite(v); }
 
-__device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, int64_t c) {
-    const double* v = a.vals + (r * a.ncols + c) * a.nm;
+__device__ __forceinline__ int64_t fmt_ntok(const FmtArgs& a, int64_t r) {
+    return a.rstart ? a.rstart[r + 1] - a.rstart[r] : a.ncols;
+}
+
+// Token t of row r: its value slot g and column c.
+__device__ __forceinline__ void fmt_token_at(const FmtArgs& a, int64_t r, int64_t t, int64_t& g, int64_t& c) {
+    if (a.rstart) {
+        g = a.rstart[r] + t;
+        c = a.cols[g];
+    } else {
+        g = r * a.ncols + t;
+        c = t;
+    }
+}
+
+__device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, int64_t t, int64_t nt) {
+    int64_t g, c;
+    fmt_token_at(a, r, t, g, c);
+    const double* v = a.vals + g * a.nm;
     int64_t len = 0;
     if (a.mode == 0) {
         len = (a.row_offs[r + 1] - a.row_offs[r]) + 1 + (a.col_offs[c + 1] - a.col_offs[c]) + 1;  // + '\n'
         for (int m = 0; m < a.nm; ++m) len += 1 + (fmt_defined(v[m]) ? fmt_fixed(v[m], a.decimals, nullptr) : a.missing_len);
     } else {
-        if (c == 0) len += a.row_offs[r + 1] - a.row_offs[r];
+        if (t == 0) len += a.row_offs[r + 1] - a.row_offs[r];
         len += 1 + (fmt_defined(v[0]) ? fmt_fixed(v[0], a.decimals, nullptr) : a.missing_len);
-        if (c == a.ncols - 1) len += 1;
+        if (t == nt - 1) len += 1;
     }
     return len;
 }
 
-__device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int64_t c, char* o) {
-    const double* v = a.vals + (r * a.ncols + c) * a.nm;
+__device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int64_t t, int64_t nt, char* o) {
+    int64_t g, c;
+    fmt_token_at(a, r, t, g, c);
+    const double* v = a.vals + g * a.nm;
     auto put = [&](const uint8_t* s, int64_t n) {
         for (int64_t k = 0; k < n; ++k) *o++ = (char)s[k];
     };
@@ -127,9 +152,9 @@ __device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int
         for (int m = 0; m < a.nm; ++m) value(v[m]);
         *o++ = '\n';
     } else {
-        if (c == 0) put(a.row_pre + a.row_offs[r], a.row_offs[r + 1] - a.row_offs[r]);
+        if (t == 0) put(a.row_pre + a.row_offs[r], a.row_offs[r + 1] - a.row_offs[r]);
         value(v[0]);
-        if (c == a.ncols - 1) *o++ = '\n';
+        if (t == nt - 1) *o++ = '\n';
     }
 }
 
@@ -139,8 +164,9 @@ constexpr int FMT_BLOCK = 256;
 __global__ void __launch_bounds__(FMT_BLOCK) k_fmt_row_len(FmtArgs a, int64_t* __restrict__ row_len) {
     __shared__ int64_t red[FMT_BLOCK];
     const int64_t r = blockIdx.x;
+    const int64_t nt = fmt_ntok(a, r);
     int64_t s = 0;
-    for (int64_t c = threadIdx.x; c < a.ncols; c += FMT_BLOCK) s += fmt_token_len(a, r, c);
+    for (int64_t t = threadIdx.x; t < nt; t += FMT_BLOCK) s += fmt_token_len(a, r, t, nt);
     red[threadIdx.x] = s;
     __syncthreads();
     for (int w = FMT_BLOCK / 2; w > 0; w >>= 1) {
@@ -155,10 +181,11 @@ __global__ void __launch_bounds__(FMT_BLOCK)
 k_fmt_rows(FmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out) {
     __shared__ int64_t scan[FMT_BLOCK];
     const int64_t r = blockIdx.x;
+    const int64_t nt = fmt_ntok(a, r);
     int64_t base = row_base[r];
-    for (int64_t c0 = 0; c0 < a.ncols; c0 += FMT_BLOCK) {
-        const int64_t c = c0 + threadIdx.x;
-        const int64_t len = c < a.ncols ? fmt_token_len(a, r, c) : 0;
+    for (int64_t t0 = 0; t0 < nt; t0 += FMT_BLOCK) {
+        const int64_t t = t0 + threadIdx.x;
+        const int64_t len = t < nt ? fmt_token_len(a, r, t, nt) : 0;
         scan[threadIdx.x] = len;
         __syncthreads();
         for (int w = 1; w < FMT_BLOCK; w <<= 1) {  // inclusive Hillis-Steele scan
@@ -167,7 +194,7 @@ k_fmt_rows(FmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ o
             scan[threadIdx.x] += add;
             __syncthreads();
         }
-        if (c < a.ncols) fmt_token_write(a, r, c, out + base + scan[threadIdx.x] - len);
+        if (t < nt) fmt_token_write(a, r, t, nt, out + base + scan[threadIdx.x] - len);
         base += scan[FMT_BLOCK - 1];
         __syncthreads();
     }
