@@ -183,6 +183,38 @@ int taxi2_format_ragged(taxi2_ctx* ctx, int mode, const double* vals, int64_t nr
                         const uint8_t* col_pre, const int64_t* col_offs, int decimals, const uint8_t* missing,
                         int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len);
 
+/* ---- versusAll summary.tsv text (versus_all.py:278-350 SummaryHandler, fed at :754-768) ----- *
+ * One line per ordered pair (r, c) of vals[nrows][ncols][nm] (host, f64, NaN/inf -> missing):
+ *   row_pre[r] TAB col_pre[c] (TAB value){nm} row_suf[2r] col_suf[2c] row_suf[2r+1] col_suf[2c+1]
+ *   TAB label LF
+ * where row_suf / col_suf are 2 strings per row / column (offsets [2n + 1]) that carry their own
+ * leading TABs (entry 2k: "\t" + extras values; entry 2k+1: "\tgenus\tspecies"), and label is
+ * labels[k] (offsets [6]: "no info", "intra-species", "inter-species", "intra-genus",
+ * "inter-genus") for k = SubsetDistance.get_comparison_type (versus_all.py:255-271) of
+ * (genus equal?, species equal?) from row_codes / col_codes [n][2] = (genus code, species code)
+ * -- equal code <=> same subset (a sequence missing from a partition gets a code of its own that
+ * equals every other missing one: None == None) -- or None when has_genera / has_species is 0.
+ * Values as in taxi2_format_rows; returns 1 when cap < *out_len. */
+int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int64_t ncols, int nm,
+                         const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                         const int64_t* col_offs, const uint8_t* row_suf, const int64_t* row_suf_offs,
+                         const uint8_t* col_suf, const int64_t* col_suf_offs, const int32_t* row_codes,
+                         const int32_t* col_codes, int has_genera, int has_species, const uint8_t* labels,
+                         const int64_t* label_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                         uint8_t* out, int64_t cap, int64_t* out_len);
+
+/* ---- subset aggregation (versus_all.py:57-96 SimpleAggregator / DistanceAggregator, fed by
+ * _aggregate_distances :617-640) ------------------------------------------------------------ *
+ * Host-only (no context).  d[n][n][m]: the (x100-adjusted) ordered-pair values, non-finite = None;
+ * code[n] in [0, ns): each sequence's subset (the partition's value, None included, numbered in
+ * first-appearance order = the aggregators' key order).  For key (a, b) and metric k the values of
+ * the pairs with code[x] == a, code[y] == b are accumulated in x-major order, None skipped,
+ * exactly as SimpleAggregator.add: sum += v, min (from +inf), max (from 0.0), count.
+ * Outputs sum / min / max / count [ns][ns][m].  threads <= 0: up to 16; keys are split by their
+ * x subset, so each key's summation order is the reference's. */
+int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* code, int32_t ns, double* sum,
+                           double* mn, double* mx, int64_t* count, int threads);
+
 /* ---- Dereplicate's greedy walk (dereplicate.py:180-196 drop_*_pairs, 289-337 find_replicates,
  * 393-425 the lazily pulled chain that interleaves them) ------------------------------------ *
  * Host-only (no context, no device): over precomputed distances d[n][n] of the ordered pairs of

@@ -323,3 +323,29 @@ def dereplicate(items: list[tuple[str, int]], dist, similarity: float):
             excluded.add(exc[0])
             lines.append(Replicate(group[0], group[1], inc, exc))
     return lines, kept, excluded
+
+
+# --------------------------------------------------------------------------- A11
+def subset_aggregates(ids: list[str], partition: dict, value, n_metrics: int) -> dict:
+    """VersusAll's per-partition ``DistanceAggregator`` (``tasks/versus_all.py:57-96, 617-640``):
+    over the ordered product x-major, key (partition.get(id_x), partition.get(id_y)) in first-seen
+    order; per metric ``[sum, min, max, count]`` with min from +inf, max from 0.0, None skipped and
+    the sum accumulated in visiting order.  ``value(i, j, k)`` -> float or None."""
+    aggs: dict = {}
+    n = len(ids)
+    for i in range(n):
+        for j in range(n):
+            key = (partition.get(ids[i], None), partition.get(ids[j], None))
+            acc = aggs.setdefault(key, [[0.0, math.inf, 0.0, 0] for _ in range(n_metrics)])
+            for k in range(n_metrics):
+                v = value(i, j, k)
+                if v is None:
+                    continue
+                a = acc[k]
+                a[0] += v
+                if v < a[1]:
+                    a[1] = v
+                if v > a[2]:
+                    a[2] = v
+                a[3] += 1
+    return aggs

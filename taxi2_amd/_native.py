@@ -42,6 +42,8 @@ EXPORTS = (
     "taxi2_zlib_lengths",
     "taxi2_format_rows",
     "taxi2_format_ragged",
+    "taxi2_format_summary",
+    "taxi2_subset_aggregate",
     "taxi2_dereplicate_walk",
 )
 
@@ -94,6 +96,9 @@ _SIGNATURES = {
                                  ctypes.POINTER(_I64)]),
     "taxi2_format_ragged": (_INT, [_P, _INT, _P, _I64, _P, _P, _I64, _INT, _P, _P, _P, _P, _INT, _P, _I32, _P,
                                    _I64, ctypes.POINTER(_I64)]),
+    "taxi2_format_summary": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _INT, _INT,
+                                    _P, _P, _INT, _P, _I32, _P, _I64, ctypes.POINTER(_I64)]),
+    "taxi2_subset_aggregate": (_INT, [_P, _I64, _INT, _P, _I32, _P, _P, _P, _P, _INT]),
     "taxi2_dereplicate_walk": (_INT, [_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, ctypes.POINTER(_I64), _P,
                                       _P, _I64, ctypes.POINTER(_I64), _P]),
 }
@@ -455,32 +460,53 @@ class Engine:
             ncols = len(col_pre) if col_pre is not None else (int(cs.max()) + 1 if len(cs) else 0)
         return self._format(mode, v, nrows, rs, cs, ncols, v.shape[1], row_pre, col_pre, decimals, missing)
 
-    def _format(self, mode, v, nrows, rs, cs, ncols, nm, row_pre, col_pre, decimals, missing) -> bytes:
-        def pack(strings):
-            enc = [s.encode("utf-8") for s in strings]
-            offs = np.zeros(len(enc) + 1, dtype=np.int64)
-            if enc:
-                offs[1:] = np.cumsum([len(e) for e in enc])
-            return np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8), offs
+    def format_summary(self, vals: np.ndarray, row_pre, col_pre, row_suf, col_suf, row_codes, col_codes, *,
+                       has_genera: bool, has_species: bool, decimals: int = 4, missing: str = "NA") -> bytes:
+        """summary.tsv lines (taxi2_format_summary) for ``vals`` (nrows, ncols, nm): row_suf / col_suf
+        = 2 strings per row / column (extras with leading TABs; TAB genus TAB species),
+        row_codes / col_codes (n, 2) = (genus, species) subset codes."""
+        v = np.ascontiguousarray(vals, dtype=np.float64)
+        nrows, ncols, nm = v.shape
+        rsb, rso = pack_strings(row_suf)
+        csb, cso = pack_strings(col_suf)
+        if len(rso) != 2 * nrows + 1 or len(cso) != 2 * ncols + 1:
+            raise ValueError("two suffix strings per row and per column")
+        rc_ = np.ascontiguousarray(row_codes, dtype=np.int32).reshape(nrows, 2)
+        cc_ = np.ascontiguousarray(col_codes, dtype=np.int32).reshape(ncols, 2)
+        lb, lo = pack_strings(COMPARISON_LABELS)
+        extra = (rsb, rso, csb, cso, rc_, cc_, int(bool(has_genera)), int(bool(has_species)), lb, lo)
+        sfx = int(rso[-1]) * ncols + int(cso[-1]) * nrows + nrows * ncols * 16
+        return self._format(2, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing, extra, sfx)
 
+    def _format(self, mode, v, nrows, rs, cs, ncols, nm, row_pre, col_pre, decimals, missing, summary=None,
+                extra_cap: int = 0) -> bytes:
+        pack = pack_strings
         rb, ro = pack(row_pre)
         if len(ro) != nrows + 1:
             raise ValueError("one row prefix per row")
-        cb, co = pack(col_pre) if mode == 0 else (None, None)
-        if mode == 0 and len(co) != ncols + 1:
+        cb, co = pack(col_pre) if mode != 1 else (None, None)
+        if mode != 1 and len(co) != ncols + 1:
             raise ValueError("one column prefix per column")
         miss = missing.encode("utf-8")
         need = _I64(0)
         ntok = nrows * ncols if rs is None else int(rs[-1] - rs[0])
         cap = max(1, ntok * (nm * (decimals + 8) + 4) + int(ro[-1]) * (ncols if rs is None else max(1, ntok))
-                  + (int(co[-1]) * nrows if mode == 0 and rs is None else 0)
-                  + (int(np.diff(co).max(initial=0)) * ntok if mode == 0 and rs is not None else 0))
-        name = "taxi2_format_rows" if rs is None else "taxi2_format_ragged"
+                  + (int(co[-1]) * nrows if mode != 1 and rs is None else 0)
+                  + (int(np.diff(co).max(initial=0)) * ntok if mode == 0 and rs is not None else 0) + extra_cap)
+        name = "taxi2_format_summary" if summary else "taxi2_format_rows" if rs is None else "taxi2_format_ragged"
         for _ in range(2):
             out = np.empty(cap, dtype=np.uint8)
             cpre = (cb.ctypes.data if cb is not None else None, co.ctypes.data if co is not None else None)
             with self._lock:
-                if rs is None:
+                if summary is not None:
+                    rsb, rso, csb, cso, rc_, cc_, hg, hs, lb, lo = summary
+                    rc = self._lib.taxi2_format_summary(
+                        self._ctx, v.ctypes.data, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data, *cpre,
+                        rsb.ctypes.data, rso.ctypes.data, csb.ctypes.data, cso.ctypes.data, rc_.ctypes.data,
+                        cc_.ctypes.data, hg, hs, lb.ctypes.data, lo.ctypes.data, int(decimals), miss, len(miss),
+                        out.ctypes.data, cap, ctypes.byref(need),
+                    )
+                elif rs is None:
                     rc = self._lib.taxi2_format_rows(
                         self._ctx, mode, v.ctypes.data, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data, *cpre,
                         int(decimals), miss, len(miss), out.ctypes.data, cap, ctypes.byref(need),
@@ -538,6 +564,46 @@ def tri_index(a: np.ndarray, b: np.ndarray, n: int) -> np.ndarray:
     a = np.asarray(a, dtype=np.int64)
     b = np.asarray(b, dtype=np.int64)
     return a * (2 * n - a - 1) // 2 + (b - a - 1)
+
+
+def pack_strings(strings) -> tuple[np.ndarray, np.ndarray]:
+    """UTF-8 bytes (NUL-terminated buffer) + int64 offsets [n + 1] of a list of str."""
+    enc = [s.encode("utf-8") for s in strings]
+    offs = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        offs[1:] = np.cumsum([len(e) for e in enc])
+    return np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8), offs
+
+
+COMPARISON_LABELS = ("no info", "intra-species", "inter-species", "intra-genus", "inter-genus")
+
+
+class Aggregates(NamedTuple):
+    """taxi2_subset_aggregate result, each [ns][ns][m]."""
+
+    sum: np.ndarray
+    min: np.ndarray
+    max: np.ndarray
+    count: np.ndarray
+
+
+def subset_aggregate(d: np.ndarray, code, ns: int, threads: int = 0) -> Aggregates:
+    """SimpleAggregator state per (subset x, subset y, metric) over the (n, n, m) adjusted values
+    (taxi2_subset_aggregate: x-major summation order, host code in the engine library)."""
+    lib = load_library()
+    d = np.ascontiguousarray(d, dtype=np.float64)
+    if d.ndim != 3 or d.shape[0] != d.shape[1]:
+        raise ValueError("d must be (n, n, m)")
+    n, _, m = d.shape
+    code = np.ascontiguousarray(code, dtype=np.int32)
+    if len(code) != n:
+        raise ValueError("one subset code per sequence")
+    out = [np.empty((ns, ns, m)) for _ in range(3)] + [np.empty((ns, ns, m), dtype=np.int64)]
+    rc = lib.taxi2_subset_aggregate(d.ctypes.data, n, m, code.ctypes.data, ns, *[o.ctypes.data for o in out],
+                                    int(threads))
+    if rc != 0:
+        raise NativeError(f"taxi2_subset_aggregate: bad arguments ({rc})")
+    return Aggregates(*out)
 
 
 class Walk(NamedTuple):

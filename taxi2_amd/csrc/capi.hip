@@ -11,6 +11,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/taxi2_mi355x.h"
@@ -976,16 +977,36 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
 
 }  // extern "C"
 
-// Shared by taxi2_format_rows (rectangular) and taxi2_format_ragged (rstart / cols non-null).
+// Summary-mode extras (taxi2_format_summary).
+struct SummaryHost {
+    const uint8_t* rsuf;
+    const int64_t* rsuf_offs;
+    const uint8_t* csuf;
+    const int64_t* csuf_offs;
+    const int32_t* rcode;
+    const int32_t* ccode;
+    int has_g, has_s;
+    const uint8_t* lab;
+    const int64_t* lab_offs;
+};
+
+// Shared by taxi2_format_rows (rectangular), taxi2_format_ragged (rstart / cols non-null) and
+// taxi2_format_summary (mode 2, sm non-null).
 static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
                        const int64_t* rstart, const int32_t* cols, const uint8_t* row_pre, const int64_t* row_offs,
                        const uint8_t* col_pre, const int64_t* col_offs, int decimals, const uint8_t* missing,
-                       int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len) {
+                       int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len,
+                       const SummaryHost* sm = nullptr) {
     if (!ctx) return -1;
     if (!out_len || (nrows > 0 && (!vals || !row_pre || !row_offs))) return fail(ctx, "null argument");
-    if (mode != 0 && mode != 1) return fail(ctx, "mode must be 0 (linear) or 1 (matrix)");
+    if (mode < 0 || mode > 2 || (mode == 2) != (sm != nullptr))
+        return fail(ctx, "mode must be 0 (linear) or 1 (matrix)");
     if (mode == 1 && nm != 1) return fail(ctx, "matrix mode formats one metric");
-    if (mode == 0 && (!col_pre || !col_offs)) return fail(ctx, "linear mode needs column prefixes");
+    if (mode != 1 && (!col_pre || !col_offs)) return fail(ctx, "linear mode needs column prefixes");
+    if (sm && nrows > 0 && ncols > 0 &&
+        (!sm->rsuf || !sm->rsuf_offs || !sm->csuf || !sm->csuf_offs || !sm->rcode || !sm->ccode || !sm->lab ||
+         !sm->lab_offs))
+        return fail(ctx, "null summary argument");
     if (decimals < 0 || decimals > FMT_MAX_DECIMALS) return fail(ctx, "decimals must be in [0, %d]", FMT_MAX_DECIMALS);
     if (nrows < 0 || ncols < 0 || nm < 1 || missing_len < 0) return fail(ctx, "bad shape");
     const bool ragged = rstart != nullptr;
@@ -1009,12 +1030,19 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
             return fail(ctx, "value %g too large for fixed-point text with %d decimals", v0[k], decimals);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int64_t rp = row_offs[nrows] - row_offs[0];
-    const int64_t cp = mode == 0 ? col_offs[ncols] - col_offs[0] : 0;
+    const int64_t cp = mode != 1 ? col_offs[ncols] - col_offs[0] : 0;
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const int64_t rs_b = sm ? sm->rsuf_offs[2 * nrows] - sm->rsuf_offs[0] : 0;
+    const int64_t cs_b = sm ? sm->csuf_offs[2 * ncols] - sm->csuf_offs[0] : 0;
+    const int64_t lab_b = sm ? sm->lab_offs[5] - sm->lab_offs[0] : 0;
     const size_t b_vals = al(nv * 8), b_roffs = al((nrows + 1) * 8), b_coffs = al((ncols + 1) * 8),
                  b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nrows * 8),
-                 b_rst = ragged ? al((nrows + 1) * 8) : 0, b_cols = ragged ? al(ntok * 4) : 0;
-    const size_t fixed = b_vals + b_roffs + b_coffs + b_rpre + b_cpre + b_miss + 2 * b_len + b_rst + b_cols;
+                 b_rst = ragged ? al((nrows + 1) * 8) : 0, b_cols = ragged ? al(ntok * 4) : 0,
+                 b_rsuf = sm ? al(rs_b + 1) + al((2 * nrows + 1) * 8) + al(2 * nrows * 4) : 0,
+                 b_csuf = sm ? al(cs_b + 1) + al((2 * ncols + 1) * 8) + al(2 * ncols * 4) : 0,
+                 b_lab = sm ? al(lab_b + 1) + al(6 * 8) : 0;
+    const size_t fixed = b_vals + b_roffs + b_coffs + b_rpre + b_cpre + b_miss + 2 * b_len + b_rst + b_cols +
+                         b_rsuf + b_csuf + b_lab;
     if (ensure(ctx, &ctx->d_fmt, &ctx->d_fmt_bytes, fixed)) return -1;
     char* base = (char*)ctx->d_fmt;
     double* d_vals = (double*)base;
@@ -1026,11 +1054,42 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
     int64_t* d_rlen = (int64_t*)(d_miss + b_miss);
     int64_t* d_rbase = (int64_t*)((char*)d_rlen + b_len);
     int64_t* d_rst = ragged ? (int64_t*)((char*)d_rbase + b_len) : nullptr;
-    int32_t* d_cols = ragged ? (int32_t*)((char*)d_rst + b_rst) : nullptr;
-    std::vector<int64_t> roffs(nrows + 1), coffs(mode == 0 ? ncols + 1 : 1, 0), rst(ragged ? nrows + 1 : 0);
+    int32_t* d_cols = ragged ? (int32_t*)((char*)d_rbase + b_len + b_rst) : nullptr;
+    char* sbase = (char*)d_rbase + b_len + b_rst + b_cols;  // summary extras
+    std::vector<int64_t> roffs(nrows + 1), coffs(mode != 1 ? ncols + 1 : 1, 0), rst(ragged ? nrows + 1 : 0);
     for (int64_t r = 0; r <= nrows; ++r) roffs[r] = row_offs[r] - row_offs[0];
-    if (mode == 0)
+    if (mode != 1)
         for (int64_t c = 0; c <= ncols; ++c) coffs[c] = col_offs[c] - col_offs[0];
+    uint8_t *d_rsuf = nullptr, *d_csuf = nullptr, *d_lab = nullptr;
+    int64_t *d_rsoffs = nullptr, *d_csoffs = nullptr, *d_laboffs = nullptr;
+    int32_t *d_rcode = nullptr, *d_ccode = nullptr;
+    std::vector<int64_t> rso, cso, lo;
+    if (sm) {
+        d_rsuf = (uint8_t*)sbase;
+        d_rsoffs = (int64_t*)(sbase + al(rs_b + 1));
+        d_rcode = (int32_t*)((char*)d_rsoffs + al((2 * nrows + 1) * 8));
+        sbase += b_rsuf;
+        d_csuf = (uint8_t*)sbase;
+        d_csoffs = (int64_t*)(sbase + al(cs_b + 1));
+        d_ccode = (int32_t*)((char*)d_csoffs + al((2 * ncols + 1) * 8));
+        sbase += b_csuf;
+        d_lab = (uint8_t*)sbase;
+        d_laboffs = (int64_t*)(sbase + al(lab_b + 1));
+        rso.resize(2 * nrows + 1);
+        cso.resize(2 * ncols + 1);
+        lo.resize(6);
+        for (int64_t k = 0; k <= 2 * nrows; ++k) rso[k] = sm->rsuf_offs[k] - sm->rsuf_offs[0];
+        for (int64_t k = 0; k <= 2 * ncols; ++k) cso[k] = sm->csuf_offs[k] - sm->csuf_offs[0];
+        for (int k = 0; k < 6; ++k) lo[k] = sm->lab_offs[k] - sm->lab_offs[0];
+        if (rs_b) HIP_TRY(ctx, hipMemcpyAsync(d_rsuf, sm->rsuf + sm->rsuf_offs[0], rs_b, hipMemcpyHostToDevice, ctx->stream));
+        if (cs_b) HIP_TRY(ctx, hipMemcpyAsync(d_csuf, sm->csuf + sm->csuf_offs[0], cs_b, hipMemcpyHostToDevice, ctx->stream));
+        if (lab_b) HIP_TRY(ctx, hipMemcpyAsync(d_lab, sm->lab + sm->lab_offs[0], lab_b, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_rsoffs, rso.data(), rso.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_csoffs, cso.data(), cso.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_laboffs, lo.data(), 6 * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_rcode, sm->rcode, 2 * nrows * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_ccode, sm->ccode, 2 * ncols * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
     if (ragged) {
         for (int64_t r = 0; r <= nrows; ++r) rst[r] = rstart[r] - rstart[0];
         HIP_TRY(ctx, hipMemcpyAsync(d_rst, rst.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -1039,13 +1098,14 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
     HIP_TRY(ctx, hipMemcpyAsync(d_vals, v0, nv * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(d_roffs, roffs.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     if (rp) HIP_TRY(ctx, hipMemcpyAsync(d_rpre, row_pre + row_offs[0], rp, hipMemcpyHostToDevice, ctx->stream));
-    if (mode == 0) {
+    if (mode != 1) {
         HIP_TRY(ctx, hipMemcpyAsync(d_coffs, coffs.data(), (ncols + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
         if (cp) HIP_TRY(ctx, hipMemcpyAsync(d_cpre, col_pre + col_offs[0], cp, hipMemcpyHostToDevice, ctx->stream));
     }
     if (missing_len) HIP_TRY(ctx, hipMemcpyAsync(d_miss, missing, missing_len, hipMemcpyHostToDevice, ctx->stream));
     FmtArgs a{mode, d_vals, nrows, ncols, nm, decimals, d_rpre, d_roffs, d_cpre, d_coffs, d_miss, missing_len,
-              d_rst, d_cols};
+              d_rst, d_cols, d_rsuf, d_rsoffs, d_csuf, d_csoffs, d_rcode, d_ccode, sm ? sm->has_g : 0,
+              sm ? sm->has_s : 0, d_lab, d_laboffs};
     hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, ctx->stream, a, d_rlen);
     HIP_TRY(ctx, hipGetLastError());
     std::vector<int64_t> rlen(nrows), rbase(nrows);
@@ -1086,6 +1146,61 @@ int taxi2_format_ragged(taxi2_ctx* ctx, int mode, const double* vals, int64_t nr
     if (ctx && nrows > 0 && !row_start) return fail(ctx, "null row starts");
     return format_impl(ctx, mode, vals, nrows, ncols, nm, row_start, cols, row_pre, row_offs, col_pre, col_offs,
                        decimals, missing, missing_len, out, cap, out_len);
+}
+
+int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int64_t ncols, int nm,
+                         const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                         const int64_t* col_offs, const uint8_t* row_suf, const int64_t* row_suf_offs,
+                         const uint8_t* col_suf, const int64_t* col_suf_offs, const int32_t* row_codes,
+                         const int32_t* col_codes, int has_genera, int has_species, const uint8_t* labels,
+                         const int64_t* label_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                         uint8_t* out, int64_t cap, int64_t* out_len) {
+    const SummaryHost sm{row_suf, row_suf_offs, col_suf, col_suf_offs, row_codes, col_codes,
+                         has_genera ? 1 : 0, has_species ? 1 : 0, labels, label_offs};
+    return format_impl(ctx, 2, vals, nrows, ncols, nm, nullptr, nullptr, row_pre, row_offs, col_pre, col_offs,
+                       decimals, missing, missing_len, out, cap, out_len, &sm);
+}
+
+int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* code, int32_t ns, double* sum,
+                           double* mn, double* mx, int64_t* count, int threads) {
+    if (n < 0 || m < 1 || ns < 0 || (n > 0 && (!d || !code || !sum || !mn || !mx || !count))) return -1;
+    for (int64_t i = 0; i < n; ++i)
+        if (code[i] < 0 || code[i] >= ns) return -3;
+    const int64_t nk = (int64_t)ns * ns * m;
+    for (int64_t k = 0; k < nk; ++k) {  // SimpleAggregator.__init__
+        sum[k] = 0.0;
+        mn[k] = std::numeric_limits<double>::infinity();
+        mx[k] = 0.0;
+        count[k] = 0;
+    }
+    if (threads <= 0) threads = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, ns));
+    // Worker t owns the keys whose x subset a has a % threads == t, and visits its rows in ascending
+    // x, each row in ascending y: every key sees its values in the reference's x-major order.
+    auto work = [&](int t) {
+        for (int64_t x = 0; x < n; ++x) {
+            const int64_t a = code[x];
+            if (a % threads != t) continue;
+            const double* row = d + x * n * m;
+            for (int64_t y = 0; y < n; ++y) {
+                const int64_t base = (a * ns + code[y]) * m;
+                for (int k = 0; k < m; ++k) {
+                    const double v = row[y * m + k];
+                    if (!std::isfinite(v)) continue;  // None
+                    const int64_t q = base + k;
+                    sum[q] += v;
+                    if (v < mn[q]) mn[q] = v;
+                    if (v > mx[q]) mx[q] = v;
+                    ++count[q];
+                }
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    return 0;
 }
 
 int taxi2_dereplicate_walk(const double* d, int64_t n, const int64_t* id, const int64_t* len, double similarity,

@@ -84,7 +84,7 @@ __host__ __device__ inline int fmt_fixed(double x, int N, char* dst) {
 
 #ifdef __HIPCC__
 struct FmtArgs {
-    int mode;  // 0 linear, 1 matrix
+    int mode;  // 0 linear, 1 matrix, 2 summary
     const double* vals;  // [nrows][ncols][nm], or [rstart[nrows]][nm] when ragged
     int64_t nrows, ncols;
     int nm, decimals;
@@ -98,9 +98,35 @@ struct FmtArgs {
     // chunk), column cols[g]; rectangular otherwise (token t of row r = column t)
     const int64_t* rstart;
     const int32_t* cols;
+    // mode 2 (versusAll summary.tsv, versus_all.py:278-350 SummaryHandler): after the values, row
+    // suffix 2r (x extras), column suffix 2c (y extras), row suffix 2r+1 (x genus, species),
+    // column suffix 2c+1 (y genus, species), each carrying its own leading TABs, then TAB and the
+    // comparison label chosen from the (genus, species) codes (equal code = same subset)
+    const uint8_t* rsuf;
+    const int64_t* rsuf_offs;  // [2 * nrows + 1]
+    const uint8_t* csuf;
+    const int64_t* csuf_offs;  // [2 * ncols + 1]
+    const int32_t* rcode;  // [2 * nrows]: genus code, species code
+    const int32_t* ccode;  // [2 * ncols]
+    int has_g, has_s;
+    const uint8_t* lab;
+    const int64_t* lab_offs;  // [6]: no info, intra-species, inter-species, intra-genus, inter-genus
 };
 
 __device__ __forceinline__ bool fmt_defined(double v) { return __builtin_isfinite(v); }
+
+// SubsetDistance.get_comparison_type (versus_all.py:255-271): (same genus?, same species?) with
+// None when that partition is absent.
+__device__ __forceinline__ int fmt_comparison(const FmtArgs& a, int64_t r, int64_t c) {
+    const int sg = a.has_g ? (a.rcode[2 * r] == a.ccode[2 * c] ? 1 : 0) : -1;
+    const int ss = a.has_s ? (a.rcode[2 * r + 1] == a.ccode[2 * c + 1] ? 1 : 0) : -1;
+    if (sg == 0) return 4;
+    if (ss == 1) return 1;
+    if (ss == 0) return 2;
+    return sg == 1 ? 3 : 0;
+}
+
+__device__ __forceinline__ int64_t fmt_span(const int64_t* offs, int64_t k) { return offs[k + 1] - offs[k]; }
 
 __device__ __forceinline__ int64_t fmt_ntok(const FmtArgs& a, int64_t r) {
     return a.rstart ? a.rstart[r + 1] - a.rstart[r] : a.ncols;
@@ -122,9 +148,12 @@ __device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, in
     fmt_token_at(a, r, t, g, c);
     const double* v = a.vals + g * a.nm;
     int64_t len = 0;
-    if (a.mode == 0) {
+    if (a.mode != 1) {
         len = (a.row_offs[r + 1] - a.row_offs[r]) + 1 + (a.col_offs[c + 1] - a.col_offs[c]) + 1;  // + '\n'
         for (int m = 0; m < a.nm; ++m) len += 1 + (fmt_defined(v[m]) ? fmt_fixed(v[m], a.decimals, nullptr) : a.missing_len);
+        if (a.mode == 2)
+            len += fmt_span(a.rsuf_offs, 2 * r) + fmt_span(a.csuf_offs, 2 * c) + fmt_span(a.rsuf_offs, 2 * r + 1) +
+                   fmt_span(a.csuf_offs, 2 * c + 1) + 1 + fmt_span(a.lab_offs, fmt_comparison(a, r, c));
     } else {
         if (t == 0) len += a.row_offs[r + 1] - a.row_offs[r];
         len += 1 + (fmt_defined(v[0]) ? fmt_fixed(v[0], a.decimals, nullptr) : a.missing_len);
@@ -145,11 +174,20 @@ __device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int
         if (fmt_defined(x)) o += fmt_fixed(x, a.decimals, o);
         else put(a.missing, a.missing_len);
     };
-    if (a.mode == 0) {
+    if (a.mode != 1) {
         put(a.row_pre + a.row_offs[r], a.row_offs[r + 1] - a.row_offs[r]);
         *o++ = '\t';
         put(a.col_pre + a.col_offs[c], a.col_offs[c + 1] - a.col_offs[c]);
         for (int m = 0; m < a.nm; ++m) value(v[m]);
+        if (a.mode == 2) {
+            put(a.rsuf + a.rsuf_offs[2 * r], fmt_span(a.rsuf_offs, 2 * r));
+            put(a.csuf + a.csuf_offs[2 * c], fmt_span(a.csuf_offs, 2 * c));
+            put(a.rsuf + a.rsuf_offs[2 * r + 1], fmt_span(a.rsuf_offs, 2 * r + 1));
+            put(a.csuf + a.csuf_offs[2 * c + 1], fmt_span(a.csuf_offs, 2 * c + 1));
+            *o++ = '\t';
+            const int k = fmt_comparison(a, r, c);
+            put(a.lab + a.lab_offs[k], fmt_span(a.lab_offs, k));
+        }
         *o++ = '\n';
     } else {
         if (t == 0) put(a.row_pre + a.row_offs[r], a.row_offs[r + 1] - a.row_offs[r]);

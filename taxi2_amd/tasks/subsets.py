@@ -1,0 +1,200 @@
+"""VersusAll's partition-aware outputs (``src/itaxotools/taxi2/tasks/versus_all.py``):
+
+* ``summary.tsv`` -- ``SummaryHandler`` (:278-350) over every ordered pair: ids, the metrics,
+  both sides' extras, genus / species of both (``partition.get(id) or "-"``) and the comparison
+  type (``SubsetDistance.get_comparison_type``, :255-271).  Written unconditionally by the
+  reference (:754-768).  Text on the GPU (``taxi2_format_summary``) when ids are unique (no line
+  merging) and the formatter is ``{:.Nf}``; the handler's line grouping in Python otherwise.
+* ``subsets/{species,genera}/linear/{pairs,identity}.tsv`` and ``.../matricial/<metric>.tsv`` --
+  ``DistanceAggregator`` min / max / mean / count per (subset x, subset y) (:57-96, 605-684):
+  accumulated natively in the reference's x-major order (``taxi2_subset_aggregate``), written by
+  the Subset*StatisticsHandler rules (:98-236).
+"""
+
+from __future__ import annotations
+
+from itertools import groupby
+from pathlib import Path
+from typing import NamedTuple
+
+import numpy as np
+
+from .common import create_parents, fixed_decimals, gpu_text_ok
+
+
+class ComparisonType:
+    """``plot.py:15-27`` labels, in index order."""
+
+    Unknown = "no info"
+    IntraSpecies = "intra-species"
+    InterSpecies = "inter-species"
+    IntraGenus = "intra-genus"
+    InterGenus = "inter-genus"
+
+
+class SubsetPair(NamedTuple):
+    x: str | None
+    y: str | None
+
+
+def comparison_type(genera: SubsetPair | None, species: SubsetPair | None) -> str:
+    """``SubsetDistance.get_comparison_type`` (versus_all.py:255-271)."""
+    same_g = bool(genera.x == genera.y) if genera else None
+    same_s = bool(species.x == species.y) if species else None
+    if same_g is False:
+        return ComparisonType.InterGenus
+    if same_s is True:
+        return ComparisonType.IntraSpecies
+    if same_s is False:
+        return ComparisonType.InterSpecies
+    return ComparisonType.IntraGenus if same_g else ComparisonType.Unknown
+
+
+def subset_codes(ids: list[str], partition) -> tuple[np.ndarray, list]:
+    """Per sequence: the code of ``partition.get(id, None)``, codes numbered in first-appearance
+    order (= DistanceAggregator's dict order over the x-major product); and the subsets by code."""
+    subsets: dict = {}
+    code = np.array([subsets.setdefault(partition.get(i, None), len(subsets)) for i in ids], dtype=np.int32)
+    return code, list(subsets)
+
+
+# ----------------------------------------------------------------------------- summary.tsv
+SUMMARY_CHUNK_VALUES = 1 << 22  # values per taxi2_format_summary call (rows of N * M values)
+
+
+def write_summary(path: Path, seqs: list, A: np.ndarray, metrics: list, genera, species, fmt: str, missing: str,
+                  eng=None) -> None:
+    """``summary.tsv`` for the (N, N, M) adjusted values ``A`` (NaN = None)."""
+    create_parents(path)
+    n = len(seqs)
+    if n == 0:  # no distances: the handler writes nothing (versus_all.py via distances.py:84-88)
+        open(path, "w").close()
+        return
+    ids = [s.id for s in seqs]
+    gx = [genera.get(i, None) for i in ids] if genera else None
+    sx = [species.get(i, None) for i in ids] if species else None
+    head = ["seqid (query 1)", "seqid (query 2)", *[str(m) for m in metrics],
+            *[k + " (query 1)" for k in seqs[0].extras], *[k + " (query 2)" for k in seqs[0].extras],
+            "genus (query 1)", "species (query 1)", "genus (query 2)", "species (query 2)", "comparison_type"]
+    dec = fixed_decimals(fmt)
+    if eng is not None and len(set(ids)) == n and gpu_text_ok(A, dec):
+        ext = ["".join("\t" + (v if v is not None else missing) for v in s.extras.values()) for s in seqs]
+        gs = ["\t" + ((gx[k] if gx else None) or "-") + "\t" + ((sx[k] if sx else None) or "-") for k in range(n)]
+        suf = [t for pair in zip(ext, gs) for t in pair]
+        gcode = subset_codes(ids, genera)[0] if genera else np.zeros(n, np.int32)
+        scode = subset_codes(ids, species)[0] if species else np.zeros(n, np.int32)
+        codes = np.stack([gcode, scode], axis=1)
+        step = max(1, SUMMARY_CHUNK_VALUES // max(1, n * A.shape[2]))
+        with open(path, "wb") as fh:
+            fh.write(("\t".join(head) + "\n").encode("utf-8"))
+            for r0 in range(0, n, step):
+                r1 = min(n, r0 + step)
+                fh.write(eng.format_summary(A[r0:r1], ids[r0:r1], ids, suf[2 * r0 : 2 * r1], suf, codes[r0:r1], codes,
+                                            has_genera=bool(genera), has_species=bool(species), decimals=dec,
+                                            missing=missing))
+        return
+    # line grouping of DistanceHandler.Linear (distances.py:96-111): runs of equal (x.id, y.id)
+    text = _values_text(A, fmt, missing)
+
+    def lines():
+        pairs = ((i, j) for i in range(n) for j in range(n))
+        for _, run in groupby(pairs, key=lambda ij: (ids[ij[0]], ids[ij[1]])):
+            yield list(run)
+
+    with open(path, "w") as fh:
+        first = True
+        for run in lines():
+            i0, j0 = run[0]
+            if first:
+                labels = [str(m) for _ in run for m in metrics]
+                head[2 : 2 + len(metrics)] = labels
+                fh.write("\t".join(head) + "\n")
+                first = False
+            x, y = seqs[i0], seqs[j0]
+            g = SubsetPair(gx[i0], gx[j0]) if gx is not None else None
+            s = SubsetPair(sx[i0], sx[j0]) if sx is not None else None
+            fh.write("\t".join((
+                x.id, y.id, *[t for i, j in run for t in text[i, j]],
+                *[v if v is not None else missing for v in x.extras.values()],
+                *[v if v is not None else missing for v in y.extras.values()],
+                (g.x if g else None) or "-", (s.x if s else None) or "-",
+                (g.y if g else None) or "-", (s.y if s else None) or "-",
+                comparison_type(g, s),
+            )) + "\n")
+
+
+def _values_text(A: np.ndarray, fmt: str, missing: str) -> np.ndarray:
+    from .common import format_values
+
+    return format_values(A, fmt, missing)
+
+
+# ----------------------------------------------------------------------------- subset statistics
+class SubsetStats(NamedTuple):
+    subsets: list  # subset labels by code (None included)
+    mean: np.ndarray  # [ns][ns][m], NaN where count == 0
+    min: np.ndarray
+    max: np.ndarray
+    count: np.ndarray
+
+
+def aggregate(A: np.ndarray, ids: list[str], partition) -> SubsetStats:
+    """DistanceAggregator per metric over the (N, N, M) adjusted values (None skipped)."""
+    from .._native import subset_aggregate
+
+    code, subsets = subset_codes(ids, partition)
+    agg = subset_aggregate(A, code, len(subsets))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        mean = np.where(agg.count > 0, agg.sum / np.maximum(agg.count, 1), np.nan)
+    mn = np.where(agg.count > 0, agg.min, np.nan)
+    mx = np.where(agg.count > 0, agg.max, np.nan)
+    return SubsetStats(subsets, mean, mn, mx, agg.count)
+
+
+def _text(v: float, fmt: str) -> str:
+    return "NA" if not np.isfinite(v) else fmt.format(float(v))
+
+
+def write_subset_statistics(path: Path, st: SubsetStats, metrics: list, fmt: str, template: str) -> None:
+    """``linear/{pairs,identity}.tsv`` (versus_all.py:642-667) and ``matricial/<metric>.tsv``
+    (:669-684) under ``path``; the handlers' missing text is always "NA"."""
+    lin = Path(path) / "linear"
+    create_parents(lin)
+    labels = [f"{m} {s}" for m in metrics for s in ("mean", "min", "max")]
+    ns = len(st.subsets)
+
+    def name(v) -> str:
+        return "?" if v is None else v
+
+    def stats(a: int, b: int) -> list[str]:
+        return [_text(v, fmt) for k in range(len(metrics)) for v in (st.mean[a, b, k], st.min[a, b, k], st.max[a, b, k])]
+
+    with open(lin / "pairs.tsv", "w") as fp, open(lin / "identity.tsv", "w") as fi:
+        wrote_p = wrote_i = False
+        for a in range(ns):
+            for b in range(ns):
+                if st.subsets[a] == st.subsets[b]:  # bunch[0].idx == bunch[0].idy
+                    if not wrote_i:
+                        fi.write("\t".join(("target", *labels)) + "\n")
+                        wrote_i = True
+                    fi.write("\t".join((name(st.subsets[a]), *stats(a, b))) + "\n")
+                else:
+                    if not wrote_p:
+                        fp.write("\t".join(("target", "query", *labels)) + "\n")
+                        wrote_p = True
+                    fp.write("\t".join((name(st.subsets[a]), name(st.subsets[b]), *stats(a, b))) + "\n")
+    mat = Path(path) / "matricial"
+    create_parents(mat)
+    for k, metric in enumerate(metrics):
+        with open(mat / f"{metric}.tsv", "w") as fh:
+            if ns:
+                fh.write("\t".join(("", *[name(s) for s in st.subsets])) + "\n")
+            for a in range(ns):
+                cells = []
+                for b in range(ns):
+                    if not st.count[a, b, k]:
+                        cells.append("NA")
+                    else:
+                        cells.append(template.format(mean=_text(st.mean[a, b, k], fmt), min=_text(st.min[a, b, k], fmt),
+                                                     max=_text(st.max[a, b, k], fmt)))
+                fh.write("\t".join((name(st.subsets[a]), *cells)) + "\n")

@@ -8,15 +8,17 @@ normalize (when aligning) -> ordered product x-major -> Biopython global alignme
 p / p-gaps / jc / k2p for every ordered pair, ``None`` where the aligned pair is identical
 (``x != y`` on full tuples, :549-552), x100 when ``percentage_multiply`` (:554-562) ->
 ``distances/linear.tsv`` (Linear.WithExtras) and ``distances/matricial/<metric>.tsv``, plus
-``align/aligned_pairs.txt`` (Formatted) when ``params.pairs.write``.
+``align/aligned_pairs.txt`` (Formatted) when ``params.pairs.write``, ``summary.tsv`` (always, with
+genus / species / comparison type from ``input.genera`` / ``input.species``) and, per given
+partition, the subset statistics under ``subsets/{genera,species}`` (``tasks/subsets.py``).
 
 The N(N-1)/2 unordered pairs run on the MI355X engine in blocks; one DP fill gives both ordered
 pairs.  With torch.distributed initialised (one process per GPU) the pair space is sharded by
 row blocks and gathered over RCCL (``taxi2_amd/sharding.py``).
 
-Out of scope: per-sequence statistics, species/genus aggregation,
-histograms and the summary file.  Their params exist with the reference's names but default
-to False here; setting one raises NotImplementedError.
+Out of scope: per-sequence statistics (``stats/*.tsv``) and histograms.
+Their params exist with the reference's names but default to False here; setting one raises
+NotImplementedError.
 """
 
 from __future__ import annotations
@@ -303,6 +305,23 @@ class VersusAll:
                 for pair in aligner.align_many([SequencePair(x, y) for y in seqs]):
                     fh.write(pair)
 
+    def write_summary(self, seqs: list, A: np.ndarray):
+        from .subsets import write_summary
+
+        write_summary(self.paths.summary, seqs, A, self.params.distances.metrics, self.input.genera,
+                      self.input.species, self.params.format.float, self.params.format.missing,
+                      self._engine() if seqs else None)
+
+    def write_subsets(self, seqs: list, A: np.ndarray):
+        from .subsets import aggregate, write_subset_statistics
+
+        ids = [s.id for s in seqs]
+        for partition, name in ((self.input.genera, "genera"), (self.input.species, "species")):
+            if partition:
+                write_subset_statistics(self.paths.subsets / name, aggregate(A, ids, partition),
+                                        self.params.distances.metrics, self.params.format.float,
+                                        self.params.format.stats_template)
+
     # ------------------------------------------------------------------ driver
     def start(self) -> Results:
         ts = perf_counter()
@@ -326,6 +345,8 @@ class VersusAll:
             self.write_pairs(seqs)
             self.write_distances_linear(seqs, A)
             self.write_distances_multimatrix(seqs, A)
+            self.write_summary(seqs, A)
+            self.write_subsets(seqs, A)
         n = len(seqs)
         total = len(self.params.distances.metrics) * n * n
         report(self.progress_handler, "Finalizing...", total, total)
