@@ -16,6 +16,7 @@
 
 #include "../../include/taxi2_mi355x.h"
 #include "align1_kernel.hpp"
+#include "align1c_kernel.hpp"
 #include "align_kernel.hpp"
 #include "ncd_kernels.hpp"
 #include "format_kernels.hpp"
@@ -213,6 +214,9 @@ struct Variant1 {
     const void* fn[2];  // pass 1 (orientation A + divergence flag), pass 2 (orientation B)
     void (*launch[2])(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int,
                       int, double*, int32_t*, uint32_t*, uint32_t*, unsigned long long*);
+    const void* fnc[2];  // chained kernel (k_align1c), same passes
+    void (*launchc[2])(dim3, dim3, size_t, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int,
+                       int, double*, int32_t*, uint32_t*, uint32_t*, unsigned long long*);
 };
 
 template <int K, int W, bool DEF, int OCC, bool B, int NW>
@@ -223,10 +227,21 @@ void launch_align1(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetVie
                        nx);
 }
 
+template <int K, int W, bool DEF, int OCC, bool B, int NW>
+void launch_align1c(dim3 g, dim3 b, size_t lds, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc,
+                    MetricSpec ms, int xcap, int om, double* out, int32_t* so, uint32_t* wl, uint32_t* wc,
+                    unsigned long long* nx) {
+    hipLaunchKernelGGL((k_align1c<K, W, DEF, OCC, B, NW>), g, b, lds, st, x, y, ps, sc, ms, xcap, om, out, so, wl,
+                       wc, nx);
+}
+
 #define T2_VARIANT1N(K, W, DEF, OCC, NW)                                                                 \
     Variant1{K, W, OCC, DEF, NW,                                                                          \
              {(const void*)&k_align1<K, W, DEF, OCC, false, NW>, (const void*)&k_align1<K, W, DEF, OCC, true, NW>}, \
-             {&launch_align1<K, W, DEF, OCC, false, NW>, &launch_align1<K, W, DEF, OCC, true, NW>}}
+             {&launch_align1<K, W, DEF, OCC, false, NW>, &launch_align1<K, W, DEF, OCC, true, NW>},      \
+             {(const void*)&k_align1c<K, W, DEF, OCC, false, NW>,                                           \
+              (const void*)&k_align1c<K, W, DEF, OCC, true, NW>},                                           \
+             {&launch_align1c<K, W, DEF, OCC, false, NW>, &launch_align1c<K, W, DEF, OCC, true, NW>}}
 #define T2_VARIANT1(K, W, DEF, OCC) T2_VARIANT1N(K, W, DEF, OCC, 2)
 
 // Ordered by column capacity 64 * K * W.  Two-word counters up to A1_MAX_LEN, three-word counters
@@ -279,11 +294,16 @@ const Variant1* pick_variant1(const KScores& k, int max_len) {
 int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
                         hipStream_t st, int xcap) {
-    const size_t lds = a1_lds_bytes(xcap, v.K, v.W, v.def);
+    // chained kernel (consecutive pairs sharing their column sequence stream through the lanes);
+    // TAXI2_A1_NOCHAIN=1 selects the one-pair-at-a-time kernel
+    const bool chain = !getenv("TAXI2_A1_NOCHAIN");
+    const size_t lds = chain ? a1c_lds_bytes(v.K, v.W, v.def) : a1_lds_bytes(xcap, v.K, v.W, v.def);
+    const void* const* fns = chain ? v.fnc : v.fn;
+    auto launch = chain ? v.launchc : v.launch;
     if (lds > 160 * 1024) return fail(ctx, "LDS requirement %zu exceeds 160 KiB", lds);
     if (lds > 64 * 1024)
-        for (const void* fn : v.fn)
-            HIP_TRY(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        for (int k = 0; k < 2; ++k)
+            HIP_TRY(ctx, hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // d_work: [u32 worklist count, pad] [u64 pass-1 cursor] [u64 pass-2 cursor] [u32 worklist...]
     if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32 + (size_t)ps.count * 4)) return -1;
     uint32_t* wcount = (uint32_t*)ctx->d_work;
@@ -294,11 +314,18 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
     // a device cursor; pass 2's length is known only on the device)
     const int64_t resident = (int64_t)ctx->num_cus * std::max(1, 4 * v.occ / v.W);
     const int64_t grid = std::min<int64_t>(ps.count, resident);
-    v.launch[0](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
-                d_out, d_scores, wlist, wcount, next);
+    // the int argument is xcap for k_align1 and the chunk request for k_align1c (0 = automatic;
+    // TAXI2_A1_CHUNK forces 1..16 pairs per cursor step, e.g. to test long chains on small inputs)
+    int arg = xcap;
+    if (chain) {
+        const char* c = getenv("TAXI2_A1_CHUNK");
+        arg = c ? std::max(0, std::min(A1C_CHUNK, atoi(c))) : 0;
+    }
+    launch[0](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, arg, out_mode, d_out,
+              d_scores, wlist, wcount, next);
     HIP_TRY(ctx, hipGetLastError());
-    v.launch[1](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, xcap, out_mode,
-                d_out, nullptr, wlist, wcount, next + 1);
+    launch[1](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, arg, out_mode, d_out,
+              nullptr, wlist, wcount, next + 1);
     HIP_TRY(ctx, hipGetLastError());
     if (getenv("TAXI2_A1_STATS")) {  // diagnostics: share of pairs re-run in orientation B
         uint32_t n2 = 0;

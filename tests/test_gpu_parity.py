@@ -320,3 +320,53 @@ def test_single_orientation_long_counters(engine, oracle_c):
     assert_metrics_equal(got, exp)
     assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(two, nan=9.0))
     st.free()
+
+
+@pytest.mark.parametrize("chunk", [16, 7])
+def test_chained_pairs(engine, oracle_c, chunk):
+    """k_align1c streams the rows of consecutive pairs that share their column sequence through
+    the same lanes.  Small inputs get chunks of one pair automatically, so TAXI2_A1_CHUNK forces
+    long chains here: ragged lengths (len(b) > len(a) breaks a chain), empty and 1-base sequences
+    inside chunks, a triangle row boundary mid-chunk, both counter widths, both passes, and the
+    rectangle (query-major) source; every result against the oracle and the unchained kernel."""
+    from taxi2_amd._native import tri_pairs
+
+    rng = np.random.default_rng(chunk)
+    fam = family_sequences(18, 600, 0x53 + chunk, ancestors=3, max_sub=0.05, indel_rate=0.02)
+    seqs = [s[: 300 + int(rng.integers(0, 300))] for s in fam]
+    seqs[3] = ""
+    seqs[7] = "A"
+    seqs[11] = seqs[10]  # identical neighbours: a full-tie pair inside a chain
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"]):
+        got, gsc = _with_env("TAXI2_A1_CHUNK", str(chunk),
+                             lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
+        one = _with_env("TAXI2_A1_NOCHAIN", "1", lambda: engine.all_pairs(st, 0, len(a), METRICS, sc))
+        exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
+        assert_metrics_equal(got, exp)
+        nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
+        assert np.array_equal(gsc[nonempty], esc[nonempty])
+        assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(one, nan=9.0))
+    # an offset block of the triangle (chunks start mid-row)
+    k0, cnt = 40, 61
+    got = _with_env("TAXI2_A1_CHUNK", str(chunk), lambda: engine.all_pairs(st, k0, cnt, METRICS, None))
+    exp, _ = oracle_c.batch(seqs, a[k0 : k0 + cnt], b[k0 : k0 + cnt], align=True, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp)
+    # rectangle: query-major pairs share the query as their column sequence
+    qs = engine.upload(seqs[:5], align=True)
+    rs = engine.upload(seqs[5:], align=True)
+    got = _with_env("TAXI2_A1_CHUNK", str(chunk), lambda: engine.rect_pairs(qs, rs, 0, 5, METRICS, None))
+    pa = np.repeat(np.arange(5), len(seqs) - 5)
+    pb = np.tile(np.arange(5, len(seqs)), 5)
+    exp, _ = oracle_c.batch(seqs, pa, pb, align=True, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp[:, 0, :])
+    # three-word counters (lengths > 1023)
+    long = [s * 3 for s in seqs[:8] if s]
+    lt = engine.upload(long, align=True)
+    la, lb = tri_pairs(len(long))
+    got = _with_env("TAXI2_A1_CHUNK", str(chunk), lambda: engine.all_pairs(lt, 0, len(la), METRICS, None))
+    exp, _ = oracle_c.batch(long, la, lb, align=True, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp)
+    for s in (st, qs, rs, lt):
+        s.free()
