@@ -18,6 +18,7 @@
 #include "align1_kernel.hpp"
 #include "align1c_kernel.hpp"
 #include "align_kernel.hpp"
+#include "alignt_kernel.hpp"
 #include "ncd_kernels.hpp"
 #include "format_kernels.hpp"
 #include "common.hpp"
@@ -57,6 +58,8 @@ struct taxi2_ctx {
     size_t d_aux_bytes = 0;
     void* d_work = nullptr;  // single-orientation aligner: [count][worklist...]
     size_t d_work_bytes = 0;
+    void* d_trace = nullptr;  // trace-and-walk aligner: two chain trace buffers per workgroup
+    size_t d_trace_bytes = 0;
     void* d_fmt = nullptr;  // text formatter staging
     size_t d_fmt_bytes = 0;
     void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
@@ -336,6 +339,63 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
     return 0;
 }
 
+// ---------------------------------------------------------------- trace-and-walk variants
+struct VariantT {
+    int K, W, occ;
+    bool def;
+    const void* fn;
+    void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int, int, double*,
+                   int32_t*, uint8_t*, int64_t, int, int, unsigned long long*);
+};
+
+template <int K, int W, bool DEF, int OCC>
+void launch_alignt(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
+                   int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
+                   unsigned long long* nx) {
+    hipLaunchKernelGGL((k_alignt<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
+                       hops, nx);
+}
+
+#define T2_VARIANTT(K, W, DEF, OCC) \
+    VariantT{K, W, OCC, DEF, (const void*)&k_alignt<K, W, DEF, OCC>, &launch_alignt<K, W, DEF, OCC>}
+
+// Ordered by column capacity 64 * K * W (waves per SIMD in `occ`).
+const VariantT kAlignT[] = {
+    T2_VARIANTT(4, 1, true, 6),  T2_VARIANTT(8, 1, true, 6),  T2_VARIANTT(8, 2, true, 6),
+    T2_VARIANTT(4, 1, false, 6), T2_VARIANTT(8, 1, false, 6), T2_VARIANTT(8, 2, false, 6),
+};
+
+const VariantT* pick_variantt(const KScores& k, int max_len) {
+    const bool def = is_default(k);
+    for (const auto& v : kAlignT)
+        if (v.def == def && 64 * v.K * v.W >= max_len) return &v;
+    return nullptr;
+}
+
+int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
+                        const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
+                        hipStream_t st, int max_len) {
+    const int64_t resident = (int64_t)ctx->num_cus * std::max(1, 4 * v.occ / (v.W + 1));
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ps.count, resident));
+    // chunk (pairs per cursor step): TAXI2_AT_CHUNK forces 1..AT_CHUNK, else the kernel's automatic
+    // rule (at least ~8 chunks per workgroup); it bounds the rows of a chain, hence the buffers
+    int chunk = 0;
+    if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(AT_CHUNK, atoi(c)));
+    const int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(AT_CHUNK, ps.count / (grid * 8)));
+    const int cap_rows = (int)eff * std::max(1, max_len);
+    const size_t bb = at_buf_bytes(cap_rows, v.K, v.W);
+    if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
+    int hops = 32;
+    if (const char* h = getenv("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32)) return -1;
+    unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 32, st));
+    v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), ps, k, ms, chunk, out_mode, d_out,
+             d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
 int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                        const taxi2_scores* sc, const MetricSpec& ms, int out_mode, double* d_out,
                        int32_t* d_scores, hipStream_t st) {
@@ -350,6 +410,13 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (mag * (2LL * max_len + 2) >= (1LL << 26))
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
+    if (!is_linear(k) && !getenv("TAXI2_NO_ALIGNT")) {
+        const VariantT* vt = pick_variantt(k, max_len);
+        if (vt) {
+            if (ps.count <= 0) return 0;
+            return launch_alignt_pairs(ctx, *vt, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, max_len);
+        }
+    }
     if (!is_linear(k) && max_len <= A1_MAX_LEN_LONG && !getenv("TAXI2_NO_ALIGN1")) {
         if (ps.count <= 0) return 0;
         const Variant1* v1 = pick_variant1(k, max_len);
@@ -623,6 +690,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
+    if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
     if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
     if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);

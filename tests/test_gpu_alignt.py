@@ -1,0 +1,117 @@
+"""GPU parity of the trace-and-walk aligner (taxi2_amd/csrc/alignt_kernel.hpp), the default for
+Gotoh scores up to 1 024 columns: the fill stores one byte of tie information per cell and a
+walker wave traces both Biopython first paths (priority M>Ix>Iy for (a, b), M>Iy>Ix for
+(b, a)).
+
+Every case is checked against the C restatement (oracle/taxi2_oracle.c, scores bit-exact,
+p / p-gaps bit-exact, jc / k2p within 1e-12) AND against the forward-carry kernels
+(TAXI2_NO_ALIGNT=1), bit for bit.  TAXI2_AT_CHUNK forces long chains on small inputs and
+TAXI2_AT_HOPS=1 starves the walker so that most walks finish in the post-chain drain.
+"""
+
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from tests.seqgen import family_sequences
+from tests.test_gpu_parity import METRICS, SCORE_SETS, assert_metrics_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_env(env: dict, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _tie_heavy(n: int, length: int, seed: int) -> list[str]:
+    """Near-identical families with ragged ends, lowercase runs and IUPAC bytes: many Ix / Iy
+    ties (the (a, b) and (b, a) alignments differ), and the byte-compare substitution path."""
+    fam = family_sequences(n, length, seed, ancestors=3, max_sub=0.05, indel_rate=0.02)
+    rng = np.random.default_rng(seed)
+    out = []
+    for k, s in enumerate(fam):
+        s = s[: length - 200 + int(rng.integers(0, 200))]
+        if k % 4 == 1:
+            s = s[:100] + s[100:160].lower() + s[160:]
+        if k % 5 == 2:
+            b = bytearray(s.encode())
+            for pos in rng.integers(0, len(b), 6):
+                b[pos] = ord("NRYKM"[int(rng.integers(0, 5))])
+            s = b.decode()
+        out.append(s)
+    return out
+
+
+@pytest.mark.parametrize("env", [{}, {"TAXI2_AT_CHUNK": "8"}, {"TAXI2_AT_CHUNK": "3", "TAXI2_AT_HOPS": "1"}])
+def test_alignt_triangle(engine, oracle_c, env):
+    from taxi2_amd._native import tri_pairs
+
+    seqs = _tie_heavy(18, 900, 0x61)
+    seqs += ["ACGT" * 256, "A", "", "N" * 40, seqs[0]]  # 1024 (capacity), 1, empty, no ACGT, duplicate
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
+    for name in ("default", "generic"):
+        sc = SCORE_SETS[name]
+        got, gsc = _with_env(env, lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
+        old, osc = _with_env({"TAXI2_NO_ALIGNT": "1"},
+                             lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
+        exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
+        assert np.array_equal(gsc[nonempty], esc[nonempty])
+        assert_metrics_equal(got, exp)
+        assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(old, nan=9.0))
+        assert np.array_equal(gsc, osc)
+        asym = ~np.all(np.isclose(np.nan_to_num(exp[:, 0]), np.nan_to_num(exp[:, 1])), axis=1)
+        assert asym.sum() > 0  # the two orientations really differ somewhere
+    # an offset block of the triangle (chunks start mid-row)
+    k0, cnt = 57, 83
+    got = _with_env(env, lambda: engine.all_pairs(st, k0, cnt, METRICS, None))
+    exp, _ = oracle_c.batch(seqs, a[k0 : k0 + cnt], b[k0 : k0 + cnt], align=True, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp)
+    st.free()
+
+
+@pytest.mark.parametrize("env", [{}, {"TAXI2_AT_CHUNK": "5"}])
+def test_alignt_rectangle(engine, oracle_c, env):
+    """One ordered orientation per pair (versusReference): the walk of the (query, ref) slot,
+    with queries longer and shorter than the references (rows / columns swapped)."""
+    seqs = _tie_heavy(14, 700, 0x62)
+    qseq = seqs[:6]
+    rseq = [s[:350] if k % 2 else s for k, s in enumerate(seqs[6:])]
+    qs = engine.upload(qseq, align=True)
+    rs = engine.upload(rseq, align=True)
+    got = _with_env(env, lambda: engine.rect_pairs(qs, rs, 0, len(qseq), METRICS, SCORE_SETS["default"]))
+    allseq = qseq + rseq
+    pa = np.repeat(np.arange(len(qseq)), len(rseq))
+    pb = np.tile(np.arange(len(rseq)), len(qseq)) + len(qseq)
+    exp, _ = oracle_c.batch(allseq, pa, pb, align=True, scores=SCORE_SETS["default"])
+    assert_metrics_equal(got, exp[:, 0, :])
+    qs.free()
+    rs.free()
+
+
+def test_alignt_bench_shape(engine, oracle_c):
+    """The bench generator (config 3, 1 000 bp, unrelated families) with chains of 8 pairs."""
+    from taxi2_amd._native import tri_pairs
+
+    seqs = family_sequences(30, 1000, 0x7A12, ancestors=6)
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    got, gsc = _with_env({"TAXI2_AT_CHUNK": "8"},
+                         lambda: engine.all_pairs(st, 0, len(a), METRICS, None, with_scores=True))
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=SCORE_SETS["default"])
+    assert np.array_equal(gsc, esc)
+    assert_metrics_equal(got, exp)
+    st.free()
