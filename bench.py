@@ -40,12 +40,11 @@ HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz -- one wave64 int32 VALU instruction per 4 clk per
 # SIMD, measured with tools/valu_peak.hip (DESIGN.md "Compute ceiling")
 INT_VALU_PEAK = 256 * 64 * 2.4e9
-# Non-compare VALU lane-ops per USEFUL cell of the bench workload: 34.25 per cell in the pass-1
-# step loop of k_align1<8,2> (274 per 8-cell step, tools/loop_stats.py; v_cmp issue below full
-# rate) x systolic fill 1063/1000 x column padding 1024/1000 x pass-2 share of
-# kernel time 661.2/610.4 ms (profiles/r1/kernel_stats_align1.csv).
-OPS_PER_CELL = 40.4
-VALU_INSTS_PER_CELL_PMC = 52.3      # all VALU incl. compares, SQ_INSTS_VALU x 64 / cells (pmc_valu_align1)
+# VALU lane-ops per USEFUL cell of the bench workload, measured: SQ_INSTS_VALU x 64 / (pairs x
+# 1000 x 1000) over one launch of k_alignt<8,2> (fill waves + walker wave, column padding
+# 1024/1000 and the systolic skew included; profiles/r1/pmc_valu_alignt.csv).  The fill issues
+# 0.252 VALU instructions per SIMD-clock, i.e. the one-per-4-clocks wave64 issue ceiling.
+OPS_PER_CELL = 31.8
 
 
 def b_pair(L: int, M: int) -> int:
@@ -192,7 +191,6 @@ def main() -> None:
                 "bound": "valu-int32",
                 "gcups": gcups,
                 "ops_per_cell": OPS_PER_CELL,
-                "valu_insts_per_cell_pmc": VALU_INSTS_PER_CELL_PMC,
                 "achieved_tops": gcups * 1e9 * OPS_PER_CELL / 1e12,
                 "peak_tops": INT_VALU_PEAK / 1e12,
                 "frac": gcups * 1e9 * OPS_PER_CELL / INT_VALU_PEAK,

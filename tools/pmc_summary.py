@@ -54,10 +54,10 @@ def main() -> None:
         "hbm_bytes_per_launch": total_kb * 1024.0,
         "source": f"profiles/{dst.name}/pmc_fetch_{args.tag}.csv, pmc_write_{args.tag}.csv",
         "note": "FETCH_SIZE + WRITE_SIZE (KB) x 1024 from separate rocprofv3 --pmc passes over one launch of the "
-                "bench command (--steps 1 --warmup 0), summed over the path's kernels (single-orientation pass 1 "
-                "+ pass 2).  The reads are byte gathers of sequence rows (not the 16-B/lane stream the gfx950 "
-                "FETCH_SIZE x2 correction is calibrated for), so FETCH_SIZE is reported uncorrected; consecutive "
-                "pairs share their first sequence, so most reads hit L2.",
+                "bench command (--steps 1 --warmup 0), summed over the path's kernels.  k_alignt writes one trace "
+                "byte per DP cell (~1.06 MB per 1 000 bp pair, 8-byte coalesced stores per lane and step; "
+                "WRITE_SIZE is exact for such streams) and its walker reads ~2 x 1 100 single bytes per pair "
+                "(64-B line fetches, uncalibrated width: FETCH_SIZE reported uncorrected).",
     }
     (ROOT / "profiles/pmc_traffic.json").write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec, indent=1))
