@@ -1,0 +1,500 @@
+// Packed trace-and-walk aligner: alignt_kernel.hpp with TWO pairs per lane, one in each 16-bit
+// half of every register (v_pk_max_i16 / v_pk_add_u16 / v_pk_sub_i16 / v_pk_mad_u16).
+//
+// The fill of alignt_kernel.hpp is VALU-issue bound (0.25 instructions per SIMD-clock) at ~25
+// ops per cell, all of them 32-bit max / add / sub / med3 / alignbit on scores that never
+// exceed a few thousand.  In 16-bit halves one instruction serves two DP cells, so the score
+// and sign arithmetic halves; the trace packing becomes arithmetic on both halves at once
+// (balanced base-4 digits) and one v_perm per two columns gathers the four bytes.
+//
+// Streams.  A chain's pairs (same column sequence) alternate between stream 0 (low halves) and
+// stream 1 (high halves); each stream feeds its pairs' rows back to back, so at step s lane l
+// works on row s - l of BOTH streams.  Everything per row (row info ring, first / last-row
+// resets, end-gap row scores, column-0 boundary, substitution words) exists once per stream.
+//
+// Per cell and pair the byte is (int8) (16 sc + 4 sb + sa) << 2 | tagF << 1 | tagG with the
+// signs sa = sign(G - X), sb = sign(cg - cx), sc = sign(cf - cy) of alignt_kernel.hpp.  Bytes
+// are stored per lane and step as [k][stream] (2K bytes, one 16-byte store for K = 8).
+//
+// Substitution scores come from an LDS table eqt[base][thread][K/2] of 16-bit fields (the
+// doubled match / mismatch score of each column against a row byte "ACGT"[base]); per step each
+// stream reads its row's K/2 words (one ds_read_b128), per cell one v_perm builds the packed
+// pair of scores.  Rows with any other byte build their words by byte compares (rare path).
+//
+// 16-bit range: values stay within [-(2 P (nA + nB) + 2 |eo| + 2 |io|), 2 ma min(nA, nB) + 1]
+// (P = largest per-column penalty) and the -inf boundary is -16384; the host admits a launch
+// only when every difference fits int16 (at_fits16), else it uses the 32-bit kernel.
+#pragma once
+#include "alignt_kernel.hpp"
+
+namespace taxi2 {
+
+typedef short at_s2 __attribute__((ext_vector_type(2)));
+
+constexpr int AT2_CHUNK = 8;          // pairs per cursor step (both streams)
+constexpr int NEG16 = -16384;
+constexpr uint32_t NEG16X2 = 0xC000C000u;
+
+__device__ __forceinline__ at_s2 as_s2(uint32_t v) { return __builtin_bit_cast(at_s2, v); }
+__device__ __forceinline__ uint32_t as_u32(at_s2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ at_s2 pmax(at_s2 a, at_s2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16); }
+// per half clamp to [-1, 1] (the compiler would expand it into compares and selects)
+__device__ __forceinline__ at_s2 psign(at_s2 d) {
+    uint32_t r;
+    asm("v_pk_max_i16 %0, %1, -1 op_sel_hi:[1,0]\n\tv_pk_min_i16 %0, %0, 1 op_sel_hi:[1,0]" : "=&v"(r) : "v"(as_u32(d)));
+    return as_s2(r);
+}
+// per half a * 4 + b
+__device__ __forceinline__ at_s2 pmad4(at_s2 a, at_s2 b) {
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)));
+    return as_s2(r);
+}
+
+// Host: do all differences of the packed fill fit int16?
+__host__ __device__ inline bool at_fits16(const KScores& k, int max_len) {
+    auto ab = [](int v) { return v < 0 ? -v : v; };
+    const long long P = std::max({ab(k.ma), ab(k.mi), ab(k.ie), ab(k.ee)});
+    const long long O = std::max(ab(k.io), ab(k.eo));
+    const long long lo = 2 * (P * 2 * (long long)max_len + 2 * O + 2);
+    const long long hi = 2 * (long long)ab(k.ma) * max_len + 2;
+    return lo + 2 * O + 2 * P - NEG16 + 8 < 32767 && hi + 2 * O + 2 * P - NEG16 + 8 < 32767;
+}
+
+// row info of stream-local row g: the chain pairs of stream `st` are tab[st], tab[st + 2], ...
+__device__ __forceinline__ uint32_t a2_row_info(const ChainPair* __restrict__ tab, int n, int st, int rows, int g) {
+    if (g >= rows) return A1C_NONE;
+    int k = st;
+    for (int t = st + 2; t < n; t += 2)
+        if (tab[t].r0 <= g) k = t;
+    const ChainPair& cp = tab[k];
+    const int i = g - cp.r0;
+    uint32_t v = a1_xinfo(cp.rseq[i], i, cp.fx, cp.lx);
+    if (i == 0) v |= A1C_FIRST;
+    if (i == cp.nA - 1) v |= A1C_LAST;
+    return v | ((uint32_t)(i + 1) << 18);
+}
+
+template <int K, int W, bool DEF, int OCC>
+__global__ void __launch_bounds__(64 * (W + 1), OCC)
+k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
+          double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
+          int cap_rows, int hops, unsigned long long* __restrict__ next) {
+    static_assert(K % 2 == 0 && K <= 8, "16-bit score fields: K / 2 words per stream and base");
+    constexpr int NT = 64 * W;
+    constexpr int XR = a1c_xr(W);
+    constexpr int KW = K / 2;
+    const KScores sc0 = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
+    const KScores sc = doubled(sc0);
+    __shared__ uint32_t xinfo[2][XR];
+    __shared__ ChainPair tab[2][AT2_CHUNK];
+    __shared__ int fin[2][AT2_CHUNK];
+    __shared__ uint32_t fin_n[2];
+    __shared__ AtChain chs[2];
+    __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * RING];
+    __shared__ uint8_t colb[NT * K];
+    __shared__ uint32_t colc[K][NT];            // Ix open (both halves; end-gap score on column nB)
+    __shared__ uint32_t colx[DEF ? 1 : K][NT];  // Ix extend (non-default scores)
+    __shared__ uint32_t eqt[4][NT][KW];         // 16-bit substitution score fields by row base
+    __shared__ int64_t s_qc, s_qend;
+    __shared__ int s_n, s_rows[2];
+    __shared__ AtWalk wks[64];
+
+    const int tid = (int)threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const bool walker = w == W;
+    const int nm = ms.n;
+    const int64_t total = ps.count;
+    const int64_t chunk = chunk_req >= 1 ? min((int64_t)chunk_req, (int64_t)AT2_CHUNK)
+                                         : max((int64_t)1, min((int64_t)AT2_CHUNK, total / ((int64_t)gridDim.x * 8)));
+    uint8_t* const bufs = trace + (size_t)blockIdx.x * 2 * (size_t)buf_bytes;
+
+    if (tid == 0) {
+        s_qc = 0;
+        s_qend = 0;
+    }
+    int cur = 0;
+    int prev_n = 0;
+
+    auto walk_init = [&](int pb, int n) {
+        const int nw = out_mode == OUT_BOTH ? 2 * n : n;
+        AtWalk& W_ = wks[lane];
+        W_.st = AT_DONE;
+        if (lane < nw) {
+            const int pi = lane < n ? lane : lane - n;
+            const ChainPair& cp = tab[pb][pi];
+            W_.pi = pi;
+            W_.prio = out_mode == OUT_BOTH ? (lane >= n) : cp.swp;
+            W_.i = cp.nA + 1;
+            W_.j = chs[pb].nB + 1;
+            W_.st = AT_M;
+            W_.first = 1;
+            W_.valid = W_.ts = W_.tv = W_.gap = 0;
+            W_.cb = W_.xa = W_.yb = 0u;
+        }
+    };
+    auto walk_run = [&](int pb, int budget) {
+        AtWalk& W_ = wks[lane];
+        int st = W_.st;
+        if (!__any(st != AT_DONE)) return;
+        const int pi = W_.pi;
+        const ChainPair& cp = tab[pb][pi];
+        const AtChain& ch = chs[pb];
+        const int fx = cp.fx, lx = cp.lx, fy = ch.fy, ly = ch.ly, r0 = cp.r0, sm = cp.pad;
+        const int prio = W_.prio;
+        const uint8_t* rs = cp.rseq;
+        const uint8_t* cs = ch.cseq;
+        const uint8_t* tr = bufs + (size_t)pb * (size_t)buf_bytes + sm;
+        int i = W_.i, j = W_.j, first = W_.first;
+        uint32_t cb = W_.cb, xa = W_.xa, yb = W_.yb;
+        int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
+        for (int h = 0; budget < 0 || h < budget; ++h) {
+            if (!__any(st != AT_DONE)) break;
+            if (st == AT_DONE) continue;
+            int ni, nj;
+            if (st == AT_M) {
+                if (!first) {
+                    const int bx = base_code(xa), by = base_code(yb);
+                    if (bx < 4 && by < 4) {
+                        ++valid;
+                        const int dd = bx ^ by;
+                        ts += dd == 2;
+                        tv += (dd != 0) & (dd != 2);
+                    }
+                }
+                ni = i - 1;
+                nj = j - 1;
+            } else if (st == AT_IX) {
+                if (base_code(xa) < 4 && j - 1 >= fy && j <= ly) ++gap;
+                ni = i - 1;
+                nj = j;
+            } else {
+                if (base_code(yb) < 4 && i - 1 >= fx && i <= lx) ++gap;
+                ni = i;
+                nj = j - 1;
+            }
+            first = 0;
+            if (ni == 0 && nj == 0) {
+                const int64_t p = cp.p;
+                double* o;
+                if (out_mode == OUT_BOTH) o = out + (p * 2 + ((prio ^ cp.swp) ? 1 : 0)) * nm;
+                else o = out + p * nm;
+                for (int m = 0; m < nm; ++m)
+                    o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
+                if (sout && (out_mode != OUT_BOTH || !prio)) sout[p] = fin[pb][pi] >> 1;
+                st = AT_DONE;
+                continue;
+            }
+            uint32_t nb = 0;
+            if (ni >= 1 && nj >= 1) {
+                const int t = (nj - 1) / K;
+                const int k = nj - 1 - t * K;
+                const int s = r0 + ni - 1 + (t & 63);
+                nb = *(const volatile uint8_t*)(tr + ((size_t)s * NT + t) * (2 * K) + 2 * k);
+            }
+            xa = ni >= 1 ? rs[ni - 1] : 0u;
+            yb = nj >= 1 ? cs[nj - 1] : 0u;
+            // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa (balanced base-4 digits)
+            const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 21;
+            const int cu = ((int)(int8_t)(uint8_t)cb >> 2) + 21;
+            int nst;
+            if (ni == 0) {
+                nst = AT_IY;
+            } else if (nj == 0) {
+                nst = AT_IX;
+            } else if (st == AT_M) {  // best state of (ni, nj)
+                const int ca = (nu & 3) - 1;
+                nst = ca > 0 ? ((nb & 1u) ? AT_M : AT_IY) : (ca == 0 ? (prio ? AT_IY : AT_IX) : AT_IX);
+            } else if (st == AT_IX) {  // how Ix(i, j) was formed
+                const int sb = ((cu >> 2) & 3) - 1;
+                const bool gp = prio ? sb >= 0 : sb > 0;
+                nst = gp ? ((nb & 1u) ? AT_M : AT_IY) : AT_IX;
+            } else {  // how Iy(i, j) was formed
+                const int sc_ = (cu >> 4) - 1;
+                const bool fp = prio ? sc_ > 0 : sc_ >= 0;
+                nst = fp ? ((nb & 2u) ? AT_M : AT_IX) : AT_IY;
+            }
+            cb = nb;
+            i = ni;
+            j = nj;
+            st = nst;
+        }
+        W_.i = i;
+        W_.j = j;
+        W_.st = st;
+        W_.first = first;
+        W_.cb = cb;
+        W_.xa = xa;
+        W_.yb = yb;
+        W_.valid = valid;
+        W_.ts = ts;
+        W_.tv = tv;
+        W_.gap = gap;
+    };
+
+    for (;;) {
+        // ---- cut the next chain (thread 0); its pairs alternate between the two streams
+        __syncthreads();
+        if (tid == 0) {
+            int n = 0, rows[2] = {0, 0};
+            const uint8_t* ccol = nullptr;
+            while (n == 0) {
+                if (s_qc >= s_qend) {
+                    const int64_t q0 = (int64_t)atomicAdd(next, (unsigned long long)chunk);
+                    if (q0 >= total) break;
+                    s_qc = q0;
+                    s_qend = min(q0 + chunk, total);
+                }
+                int64_t q = s_qc;
+                for (; q < s_qend; ++q) {
+                    const int64_t p = q;
+                    int64_t a, b;
+                    decode_pair(ps, p, a, b);
+                    const int4 ma = XS.meta[a];
+                    const int4 mb = YS.meta[b];
+                    if (ma.x == 0 || mb.x == 0) {
+                        if (n > 0) break;
+                        for (int m = 0; m < nm; ++m) {
+                            if (out_mode == OUT_BOTH) {
+                                out[(p * 2 + 0) * nm + m] = __builtin_nan("");
+                                out[(p * 2 + 1) * nm + m] = __builtin_nan("");
+                            } else {
+                                out[p * nm + m] = __builtin_nan("");
+                            }
+                        }
+                        if (sout) {
+                            const int ne = ma.x + mb.x;
+                            sout[p] = ne == 0 ? 0 : sc0.eo + sc0.ee * (ne - 1);
+                        }
+                        continue;
+                    }
+                    const bool swp = mb.x <= ma.x;
+                    const uint8_t* cseq = swp ? XS.bytes + XS.offs[a] : YS.bytes + YS.offs[b];
+                    const int4 rm = swp ? mb : ma;
+                    const int sm = n & 1;
+                    if (n > 0 && (cseq != ccol || rows[sm] + rm.x > cap_rows)) break;
+                    if (n == 0) {
+                        const int4 cm = swp ? ma : mb;
+                        ccol = cseq;
+                        chs[cur] = AtChain{cseq, 0, cm.x, cm.y, cm.z};
+                    }
+                    tab[cur][n] = ChainPair{swp ? YS.bytes + YS.offs[b] : XS.bytes + XS.offs[a], p, rm.x, rm.y,
+                                            rm.z, rows[sm], swp ? 1 : 0, sm};
+                    rows[sm] += rm.x;
+                    ++n;
+                }
+                s_qc = q;
+            }
+            if (n > 0) chs[cur].n = n;
+            s_n = n;
+            s_rows[0] = rows[0];
+            s_rows[1] = rows[1];
+            fin_n[0] = fin_n[1] = 0u;
+        }
+        __syncthreads();
+        const int n = s_n;
+        const int rows0 = s_rows[0], rows1 = s_rows[1];
+        const int pb = cur ^ 1;
+        if (walker) walk_init(pb, prev_n);
+        if (n == 0) {
+            if (walker) walk_run(pb, -1);
+            break;
+        }
+        const int nB = chs[cur].nB;
+
+        // ---- fill-lane column constants (once per chain)
+        const int j0 = (w * 64 + lane) * K + 1;
+        if (!walker) {
+            const uint8_t* cseq = chs[cur].cseq;
+            uint32_t ew[4][KW];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < KW; ++q) ew[r][q] = 0u;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int j = j0 + k;
+                uint32_t c = 0u;
+                if (j <= nB) c = cseq[j - 1];
+                colb[tid * K + k] = (uint8_t)c;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int s = (j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi;
+                    ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
+                }
+                const int ox = (j == nB) ? sc.eo : sc.io;
+                colc[k][tid] = pk2(ox, ox);
+                if (!DEF) {
+                    const int ex = (j == nB) ? sc.ee : sc.ie;
+                    colx[DEF ? 0 : k][tid] = pk2(ex, ex);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < KW; ++q) eqt[r][tid][q] = ew[r][q];
+        }
+        if (tid < 64) xinfo[0][tid] = a2_row_info(tab[cur], n, 0, rows0, tid);
+        else if (tid < 128) xinfo[1][tid - 64] = a2_row_info(tab[cur], n, 1, rows1, tid - 64);
+        uint32_t stG[K], stX[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int g0 = sc.eo + sc.ee * (j0 + k - 1);
+            stG[k] = pk2(g0, g0);
+            stX[k] = NEG16X2;
+        }
+        uint32_t payF = NEG16X2, payY = NEG16X2;
+        uint32_t carry = 0u;
+        const uint2* ring_in = (w > 0 && !walker) ? ring + (size_t)(w - 1) * RING : nullptr;
+        uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
+        uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
+        __syncthreads();  // xinfo block 0, column tables
+
+        const int rmax = max(rows0, rows1);
+        const int nsteps = rmax + 63;
+        const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
+        const int nint = nblk + WAVE_LAG * (W - 1);
+        for (int it = 0; it < nint; ++it) {
+            if (walker) {
+                walk_run(pb, hops);
+            } else {
+                const int blk = it - WAVE_LAG * w;
+                if (blk >= 0 && blk < nblk) {
+                    const int s0 = blk * INTERVAL;
+                    const int s1 = min(s0 + INTERVAL, nsteps);
+                    for (int s = s0; s < s1; ++s) {
+                        const int g = s - lane;
+                        const uint32_t x0 = g >= 0 ? xinfo[0][g & (XR - 1)] : A1C_NONE;
+                        const uint32_t x1 = g >= 0 ? xinfo[1][g & (XR - 1)] : A1C_NONE;
+                        uint32_t inF, inY;
+                        if (w == 0) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
+                            const int i0 = (int)((x0 >> 18) & 0xFFFu), i1 = (int)((x1 >> 18) & 0xFFFu);
+                            inF = shr_old(payF, pk2(sc.eo + sc.ee * (i0 - 1), sc.eo + sc.ee * (i1 - 1)));
+                            inY = shr_old(payY, NEG16X2);
+                        } else {
+                            const uint2 o = ring_in[(s + 1) & (RING - 1)];
+                            inF = shr_old(payF, o.x);
+                            inY = shr_old(payY, o.y);
+                        }
+                        const bool a0 = !(x0 & A1C_NONE), a1 = !(x1 & A1C_NONE);
+                        if (a0 || a1) {
+                            if ((x0 & A1C_FIRST) || (x1 & A1C_FIRST)) {  // a new pair starts in a stream
+                                uint32_t m = ((x0 & A1C_FIRST) ? 0xFFFFu : 0u) | ((x1 & A1C_FIRST) ? 0xFFFF0000u : 0u);
+                                int jb = tid * K;
+                                asm volatile("" : "+v"(jb), "+v"(m));
+#pragma unroll
+                                for (int k = 0; k < K; ++k) {
+                                    const int g0 = sc.eo + sc.ee * (jb + k);
+                                    stG[k] = (pk2(g0, g0) & m) | (stG[k] & ~m);
+                                    stX[k] = (NEG16X2 & m) | (stX[k] & ~m);
+                                }
+                                const int c0 = jb == 0 ? 1 : sc.eo + sc.ee * (jb - 1);
+                                carry = (pk2(c0, c0) & m) | (carry & ~m);
+                            }
+                            // substitution words of both rows
+                            const uint32_t e0 = (x0 >> 11) & 7u, e1 = (x1 >> 11) & 7u;
+                            uint32_t eq0[KW], eq1[KW];
+                            {
+                                const uint32_t* t0 = eqt[e0 & 3u][tid];
+                                const uint32_t* t1 = eqt[e1 & 3u][tid];
+#pragma unroll
+                                for (int q = 0; q < KW; ++q) {
+                                    eq0[q] = t0[q];
+                                    eq1[q] = t1[q];
+                                }
+                            }
+                            if (e0 >= 4u || e1 >= 4u) {  // a row byte other than A/C/G/T: compare bytes
+#pragma unroll
+                                for (int q = 0; q < KW; ++q) {
+                                    uint32_t v0 = 0u, v1 = 0u;
+#pragma unroll
+                                    for (int h = 0; h < 2; ++h) {
+                                        const uint32_t cb_ = colb[tid * K + 2 * q + h];
+                                        const int s0_ = (cb_ != 0u && cb_ == (x0 & 0xFFu)) ? sc.ma : sc.mi;
+                                        const int s1_ = (cb_ != 0u && cb_ == (x1 & 0xFFu)) ? sc.ma : sc.mi;
+                                        v0 |= ((uint32_t)s0_ & 0xFFFFu) << (16 * h);
+                                        v1 |= ((uint32_t)s1_ & 0xFFFFu) << (16 * h);
+                                    }
+                                    if (e0 >= 4u) eq0[q] = v0;
+                                    if (e1 >= 4u) eq1[q] = v1;
+                                }
+                            }
+                            const bool l0 = (x0 & A1C_LAST) != 0u, l1 = (x1 & A1C_LAST) != 0u;
+                            const uint32_t oy = pk2(l0 ? sc.eo : sc.io, l1 ? sc.eo : sc.io);
+                            const uint32_t ey = DEF ? pk2(sc.ie, sc.ie) : pk2(l0 ? sc.ee : sc.ie, l1 ? sc.ee : sc.ie);
+                            at_s2 d = as_s2(carry);
+                            at_s2 F = as_s2(inF), Y = as_s2(inY);
+                            uint32_t acc[KW];
+#pragma unroll
+                            for (int k = 0; k < K; ++k) {
+                                const at_s2 G = as_s2(stG[k]), X = as_s2(stX[k]);
+                                const at_s2 nd = pmax(G, X);
+                                const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
+                                const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
+                                const at_s2 M = as_s2(as_u32(d) | 0x00010001u) + sM;
+                                const at_s2 ex = DEF ? (at_s2){(short)sc.ie, (short)sc.ie} : as_s2(colx[DEF ? 0 : k][tid]);
+                                const at_s2 cg = G + as_s2(colc[k][tid]), cx = X + ex;
+                                const at_s2 Xn = as_s2(as_u32(pmax(cg, cx)) & 0xFFFEFFFEu);
+                                const at_s2 cf = F + as_s2(oy), cy = Y + as_s2(ey);
+                                const at_s2 Yn = as_s2(as_u32(pmax(cf, cy)) & 0xFFFEFFFEu);
+                                const at_s2 Gn = pmax(M, Yn), Fn = pmax(M, Xn);
+                                const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), psign(Gn - Xn));
+                                const uint32_t tw = (as_u32(Gn) & 0x00010001u) | ((as_u32(Fn) << 1) & 0x00020002u);
+                                const uint32_t code = (as_u32(t2 << (at_s2){2, 2}) & 0xFFFCFFFCu) | tw;
+                                if (k % 2 == 0) acc[k / 2] = code;
+                                else acc[k / 2] = __builtin_amdgcn_perm(code, acc[k / 2], 0x06040200u);
+                                stG[k] = as_u32(Gn);
+                                stX[k] = as_u32(Xn);
+                                F = Fn;
+                                Y = Yn;
+                                d = nd;
+                            }
+                            payF = as_u32(F);
+                            payY = as_u32(Y);
+                            if (j0 <= nB) {
+                                uint32_t* dst = (uint32_t*)(trb + ((size_t)s * NT + tid) * (2 * K));
+                                if constexpr (K == 8) {
+                                    *(uint4*)dst = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+                                } else {
+#pragma unroll
+                                    for (int q = 0; q < KW; ++q) dst[q] = acc[q];
+                                }
+                            }
+                            if (W > 1 && ring_out != nullptr && lane == 63)
+                                ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
+                            if ((l0 || l1) && tid == (nB - 1) / K) {  // this lane owns column nB: final scores
+                                const int out_k = (nB - 1) % K;
+                                uint32_t eG = stG[0], eX = stX[0];
+#pragma unroll
+                                for (int k = 1; k < K; ++k) {
+                                    uint32_t m = (k == out_k) ? ~0u : 0u;
+                                    asm volatile("" : "+v"(m));
+                                    eG = (stG[k] & m) | (eG & ~m);
+                                    eX = (stX[k] & m) | (eX & ~m);
+                                }
+                                const at_s2 e = pmax(as_s2(eG), as_s2(eX));
+                                if (l0) fin[cur][2 * fin_n[0]++] = (int)e.x;
+                                if (l1) fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
+                            }
+                        }
+                        carry = as_u32(pmax(as_s2(inF), as_s2(inY)));
+                    }
+                }
+            }
+            const int gpre = (it + 1) * INTERVAL + (tid & 63);
+            if (tid < 2 * INTERVAL && it + 1 < nblk) {
+                const int sm = tid >> 6;
+                xinfo[sm][gpre & (XR - 1)] = a2_row_info(tab[cur], n, sm, sm ? rows1 : rows0, gpre);
+            }
+            if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        }
+        if (walker) walk_run(pb, -1);
+        prev_n = n;
+        cur ^= 1;
+    }
+}
+
+}  // namespace taxi2

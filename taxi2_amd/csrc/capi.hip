@@ -19,6 +19,7 @@
 #include "align1c_kernel.hpp"
 #include "align_kernel.hpp"
 #include "alignt_kernel.hpp"
+#include "alignt2_kernel.hpp"
 #include "ncd_kernels.hpp"
 #include "format_kernels.hpp"
 #include "common.hpp"
@@ -372,18 +373,49 @@ const VariantT* pick_variantt(const KScores& k, int max_len) {
     return nullptr;
 }
 
+// Packed variants (two pairs per lane in 16-bit halves, alignt2_kernel.hpp); same launch shape.
+#define T2_VARIANTT2(K, W, DEF, OCC) \
+    VariantT{K, W, OCC, DEF, (const void*)&k_alignt2<K, W, DEF, OCC>, &launch_alignt2<K, W, DEF, OCC>}
+
+template <int K, int W, bool DEF, int OCC>
+void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
+                    int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
+                    unsigned long long* nx) {
+    hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
+                       hops, nx);
+}
+
+const VariantT kAlignT2[] = {
+    T2_VARIANTT2(4, 1, true, 5),  T2_VARIANTT2(8, 1, true, 5),  T2_VARIANTT2(8, 2, true, 5),
+    T2_VARIANTT2(4, 1, false, 5), T2_VARIANTT2(8, 1, false, 5), T2_VARIANTT2(8, 2, false, 5),
+};
+
+const VariantT* pick_variantt2(const KScores& k, int max_len) {
+    const bool def = is_default(k);
+    for (const auto& v : kAlignT2)
+        if (v.def == def && 64 * v.K * v.W >= max_len) return &v;
+    return nullptr;
+}
+
+// packed: two streams per chain, two trace bytes per lane-column and step
 int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
-                        hipStream_t st, int max_len) {
-    const int64_t resident = (int64_t)ctx->num_cus * std::max(1, 4 * v.occ / (v.W + 1));
+                        hipStream_t st, int max_len, bool packed) {
+    // resident workgroups of the kernel (VGPR and LDS limits), persistent grid
+    int per_cu = 0;
+    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 64 * (v.W + 1), 0));
+    const int64_t resident = (int64_t)ctx->num_cus * std::max(1, per_cu);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ps.count, resident));
     // chunk (pairs per cursor step): TAXI2_AT_CHUNK forces 1..AT_CHUNK, else the kernel's automatic
     // rule (at least ~8 chunks per workgroup); it bounds the rows of a chain, hence the buffers
+    const int cmax = packed ? AT2_CHUNK : AT_CHUNK;
     int chunk = 0;
-    if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(AT_CHUNK, atoi(c)));
-    const int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(AT_CHUNK, ps.count / (grid * 8)));
-    const int cap_rows = (int)eff * std::max(1, max_len);
-    const size_t bb = at_buf_bytes(cap_rows, v.K, v.W);
+    if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(cmax, atoi(c)));
+    const int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(cmax, ps.count / (grid * 8)));
+    // rows per stream: a stream takes every other pair of a chain
+    const int64_t per_stream = packed ? (eff + 1) / 2 : eff;
+    const int cap_rows = (int)per_stream * std::max(1, max_len);
+    const size_t bb = at_buf_bytes(cap_rows, packed ? 2 * v.K : v.K, v.W);
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
     int hops = 16;
     if (const char* h = getenv("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
@@ -411,10 +443,12 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
     if (!is_linear(k) && !getenv("TAXI2_NO_ALIGNT")) {
-        const VariantT* vt = pick_variantt(k, max_len);
+        // packed 16-bit fill when every difference fits int16 (TAXI2_NO_PACKED=1: 32-bit fill)
+        const bool packed = at_fits16(k, max_len) && !getenv("TAXI2_NO_PACKED");
+        const VariantT* vt = packed ? pick_variantt2(k, max_len) : pick_variantt(k, max_len);
         if (vt) {
             if (ps.count <= 0) return 0;
-            return launch_alignt_pairs(ctx, *vt, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, max_len);
+            return launch_alignt_pairs(ctx, *vt, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, max_len, packed);
         }
     }
     if (!is_linear(k) && max_len <= A1_MAX_LEN_LONG && !getenv("TAXI2_NO_ALIGN1")) {

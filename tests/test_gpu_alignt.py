@@ -1,11 +1,12 @@
-"""GPU parity of the trace-and-walk aligner (taxi2_amd/csrc/alignt_kernel.hpp), the default for
-Gotoh scores up to 1 024 columns: the fill stores one byte of tie information per cell and a
-walker wave traces both Biopython first paths (priority M>Ix>Iy for (a, b), M>Iy>Ix for
-(b, a)).
+"""GPU parity of the trace-and-walk aligners (taxi2_amd/csrc/alignt_kernel.hpp and its packed
+two-pairs-per-lane form alignt2_kernel.hpp, the default for Gotoh scores up to 1 024 columns):
+the fill stores one byte of tie information per cell and a walker wave traces both Biopython
+first paths (priority M>Ix>Iy for (a, b), M>Iy>Ix for (b, a)).
 
 Every case is checked against the C restatement (oracle/taxi2_oracle.c, scores bit-exact,
 p / p-gaps bit-exact, jc / k2p within 1e-12) AND against the forward-carry kernels
-(TAXI2_NO_ALIGNT=1), bit for bit.  TAXI2_AT_CHUNK forces long chains on small inputs and
+(TAXI2_NO_ALIGNT=1), bit for bit; the packed kernel also against the 32-bit one
+(TAXI2_NO_PACKED=1).  TAXI2_AT_CHUNK forces long chains on small inputs and
 TAXI2_AT_HOPS=1 starves the walker so that most walks finish in the post-chain drain.
 """
 
@@ -68,11 +69,15 @@ def test_alignt_triangle(engine, oracle_c, env):
         got, gsc = _with_env(env, lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
         old, osc = _with_env({"TAXI2_NO_ALIGNT": "1"},
                              lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
+        t32, t32sc = _with_env(dict(env, TAXI2_NO_PACKED="1"),
+                               lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
         exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
         assert np.array_equal(gsc[nonempty], esc[nonempty])
         assert_metrics_equal(got, exp)
         assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(old, nan=9.0))
         assert np.array_equal(gsc, osc)
+        assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(t32, nan=9.0))
+        assert np.array_equal(gsc, t32sc)
         asym = ~np.all(np.isclose(np.nan_to_num(exp[:, 0]), np.nan_to_num(exp[:, 1])), axis=1)
         assert asym.sum() > 0  # the two orientations really differ somewhere
     # an offset block of the triangle (chunks start mid-row)
@@ -83,7 +88,7 @@ def test_alignt_triangle(engine, oracle_c, env):
     st.free()
 
 
-@pytest.mark.parametrize("env", [{}, {"TAXI2_AT_CHUNK": "5"}])
+@pytest.mark.parametrize("env", [{}, {"TAXI2_AT_CHUNK": "5"}, {"TAXI2_NO_PACKED": "1"}])
 def test_alignt_rectangle(engine, oracle_c, env):
     """One ordered orientation per pair (versusReference): the walk of the (query, ref) slot,
     with queries longer and shorter than the references (rows / columns swapped)."""
@@ -102,15 +107,16 @@ def test_alignt_rectangle(engine, oracle_c, env):
     rs.free()
 
 
-def test_alignt_bench_shape(engine, oracle_c):
+@pytest.mark.parametrize("packed", [True, False])
+def test_alignt_bench_shape(engine, oracle_c, packed):
     """The bench generator (config 3, 1 000 bp, unrelated families) with chains of 8 pairs."""
     from taxi2_amd._native import tri_pairs
 
     seqs = family_sequences(30, 1000, 0x7A12, ancestors=6)
     st = engine.upload(seqs, align=True)
     a, b = tri_pairs(len(seqs))
-    got, gsc = _with_env({"TAXI2_AT_CHUNK": "8"},
-                         lambda: engine.all_pairs(st, 0, len(a), METRICS, None, with_scores=True))
+    env = {"TAXI2_AT_CHUNK": "8"} if packed else {"TAXI2_AT_CHUNK": "8", "TAXI2_NO_PACKED": "1"}
+    got, gsc = _with_env(env, lambda: engine.all_pairs(st, 0, len(a), METRICS, None, with_scores=True))
     exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=SCORE_SETS["default"])
     assert np.array_equal(gsc, esc)
     assert_metrics_equal(got, exp)
