@@ -19,7 +19,9 @@
 // Substitution scores come from an LDS table eqt[base][thread][K/2] of 16-bit fields (the
 // doubled match / mismatch score of each column against a row byte "ACGT"[base]); per step each
 // stream reads its row's K/2 words (one ds_read_b128), per cell one v_perm builds the packed
-// pair of scores.  Rows with any other byte build their words by byte compares (rare path).
+// pair of scores.  Rows with any other byte build their words by byte compares (rare path,
+// column bytes read from global memory).  LDS is what bounds residency here (walker state for
+// 16 walks only, 16-bit column constants broadcast to both halves with op_sel_hi).
 //
 // 16-bit range: values stay within [-(2 P (nA + nB) + 2 |eo| + 2 |io|), 2 ma min(nA, nB) + 1]
 // (P = largest per-column penalty) and the -inf boundary is -16384; the host admits a launch
@@ -43,6 +45,12 @@ __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return ((uint32_t)lo &
 __device__ __forceinline__ at_s2 psign(at_s2 d) {
     uint32_t r;
     asm("v_pk_max_i16 %0, %1, -1 op_sel_hi:[1,0]\n\tv_pk_min_i16 %0, %0, 1 op_sel_hi:[1,0]" : "=&v"(r) : "v"(as_u32(d)));
+    return as_s2(r);
+}
+// per half a + (low half of b) (b holds one 16-bit constant for both pairs)
+__device__ __forceinline__ at_s2 padd_lo(at_s2 a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(as_u32(a)), "v"(b));
     return as_s2(r);
 }
 // per half a * 4 + b
@@ -93,13 +101,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     __shared__ uint32_t fin_n[2];
     __shared__ AtChain chs[2];
     __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * RING];
-    __shared__ uint8_t colb[NT * K];
-    __shared__ uint32_t colc[K][NT];            // Ix open (both halves; end-gap score on column nB)
-    __shared__ uint32_t colx[DEF ? 1 : K][NT];  // Ix extend (non-default scores)
+    __shared__ uint16_t colc[K][NT];            // Ix open (end-gap score on column nB)
+    __shared__ uint16_t colx[DEF ? 1 : K][NT];  // Ix extend (non-default scores)
     __shared__ uint32_t eqt[4][NT][KW];         // 16-bit substitution score fields by row base
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows[2];
-    __shared__ AtWalk wks[64];
+    __shared__ AtWalk wks[2 * AT2_CHUNK];
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -120,6 +127,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
 
     auto walk_init = [&](int pb, int n) {
         const int nw = out_mode == OUT_BOTH ? 2 * n : n;
+        if (lane >= 2 * AT2_CHUNK) return;
         AtWalk& W_ = wks[lane];
         W_.st = AT_DONE;
         if (lane < nw) {
@@ -136,8 +144,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         }
     };
     auto walk_run = [&](int pb, int budget) {
-        AtWalk& W_ = wks[lane];
-        int st = W_.st;
+        AtWalk& W_ = wks[lane < 2 * AT2_CHUNK ? lane : 0];
+        int st = lane < 2 * AT2_CHUNK ? W_.st : AT_DONE;
         if (!__any(st != AT_DONE)) return;
         const int pi = W_.pi;
         const ChainPair& cp = tab[pb][pi];
@@ -221,6 +229,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             j = nj;
             st = nst;
         }
+        if (lane >= 2 * AT2_CHUNK) return;
         W_.i = i;
         W_.j = j;
         W_.st = st;
@@ -318,18 +327,13 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 const int j = j0 + k;
                 uint32_t c = 0u;
                 if (j <= nB) c = cseq[j - 1];
-                colb[tid * K + k] = (uint8_t)c;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int s = (j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi;
                     ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
                 }
-                const int ox = (j == nB) ? sc.eo : sc.io;
-                colc[k][tid] = pk2(ox, ox);
-                if (!DEF) {
-                    const int ex = (j == nB) ? sc.ee : sc.ie;
-                    colx[DEF ? 0 : k][tid] = pk2(ex, ex);
-                }
+                colc[k][tid] = (uint16_t)((j == nB) ? sc.eo : sc.io);
+                if (!DEF) colx[DEF ? 0 : k][tid] = (uint16_t)((j == nB) ? sc.ee : sc.ie);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -406,12 +410,14 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 }
                             }
                             if (e0 >= 4u || e1 >= 4u) {  // a row byte other than A/C/G/T: compare bytes
+                                const uint8_t* cseq = chs[cur].cseq;
 #pragma unroll
                                 for (int q = 0; q < KW; ++q) {
                                     uint32_t v0 = 0u, v1 = 0u;
 #pragma unroll
                                     for (int h = 0; h < 2; ++h) {
-                                        const uint32_t cb_ = colb[tid * K + 2 * q + h];
+                                        const int jc = j0 + 2 * q + h;
+                                        const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
                                         const int s0_ = (cb_ != 0u && cb_ == (x0 & 0xFFu)) ? sc.ma : sc.mi;
                                         const int s1_ = (cb_ != 0u && cb_ == (x1 & 0xFFu)) ? sc.ma : sc.mi;
                                         v0 |= ((uint32_t)s0_ & 0xFFFFu) << (16 * h);
@@ -434,8 +440,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
                                 const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
                                 const at_s2 M = as_s2(as_u32(d) | 0x00010001u) + sM;
-                                const at_s2 ex = DEF ? (at_s2){(short)sc.ie, (short)sc.ie} : as_s2(colx[DEF ? 0 : k][tid]);
-                                const at_s2 cg = G + as_s2(colc[k][tid]), cx = X + ex;
+                                const at_s2 cg = padd_lo(G, colc[k][tid]);
+                                const at_s2 cx = DEF ? X + (at_s2){(short)sc.ie, (short)sc.ie} : padd_lo(X, colx[DEF ? 0 : k][tid]);
                                 const at_s2 Xn = as_s2(as_u32(pmax(cg, cx)) & 0xFFFEFFFEu);
                                 const at_s2 cf = F + as_s2(oy), cy = Y + as_s2(ey);
                                 const at_s2 Yn = as_s2(as_u32(pmax(cf, cy)) & 0xFFFEFFFEu);
