@@ -106,6 +106,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     __shared__ uint32_t eqt[4][NT][KW];         // 16-bit substitution score fields by row base
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows[2];
+    __shared__ int s_fill;  // fill waves done with the current interval (cumulative per chain)
     __shared__ AtWalk wks[2 * AT2_CHUNK];
 
     const int tid = (int)threadIdx.x;
@@ -143,7 +144,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             W_.cb = W_.xa = W_.yb = 0u;
         }
     };
-    auto walk_run = [&](int pb, int budget) {
+    // hop until `budget` hops (< 0: unbounded) or, with target > 0, until the fill waves have
+    // signalled `target` interval completions: the walker uses exactly the time the fill waves
+    // spend on their interval and delays the barrier by at most one hop
+    auto walk_run = [&](int pb, int budget, int target) {
         AtWalk& W_ = wks[lane < 2 * AT2_CHUNK ? lane : 0];
         int st = lane < 2 * AT2_CHUNK ? W_.st : AT_DONE;
         if (!__any(st != AT_DONE)) return;
@@ -160,6 +164,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
         for (int h = 0; budget < 0 || h < budget; ++h) {
             if (!__any(st != AT_DONE)) break;
+            if (target > 0 && *(volatile int*)&s_fill >= target) break;
             if (st == AT_DONE) continue;
             int ni, nj;
             if (st == AT_M) {
@@ -301,6 +306,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             s_rows[0] = rows[0];
             s_rows[1] = rows[1];
             fin_n[0] = fin_n[1] = 0u;
+            s_fill = 0;
         }
         __syncthreads();
         const int n = s_n;
@@ -308,7 +314,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         const int pb = cur ^ 1;
         if (walker) walk_init(pb, prev_n);
         if (n == 0) {
-            if (walker) walk_run(pb, -1);
+            if (walker) walk_run(pb, -1, 0);
             break;
         }
         const int nB = chs[cur].nB;
@@ -362,7 +368,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         const int nint = nblk + WAVE_LAG * (W - 1);
         for (int it = 0; it < nint; ++it) {
             if (walker) {
-                walk_run(pb, hops);
+                walk_run(pb, hops, W * (it + 1));
             } else {
                 const int blk = it - WAVE_LAG * w;
                 if (blk >= 0 && blk < nblk) {
@@ -495,9 +501,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 xinfo[sm][gpre & (XR - 1)] = a2_row_info(tab[cur], n, sm, sm ? rows1 : rows0, gpre);
             }
             if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
+            if (!walker && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
             __syncthreads();
         }
-        if (walker) walk_run(pb, -1);
+        if (walker) walk_run(pb, -1, 0);
         prev_n = n;
         cur ^= 1;
     }

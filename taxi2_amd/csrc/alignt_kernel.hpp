@@ -100,6 +100,7 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
     __shared__ int2 colc[K][NT];  // per column: {Ix open, Ix extend} (end-gap scores on column nB)
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows;
+    __shared__ int s_fill;  // fill waves done with the current interval (cumulative per chain)
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -142,8 +143,10 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
             W_.cb = W_.xa = W_.yb = 0u;
         }
     };
-    // up to `budget` hops of every walk (budget < 0: until all are done)
-    auto walk_run = [&](int pb, int budget) {
+    // hop until `budget` hops (< 0: unbounded) or, with target > 0, until the fill waves have
+    // signalled `target` interval completions: the walker uses exactly the time the fill waves
+    // spend on their interval and delays the barrier by at most one hop
+    auto walk_run = [&](int pb, int budget, int target) {
         AtWalk& W_ = wks[lane];
         int st = W_.st;
         if (!__any(st != AT_DONE)) return;
@@ -160,6 +163,7 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
         for (int h = 0; budget < 0 || h < budget; ++h) {
             if (!__any(st != AT_DONE)) break;
+            if (target > 0 && *(volatile int*)&s_fill >= target) break;
             if (st == AT_DONE) continue;
             int ni, nj;
             if (st == AT_M) {
@@ -296,6 +300,7 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
             s_n = n;
             s_rows = rows;
             fin_n = 0u;
+            s_fill = 0;
         }
         __syncthreads();
         const int n = s_n;
@@ -304,7 +309,7 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
         if (walker) walk_init(pb, prev_n);
         if (n == 0) {
             // no more chains: finish the last chain's walks and leave
-            if (walker) walk_run(pb, -1);
+            if (walker) walk_run(pb, -1, 0);
             break;
         }
         const int nB = chs[cur].nB;
@@ -350,7 +355,7 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
         const int nint = nblk + WAVE_LAG * (W - 1);
         for (int it = 0; it < nint; ++it) {
             if (walker) {
-                walk_run(pb, hops);
+                walk_run(pb, hops, W * (it + 1));
             } else {
                 const int blk = it - WAVE_LAG * w;
                 if (blk >= 0 && blk < nblk) {
@@ -458,10 +463,11 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
             const int gpre = (it + 1) * INTERVAL + tid;
             if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a1c_row_info(tab[cur], n, rows, gpre);
             if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);  // this chain's trace stores have landed
+            if (!walker && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
             __syncthreads();
         }
         // ---- the walker finishes the previous chain (the fill waves wait at the next barrier)
-        if (walker) walk_run(pb, -1);
+        if (walker) walk_run(pb, -1, 0);
         prev_n = n;
         cur ^= 1;
     }

@@ -417,7 +417,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     const int cap_rows = (int)per_stream * std::max(1, max_len);
     const size_t bb = at_buf_bytes(cap_rows, packed ? 2 * v.K : v.K, v.W);
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
-    int hops = 16;
+    int hops = 4096;  // per-interval cap; the packed kernel stops at the fill waves' signal
     if (const char* h = getenv("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
     if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32)) return -1;
     unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
