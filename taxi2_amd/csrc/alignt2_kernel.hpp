@@ -70,18 +70,37 @@ __host__ __device__ inline bool at_fits16(const KScores& k, int max_len) {
     return lo + 2 * O + 2 * P - NEG16 + 8 < 32767 && hi + 2 * O + 2 * P - NEG16 + 8 < 32767;
 }
 
-// row info of stream-local row g: the chain pairs of stream `st` are tab[st], tab[st + 2], ...
-__device__ __forceinline__ uint32_t a2_row_info(const ChainPair* __restrict__ tab, int n, int st, int rows, int g) {
-    if (g >= rows) return A1C_NONE;
+// Row records.  One 8-byte LDS entry per step row g holds both streams: .x = two 16-bit row
+// words (stream 0 low, stream 1 high), .y = the packed column-0 boundary Ix(i, 0) = eo + ee (i-1)
+// of both rows (what wave 0's lane 0 receives from the left).  Row word bits: 0-7 the row byte,
+// 8 first row of its pair, 9 last row, 10 no row, 11-12 "ACGT" code of an exact A/C/G/T byte,
+// 13 any other byte (byte-compare substitution path).  The chain pairs of stream `st` are
+// tab[st], tab[st + 2], ...
+constexpr uint32_t A2_FIRST = 1u << 8, A2_LAST = 1u << 9, A2_NONE = 1u << 10, A2_OTHER = 1u << 13;
+
+__device__ __forceinline__ uint32_t a2_row_word(const ChainPair* __restrict__ tab, int n, int st, int rows, int g,
+                                                int& irow) {
+    irow = 0;
+    if (g >= rows) return A2_NONE;
     int k = st;
     for (int t = st + 2; t < n; t += 2)
         if (tab[t].r0 <= g) k = t;
     const ChainPair& cp = tab[k];
     const int i = g - cp.r0;
-    uint32_t v = a1_xinfo(cp.rseq[i], i, cp.fx, cp.lx);
-    if (i == 0) v |= A1C_FIRST;
-    if (i == cp.nA - 1) v |= A1C_LAST;
-    return v | ((uint32_t)(i + 1) << 18);
+    const uint32_t c = cp.rseq[i];
+    const uint32_t ec = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+    uint32_t v = c | (ec < 4u ? ec << 11 : A2_OTHER);
+    if (i == 0) v |= A2_FIRST;
+    if (i == cp.nA - 1) v |= A2_LAST;
+    irow = i + 1;
+    return v;
+}
+__device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab, int n, int rows0, int rows1, int g,
+                                               const KScores& sc) {
+    int i0, i1;
+    const uint32_t w0 = a2_row_word(tab, n, 0, rows0, g, i0);
+    const uint32_t w1 = a2_row_word(tab, n, 1, rows1, g, i1);
+    return make_uint2(w0 | (w1 << 16), pk2(sc.eo + sc.ee * (i0 - 1), sc.eo + sc.ee * (i1 - 1)));
 }
 
 template <int K, int W, bool DEF, int OCC>
@@ -95,7 +114,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     constexpr int KW = K / 2;
     const KScores sc0 = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
     const KScores sc = doubled(sc0);
-    __shared__ uint32_t xinfo[2][XR];
+    __shared__ uint2 xinfo[XR];  // row records (a2_row_record)
     __shared__ ChainPair tab[2][AT2_CHUNK];
     __shared__ int fin[2][AT2_CHUNK];
     __shared__ uint32_t fin_n[2];
@@ -111,7 +130,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
-    const int w = tid >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring pointers etc. in SGPRs
     const bool walker = w == W;
     const int nm = ms.n;
     const int64_t total = ps.count;
@@ -346,8 +365,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
 #pragma unroll
                 for (int q = 0; q < KW; ++q) eqt[r][tid][q] = ew[r][q];
         }
-        if (tid < 64) xinfo[0][tid] = a2_row_info(tab[cur], n, 0, rows0, tid);
-        else if (tid < 128) xinfo[1][tid - 64] = a2_row_info(tab[cur], n, 1, rows1, tid - 64);
+        // rows 0..63, and "no row" for the ring slots read as rows -63..-1 by the lanes the
+        // wavefront has not reached yet (overwritten only when row XR-64 is prefetched)
+        if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, sc);
+        else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(A2_NONE | (A2_NONE << 16), 0u);
         uint32_t stG[K], stX[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -375,23 +396,25 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                     const int s0 = blk * INTERVAL;
                     const int s1 = min(s0 + INTERVAL, nsteps);
                     for (int s = s0; s < s1; ++s) {
-                        const int g = s - lane;
-                        const uint32_t x0 = g >= 0 ? xinfo[0][g & (XR - 1)] : A1C_NONE;
-                        const uint32_t x1 = g >= 0 ? xinfo[1][g & (XR - 1)] : A1C_NONE;
+                        // lane id recomputed (two v_mbcnt) rather than kept live across the chain
+                        // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
+                        int ln;
+                        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+                        const int g = s - ln;
+                        const uint2 rec = xinfo[g & (XR - 1)];
+                        const uint32_t rw = rec.x;
                         uint32_t inF, inY;
                         if (w == 0) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
-                            const int i0 = (int)((x0 >> 18) & 0xFFFu), i1 = (int)((x1 >> 18) & 0xFFFu);
-                            inF = shr_old(payF, pk2(sc.eo + sc.ee * (i0 - 1), sc.eo + sc.ee * (i1 - 1)));
+                            inF = shr_old(payF, rec.y);
                             inY = shr_old(payY, NEG16X2);
                         } else {
                             const uint2 o = ring_in[(s + 1) & (RING - 1)];
                             inF = shr_old(payF, o.x);
                             inY = shr_old(payY, o.y);
                         }
-                        const bool a0 = !(x0 & A1C_NONE), a1 = !(x1 & A1C_NONE);
-                        if (a0 || a1) {
-                            if ((x0 & A1C_FIRST) || (x1 & A1C_FIRST)) {  // a new pair starts in a stream
-                                uint32_t m = ((x0 & A1C_FIRST) ? 0xFFFFu : 0u) | ((x1 & A1C_FIRST) ? 0xFFFF0000u : 0u);
+                        if ((rw & (A2_NONE | (A2_NONE << 16))) != (A2_NONE | (A2_NONE << 16))) {
+                            if (rw & (A2_FIRST | (A2_FIRST << 16))) {  // a new pair starts in a stream
+                                uint32_t m = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
                                 int jb = tid * K;
                                 asm volatile("" : "+v"(jb), "+v"(m));
 #pragma unroll
@@ -404,19 +427,22 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 carry = (pk2(c0, c0) & m) | (carry & ~m);
                             }
                             // substitution words of both rows
-                            const uint32_t e0 = (x0 >> 11) & 7u, e1 = (x1 >> 11) & 7u;
                             uint32_t eq0[KW], eq1[KW];
                             {
-                                const uint32_t* t0 = eqt[e0 & 3u][tid];
-                                const uint32_t* t1 = eqt[e1 & 3u][tid];
+                                // the per-thread table address is recomputed here (one op) rather
+                                // than kept live across the chain loop (it was spilled to scratch)
+                                const int tq = w * 64 + ln;
+                                const uint32_t* t0 = eqt[(rw >> 11) & 3u][tq];
+                                const uint32_t* t1 = eqt[(rw >> 27) & 3u][tq];
 #pragma unroll
                                 for (int q = 0; q < KW; ++q) {
                                     eq0[q] = t0[q];
                                     eq1[q] = t1[q];
                                 }
                             }
-                            if (e0 >= 4u || e1 >= 4u) {  // a row byte other than A/C/G/T: compare bytes
+                            if (rw & (A2_OTHER | (A2_OTHER << 16))) {  // a row byte other than A/C/G/T
                                 const uint8_t* cseq = chs[cur].cseq;
+                                const uint32_t b0 = rw & 0xFFu, b1 = (rw >> 16) & 0xFFu;
 #pragma unroll
                                 for (int q = 0; q < KW; ++q) {
                                     uint32_t v0 = 0u, v1 = 0u;
@@ -424,18 +450,22 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     for (int h = 0; h < 2; ++h) {
                                         const int jc = j0 + 2 * q + h;
                                         const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
-                                        const int s0_ = (cb_ != 0u && cb_ == (x0 & 0xFFu)) ? sc.ma : sc.mi;
-                                        const int s1_ = (cb_ != 0u && cb_ == (x1 & 0xFFu)) ? sc.ma : sc.mi;
+                                        const int s0_ = (cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi;
+                                        const int s1_ = (cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi;
                                         v0 |= ((uint32_t)s0_ & 0xFFFFu) << (16 * h);
                                         v1 |= ((uint32_t)s1_ & 0xFFFFu) << (16 * h);
                                     }
-                                    if (e0 >= 4u) eq0[q] = v0;
-                                    if (e1 >= 4u) eq1[q] = v1;
+                                    if (rw & A2_OTHER) eq0[q] = v0;
+                                    if (rw & (A2_OTHER << 16)) eq1[q] = v1;
                                 }
                             }
-                            const bool l0 = (x0 & A1C_LAST) != 0u, l1 = (x1 & A1C_LAST) != 0u;
-                            const uint32_t oy = pk2(l0 ? sc.eo : sc.io, l1 ? sc.eo : sc.io);
-                            const uint32_t ey = DEF ? pk2(sc.ie, sc.ie) : pk2(l0 ? sc.ee : sc.ie, l1 ? sc.ee : sc.ie);
+                            // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half
+                            const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
+                            const uint32_t oy = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
+                                                       (at_s2){(short)sc.io, (short)sc.io});
+                            const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
+                                                    : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
+                                                             (at_s2){(short)sc.ie, (short)sc.ie});
                             at_s2 d = as_s2(carry);
                             at_s2 F = as_s2(inF), Y = as_s2(inY);
                             uint32_t acc[KW];
@@ -476,7 +506,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             }
                             if (W > 1 && ring_out != nullptr && lane == 63)
                                 ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
-                            if ((l0 || l1) && tid == (nB - 1) / K) {  // this lane owns column nB: final scores
+                            if ((rw & (A2_LAST | (A2_LAST << 16))) && tid == (nB - 1) / K) {  // owner of column nB
                                 const int out_k = (nB - 1) % K;
                                 uint32_t eG = stG[0], eX = stX[0];
 #pragma unroll
@@ -487,19 +517,16 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     eX = (stX[k] & m) | (eX & ~m);
                                 }
                                 const at_s2 e = pmax(as_s2(eG), as_s2(eX));
-                                if (l0) fin[cur][2 * fin_n[0]++] = (int)e.x;
-                                if (l1) fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
+                                if (rw & A2_LAST) fin[cur][2 * fin_n[0]++] = (int)e.x;
+                                if (rw & (A2_LAST << 16)) fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
                             }
                         }
                         carry = as_u32(pmax(as_s2(inF), as_s2(inY)));
                     }
                 }
             }
-            const int gpre = (it + 1) * INTERVAL + (tid & 63);
-            if (tid < 2 * INTERVAL && it + 1 < nblk) {
-                const int sm = tid >> 6;
-                xinfo[sm][gpre & (XR - 1)] = a2_row_info(tab[cur], n, sm, sm ? rows1 : rows0, gpre);
-            }
+            const int gpre = (it + 1) * INTERVAL + tid;
+            if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, sc);
             if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
             if (!walker && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
             __syncthreads();

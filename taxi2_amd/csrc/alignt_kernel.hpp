@@ -104,7 +104,7 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
-    const int w = tid >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring pointers etc. in SGPRs
     const bool walker = w == W;
     const int nm = ms.n;
     const int64_t total = ps.count;
