@@ -386,8 +386,8 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
 }
 
 const VariantT kAlignT2[] = {
-    T2_VARIANTT2(4, 1, true, 6),  T2_VARIANTT2(8, 1, true, 6),  T2_VARIANTT2(8, 2, true, 6),
-    T2_VARIANTT2(4, 1, false, 6), T2_VARIANTT2(8, 1, false, 6), T2_VARIANTT2(8, 2, false, 6),
+    T2_VARIANTT2(4, 1, true, 6),  T2_VARIANTT2(8, 1, true, 6),  T2_VARIANTT2(6, 2, true, 6),  T2_VARIANTT2(8, 2, true, 6),
+    T2_VARIANTT2(4, 1, false, 6), T2_VARIANTT2(8, 1, false, 6), T2_VARIANTT2(6, 2, false, 6), T2_VARIANTT2(8, 2, false, 6),
 };
 
 const VariantT* pick_variantt2(const KScores& k, int max_len) {
