@@ -13,7 +13,9 @@
 // resets, end-gap row scores, column-0 boundary, substitution words) exists once per stream.
 //
 // Per cell and pair the byte is (int8) (16 sc + 4 sb + sa) << 2 | tagF << 1 | tagG with the
-// signs sa = sign(G - X), sb = sign(cg - cx), sc = sign(cf - cy) of alignt_kernel.hpp.  Bytes
+// signs sa = sign(G - X), sb = sign(cg - cx), sc = sign(cf - cy) of alignt_kernel.hpp (default
+// scores: no tagF, it follows from sa and tagG because opens <= extends; the packing is then one
+// v_bfi).  Bytes
 // are stored per lane and step as [k][stream] (2K bytes, one 16-byte store for K = 8).
 //
 // Substitution scores come from an LDS table eqt[base][thread][K/2] of 16-bit fields (the
@@ -246,7 +248,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             } else {  // how Iy(i, j) was formed
                 const int sc_ = (cu >> 4) - 1;
                 const bool fp = prio ? sc_ > 0 : sc_ >= 0;
-                nst = fp ? ((nb & 2u) ? AT_M : AT_IX) : AT_IY;
+                // tagF of (ni, nj).  Default scores (open <= extend) store none: F-path taken means
+                // F + oy >= Y + ey, impossible when Iy is the strict maximum (oy <= ey), so M >= Ix
+                // exactly when the cell's class is M (sa > 0 with tagG); Ix / Ix=Iy classes give
+                // Ix > M.
+                const bool tagF = DEF ? ((((nu & 3) - 1) > 0) && (nb & 1u)) : (nb & 2u);
+                nst = fp ? (tagF ? AT_M : AT_IX) : AT_IY;
             }
             cb = nb;
             i = ni;
@@ -483,8 +490,13 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 const at_s2 Yn = as_s2(as_u32(pmax(cf, cy)) & 0xFFFEFFFEu);
                                 const at_s2 Gn = pmax(M, Yn), Fn = pmax(M, Xn);
                                 const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), psign(Gn - Xn));
-                                const uint32_t tw = (as_u32(Gn) & 0x00010001u) | ((as_u32(Fn) << 1) & 0x00020002u);
-                                const uint32_t code = (as_u32(t2 << (at_s2){2, 2}) & 0xFFFCFFFCu) | tw;
+                                const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
+                                uint32_t code;
+                                if constexpr (DEF) {  // tagF is implied (see the walker): one v_bfi
+                                    code = (as_u32(Gn) & 0x00010001u) | (t4 & ~0x00010001u);
+                                } else {
+                                    code = t4 | (as_u32(Gn) & 0x00010001u) | ((as_u32(Fn) << 1) & 0x00020002u);
+                                }
                                 if (k % 2 == 0) acc[k / 2] = code;
                                 else acc[k / 2] = __builtin_amdgcn_perm(code, acc[k / 2], 0x06040200u);
                                 stG[k] = as_u32(Gn);
