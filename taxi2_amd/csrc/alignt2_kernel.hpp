@@ -49,6 +49,12 @@ __device__ __forceinline__ at_s2 psign(at_s2 d) {
     asm("v_pk_max_i16 %0, %1, -1 op_sel_hi:[1,0]\n\tv_pk_min_i16 %0, %0, 1 op_sel_hi:[1,0]" : "=&v"(r) : "v"(as_u32(d)));
     return as_s2(r);
 }
+// per half clamp to [-2, 1]
+__device__ __forceinline__ at_s2 pclamp21(at_s2 d) {
+    uint32_t r;
+    asm("v_pk_max_i16 %0, %1, -2 op_sel_hi:[1,0]\n\tv_pk_min_i16 %0, %0, 1 op_sel_hi:[1,0]" : "=&v"(r) : "v"(as_u32(d)));
+    return as_s2(r);
+}
 // per half a + (low half of b) (b holds one 16-bit constant for both pairs)
 __device__ __forceinline__ at_s2 padd_lo(at_s2 a, uint32_t b) {
     uint32_t r;
@@ -102,7 +108,8 @@ __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab
     int i0, i1;
     const uint32_t w0 = a2_row_word(tab, n, 0, rows0, g, i0);
     const uint32_t w1 = a2_row_word(tab, n, 1, rows1, g, i1);
-    return make_uint2(w0 | (w1 << 16), pk2(sc.eo + sc.ee * (i0 - 1), sc.eo + sc.ee * (i1 - 1)));
+    // boundary in the odd F representation of the fill: 2 Ix(i, 0) + 1
+    return make_uint2(w0 | (w1 << 16), pk2(sc.eo + sc.ee * (i0 - 1) + 1, sc.eo + sc.ee * (i1 - 1) + 1));
 }
 
 template <int K, int W, bool DEF, int OCC>
@@ -230,29 +237,35 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             }
             xa = ni >= 1 ? rs[ni - 1] : 0u;
             yb = nj >= 1 ? cs[nj - 1] : 0u;
-            // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa (balanced base-4 digits)
-            const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 21;
-            const int cu = ((int)(int8_t)(uint8_t)cb >> 2) + 21;
+            // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa, digits sa in [-2, 1],
+            // sb, sc in [-1, 1] (balanced base 4: u = code + 22 has digits sa + 2, sb + 1, sc + 1)
+            const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 22;
+            const int cu = ((int)(int8_t)(uint8_t)cb >> 2) + 22;
+            // class of (ni, nj) from sa = clamp(G - X1, -2, 1) and tagG (X1 = 2 Ix + 1, G tagged):
+            // 1 -> M if tagG else Iy; 0 -> M (M = Ix); -1 -> Ix = Iy tie; -2 -> Ix
+            const int sa = (nu & 3) - 2;
+            const bool tagG = nb & 1u;
+            const bool clsM = sa == 0 || (sa == 1 && tagG);
             int nst;
             if (ni == 0) {
                 nst = AT_IY;
             } else if (nj == 0) {
                 nst = AT_IX;
             } else if (st == AT_M) {  // best state of (ni, nj)
-                const int ca = (nu & 3) - 1;
-                nst = ca > 0 ? ((nb & 1u) ? AT_M : AT_IY) : (ca == 0 ? (prio ? AT_IY : AT_IX) : AT_IX);
-            } else if (st == AT_IX) {  // how Ix(i, j) was formed
+                nst = clsM ? AT_M : sa == 1 ? AT_IY : sa == -1 ? (prio ? AT_IY : AT_IX) : AT_IX;
+            } else if (st == AT_IX) {  // how Ix(i, j) was formed: sign of real (G + o) - (Ix + e)
                 const int sb = ((cu >> 2) & 3) - 1;
-                const bool gp = prio ? sb >= 0 : sb > 0;
-                nst = gp ? ((nb & 1u) ? AT_M : AT_IY) : AT_IX;
-            } else {  // how Iy(i, j) was formed
+                // a tie goes to G when G is M (both priorities) or, G = Iy, under B (Iy > Ix)
+                const bool gp = sb > 0 || (sb == 0 && (tagG || prio));
+                nst = gp ? (tagG ? AT_M : AT_IY) : AT_IX;
+            } else {  // how Iy(i, j) was formed: sign of real (F + o) - (Iy + e)
                 const int sc_ = (cu >> 4) - 1;
-                const bool fp = prio ? sc_ > 0 : sc_ >= 0;
-                // tagF of (ni, nj).  Default scores (open <= extend) store none: F-path taken means
+                // tagF of (ni, nj).  Default scores (open <= extend) store none: an F path needs
                 // F + oy >= Y + ey, impossible when Iy is the strict maximum (oy <= ey), so M >= Ix
-                // exactly when the cell's class is M (sa > 0 with tagG); Ix / Ix=Iy classes give
-                // Ix > M.
-                const bool tagF = DEF ? ((((nu & 3) - 1) > 0) && (nb & 1u)) : (nb & 2u);
+                // exactly when the cell's class is M; the Ix and Ix = Iy classes have Ix > M.
+                const bool tagF = DEF ? clsM : (nb & 2u);
+                // a tie goes to F under A (M, Ix > Iy) and, under B, only when F is M
+                const bool fp = sc_ > 0 || (sc_ == 0 && (tagF || !prio));
                 nst = fp ? (tagF ? AT_M : AT_IX) : AT_IY;
             }
             cb = nb;
@@ -381,9 +394,9 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         for (int k = 0; k < K; ++k) {
             const int g0 = sc.eo + sc.ee * (j0 + k - 1);
             stG[k] = pk2(g0, g0);
-            stX[k] = NEG16X2;
+            stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
         }
-        uint32_t payF = NEG16X2, payY = NEG16X2;
+        uint32_t payF = NEG16X2 | 0x00010001u, payY = NEG16X2;
         uint32_t carry = 0u;
         const uint2* ring_in = (w > 0 && !walker) ? ring + (size_t)(w - 1) * RING : nullptr;
         uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
@@ -428,9 +441,9 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 for (int k = 0; k < K; ++k) {
                                     const int g0 = sc.eo + sc.ee * (jb + k);
                                     stG[k] = (pk2(g0, g0) & m) | (stG[k] & ~m);
-                                    stX[k] = (NEG16X2 & m) | (stX[k] & ~m);
+                                    stX[k] = ((NEG16X2 | 0x00010001u) & m) | (stX[k] & ~m);
                                 }
-                                const int c0 = jb == 0 ? 1 : sc.eo + sc.ee * (jb - 1);
+                                const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1)) | 1;  // diagonal, | 1
                                 carry = (pk2(c0, c0) & m) | (carry & ~m);
                             }
                             // substitution words of both rows
@@ -466,45 +479,55 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     if (rw & (A2_OTHER << 16)) eq1[q] = v1;
                                 }
                             }
-                            // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half
+                            // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
+                            // minus 1 because the F payload is kept odd (below)
                             const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
-                            const uint32_t oy = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
-                                                       (at_s2){(short)sc.io, (short)sc.io});
+                            const uint32_t oy1 = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
+                                                        (at_s2){(short)(sc.io - 1), (short)(sc.io - 1)});
                             const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
                                                     : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
                                                              (at_s2){(short)sc.ie, (short)sc.ie});
-                            at_s2 d = as_s2(carry);
-                            at_s2 F = as_s2(inF), Y = as_s2(inY);
+                            // Representation (doubled scores): G = max(M, Iy) tagged (M odd, Iy even);
+                            // Ix and F = max(M, Ix) kept ODD (2v + 1, no tag): then the diagonal
+                            // max(G, Ix) | 1 = max(G | 1, X1) needs no fix-up, Ix candidates built on G | 1
+                            // and X1 stay odd and F + (oy - 1) stays even, so no "& ~1" either.  Ties the
+                            // tags used to break inside cg - cx and cf - cy now show as 0 signs, and the
+                            // walker breaks them with the neighbour's tag (it reads that byte anyway).
+                            at_s2 d1 = as_s2(carry);
+                            at_s2 F1 = as_s2(inF), Y = as_s2(inY);
                             uint32_t acc[KW];
 #pragma unroll
                             for (int k = 0; k < K; ++k) {
-                                const at_s2 G = as_s2(stG[k]), X = as_s2(stX[k]);
-                                const at_s2 nd = pmax(G, X);
+                                const at_s2 G = as_s2(stG[k]), X1 = as_s2(stX[k]);
+                                const at_s2 G1 = as_s2(as_u32(G) | 0x00010001u);
+                                const at_s2 nd1 = pmax(G1, X1);
                                 const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
                                 const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-                                const at_s2 M = as_s2(as_u32(d) | 0x00010001u) + sM;
-                                const at_s2 cg = padd_lo(G, colc[k][tid]);
-                                const at_s2 cx = DEF ? X + (at_s2){(short)sc.ie, (short)sc.ie} : padd_lo(X, colx[DEF ? 0 : k][tid]);
-                                const at_s2 Xn = as_s2(as_u32(pmax(cg, cx)) & 0xFFFEFFFEu);
-                                const at_s2 cf = F + as_s2(oy), cy = Y + as_s2(ey);
-                                const at_s2 Yn = as_s2(as_u32(pmax(cf, cy)) & 0xFFFEFFFEu);
-                                const at_s2 Gn = pmax(M, Yn), Fn = pmax(M, Xn);
-                                const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), psign(Gn - Xn));
+                                const at_s2 M = d1 + sM;
+                                const at_s2 cg = padd_lo(G1, colc[k][tid]);
+                                const at_s2 cx = DEF ? X1 + (at_s2){(short)sc.ie, (short)sc.ie} : padd_lo(X1, colx[DEF ? 0 : k][tid]);
+                                const at_s2 Xn1 = pmax(cg, cx);
+                                const at_s2 cf = F1 + as_s2(oy1), cy = Y + as_s2(ey);
+                                const at_s2 Yn = pmax(cf, cy);
+                                const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
+                                const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
                                 const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
                                 uint32_t code;
                                 if constexpr (DEF) {  // tagF is implied (see the walker): one v_bfi
                                     code = (as_u32(Gn) & 0x00010001u) | (t4 & ~0x00010001u);
-                                } else {
-                                    code = t4 | (as_u32(Gn) & 0x00010001u) | ((as_u32(Fn) << 1) & 0x00020002u);
+                                } else {  // tagF = M >= Ix  <=>  M - X1 >= 0 (both odd)
+                                    const uint32_t ge = ~as_u32(M - Xn1) >> 14;  // bit 15 / 31 -> bit 1 / 17
+                                    code = t4 | (as_u32(Gn) & 0x00010001u) | (ge & 0x00020002u);
                                 }
                                 if (k % 2 == 0) acc[k / 2] = code;
                                 else acc[k / 2] = __builtin_amdgcn_perm(code, acc[k / 2], 0x06040200u);
                                 stG[k] = as_u32(Gn);
-                                stX[k] = as_u32(Xn);
-                                F = Fn;
+                                stX[k] = as_u32(Xn1);
+                                F1 = Fn1;
                                 Y = Yn;
-                                d = nd;
+                                d1 = nd1;
                             }
+                            const at_s2 F = F1;
                             payF = as_u32(F);
                             payY = as_u32(Y);
                             if (j0 <= nB) {
@@ -533,7 +556,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 if (rw & (A2_LAST << 16)) fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
                             }
                         }
-                        carry = as_u32(pmax(as_s2(inF), as_s2(inY)));
+                        carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1
                     }
                 }
             }
