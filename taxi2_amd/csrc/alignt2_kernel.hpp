@@ -74,7 +74,8 @@ __host__ __device__ inline bool at_fits16(const KScores& k, int max_len) {
     const long long P = std::max({ab(k.ma), ab(k.mi), ab(k.ie), ab(k.ee)});
     const long long O = std::max(ab(k.io), ab(k.eo));
     const long long lo = 2 * (P * 2 * (long long)max_len + 2 * O + 2);
-    const long long hi = 2 * (long long)ab(k.ma) * max_len + 2;
+    // + the drift of the default-score fill: stored values exceed the true ones by (i + j) |2 ie|
+    const long long hi = 2 * (long long)ab(k.ma) * max_len + 2 + 2 * (long long)ab(k.ie) * 2 * max_len;
     return lo + 2 * O + 2 * P - NEG16 + 8 < 32767 && hi + 2 * O + 2 * P - NEG16 + 8 < 32767;
 }
 
@@ -104,12 +105,12 @@ __device__ __forceinline__ uint32_t a2_row_word(const ChainPair* __restrict__ ta
     return v;
 }
 __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab, int n, int rows0, int rows1, int g,
-                                               const KScores& sc) {
+                                               const KScores& sc, int dz) {
     int i0, i1;
     const uint32_t w0 = a2_row_word(tab, n, 0, rows0, g, i0);
     const uint32_t w1 = a2_row_word(tab, n, 1, rows1, g, i1);
-    // boundary in the odd F representation of the fill: 2 Ix(i, 0) + 1
-    return make_uint2(w0 | (w1 << 16), pk2(sc.eo + sc.ee * (i0 - 1) + 1, sc.eo + sc.ee * (i1 - 1) + 1));
+    // boundary in the fill's representation: odd F (2 Ix(i, 0) + 1), drift -i dz (see the cell)
+    return make_uint2(w0 | (w1 << 16), pk2(sc.eo + sc.ee * (i0 - 1) - i0 * dz + 1, sc.eo + sc.ee * (i1 - 1) - i1 * dz + 1));
 }
 
 template <int K, int W, bool DEF, int OCC>
@@ -123,6 +124,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     constexpr int KW = K / 2;
     const KScores sc0 = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
     const KScores sc = doubled(sc0);
+    // Drift (default scores, where every gap extend is ie): cells store V(i, j) - (i + j) dz, so
+    // Ix(i, j) = max(G(i-1, j) + o, Ix(i-1, j) + e) becomes max(G + (o - dz), Ix) and likewise for
+    // Iy: both extend additions vanish; M absorbs -2 dz in its substitution table.
+    const int dz = DEF ? sc.ie : 0;
     __shared__ uint2 xinfo[XR];  // row records (a2_row_record)
     __shared__ ChainPair tab[2][AT2_CHUNK];
     __shared__ int fin[2][AT2_CHUNK];
@@ -224,7 +229,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 else o = out + p * nm;
                 for (int m = 0; m < nm; ++m)
                     o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
-                if (sout && (out_mode != OUT_BOTH || !prio)) sout[p] = fin[pb][pi] >> 1;
+                if (sout && (out_mode != OUT_BOTH || !prio))  // undo the drift of cell (nA, nB)
+                    sout[p] = (fin[pb][pi] + (cp.nA + chs[pb].nB) * dz) >> 1;
                 st = AT_DONE;
                 continue;
             }
@@ -374,10 +380,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 if (j <= nB) c = cseq[j - 1];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int s = (j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi;
+                    const int s = ((j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi) - 2 * dz;
                     ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
                 }
-                colc[k][tid] = (uint16_t)((j == nB) ? sc.eo : sc.io);
+                colc[k][tid] = (uint16_t)(((j == nB) ? sc.eo : sc.io) - dz);
                 if (!DEF) colx[DEF ? 0 : k][tid] = (uint16_t)((j == nB) ? sc.ee : sc.ie);
             }
 #pragma unroll
@@ -387,12 +393,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         }
         // rows 0..63, and "no row" for the ring slots read as rows -63..-1 by the lanes the
         // wavefront has not reached yet (overwritten only when row XR-64 is prefetched)
-        if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, sc);
+        if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, sc, dz);
         else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(A2_NONE | (A2_NONE << 16), 0u);
         uint32_t stG[K], stX[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int g0 = sc.eo + sc.ee * (j0 + k - 1);
+            const int g0 = sc.eo + sc.ee * (j0 + k - 1) - (j0 + k) * dz;
             stG[k] = pk2(g0, g0);
             stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
         }
@@ -439,11 +445,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 asm volatile("" : "+v"(jb), "+v"(m));
 #pragma unroll
                                 for (int k = 0; k < K; ++k) {
-                                    const int g0 = sc.eo + sc.ee * (jb + k);
+                                    const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
                                     stG[k] = (pk2(g0, g0) & m) | (stG[k] & ~m);
                                     stX[k] = ((NEG16X2 | 0x00010001u) & m) | (stX[k] & ~m);
                                 }
-                                const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1)) | 1;  // diagonal, | 1
+                                // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
+                                const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1) - jb * dz) | 1;
                                 carry = (pk2(c0, c0) & m) | (carry & ~m);
                             }
                             // substitution words of both rows
@@ -470,8 +477,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     for (int h = 0; h < 2; ++h) {
                                         const int jc = j0 + 2 * q + h;
                                         const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
-                                        const int s0_ = (cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi;
-                                        const int s1_ = (cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi;
+                                        const int s0_ = ((cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi) - 2 * dz;
+                                        const int s1_ = ((cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi) - 2 * dz;
                                         v0 |= ((uint32_t)s0_ & 0xFFFFu) << (16 * h);
                                         v1 |= ((uint32_t)s1_ & 0xFFFFu) << (16 * h);
                                     }
@@ -483,7 +490,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             // minus 1 because the F payload is kept odd (below)
                             const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
                             const uint32_t oy1 = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
-                                                        (at_s2){(short)(sc.io - 1), (short)(sc.io - 1)});
+                                                        (at_s2){(short)(sc.io - dz - 1), (short)(sc.io - dz - 1)});
                             const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
                                                     : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
                                                              (at_s2){(short)sc.ie, (short)sc.ie});
@@ -505,9 +512,9 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
                                 const at_s2 M = d1 + sM;
                                 const at_s2 cg = padd_lo(G1, colc[k][tid]);
-                                const at_s2 cx = DEF ? X1 + (at_s2){(short)sc.ie, (short)sc.ie} : padd_lo(X1, colx[DEF ? 0 : k][tid]);
+                                const at_s2 cx = DEF ? X1 : padd_lo(X1, colx[DEF ? 0 : k][tid]);  // drift: + ie - dz = 0
                                 const at_s2 Xn1 = pmax(cg, cx);
-                                const at_s2 cf = F1 + as_s2(oy1), cy = Y + as_s2(ey);
+                                const at_s2 cf = F1 + as_s2(oy1), cy = DEF ? Y : Y + as_s2(ey);
                                 const at_s2 Yn = pmax(cf, cy);
                                 const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
                                 const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
@@ -561,7 +568,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 }
             }
             const int gpre = (it + 1) * INTERVAL + tid;
-            if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, sc);
+            if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, sc, dz);
             if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
             if (!walker && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
             __syncthreads();
