@@ -388,6 +388,8 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
 const VariantT kAlignT2[] = {
     T2_VARIANTT2(4, 1, true, 6),  T2_VARIANTT2(8, 1, true, 6),  T2_VARIANTT2(6, 2, true, 6),  T2_VARIANTT2(8, 2, true, 6),
     T2_VARIANTT2(4, 1, false, 6), T2_VARIANTT2(8, 1, false, 6), T2_VARIANTT2(6, 2, false, 6), T2_VARIANTT2(8, 2, false, 6),
+    // 1 025 - 2 048 columns: four fill waves + the walker (5 waves per workgroup)
+    T2_VARIANTT2(6, 4, true, 5), T2_VARIANTT2(8, 4, true, 5), T2_VARIANTT2(6, 4, false, 5), T2_VARIANTT2(8, 4, false, 5),
 };
 
 const VariantT* pick_variantt2(const KScores& k, int max_len) {
@@ -411,11 +413,19 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     const int cmax = packed ? AT2_CHUNK : AT_CHUNK;
     int chunk = 0;
     if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(cmax, atoi(c)));
-    const int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(cmax, ps.count / (grid * 8)));
-    // rows per stream: a stream takes every other pair of a chain
-    const int64_t per_stream = packed ? (eff + 1) / 2 : eff;
-    const int cap_rows = (int)per_stream * std::max(1, max_len);
-    const size_t bb = at_buf_bytes(cap_rows, packed ? 2 * v.K : v.K, v.W);
+    int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(cmax, ps.count / (grid * 8)));
+    // two trace buffers per resident workgroup: shrink the chunk (hence the chain rows) until they
+    // fit the budget (TAXI2_AT_TRACE_GB, default 40 GB of the 288 GB HBM)
+    double budget_gb = 40.0;
+    if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
+    auto buf_bytes = [&](int64_t e) {
+        const int64_t per_stream = packed ? (e + 1) / 2 : e;  // a stream takes every other pair of a chain
+        return at_buf_bytes((int)per_stream * std::max(1, max_len), packed ? 2 * v.K : v.K, v.W);
+    };
+    while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
+    chunk = (int)eff;  // the kernel must cut chains with the same bound the buffers were sized for
+    const int cap_rows = (int)(packed ? (eff + 1) / 2 : eff) * std::max(1, max_len);
+    const size_t bb = buf_bytes(eff);
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
     int hops = 4096;  // per-interval cap; the packed kernel stops at the fill waves' signal
     if (const char* h = getenv("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
