@@ -409,19 +409,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
         __syncthreads();  // xinfo block 0, column tables
 
-        const int rmax = max(rows0, rows1);
-        const int nsteps = rmax + 63;
-        const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
-        const int nint = nblk + WAVE_LAG * (W - 1);
-        for (int it = 0; it < nint; ++it) {
-            if (walker) {
-                walk_run(pb, hops, W * (it + 1));
-            } else {
-                const int blk = it - WAVE_LAG * w;
-                if (blk >= 0 && blk < nblk) {
-                    const int s0 = blk * INTERVAL;
-                    const int s1 = min(s0 + INTERVAL, nsteps);
-                    for (int s = s0; s < s1; ++s) {
+        // One systolic step of a fill wave, specialised on the wave's role: FW = wave 0 (column-0
+        // boundary from the row record, no ring read), HO = writes the ring to the next wave.  Per-step
+        // uniform branches on w cost spilled SGPR masks (v_readlane) on every step.
+        auto step = [&](auto FW, auto HO, const int s) {
                         // lane id recomputed (two v_mbcnt) rather than kept live across the chain
                         // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
                         int ln;
@@ -430,7 +421,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                         const uint2 rec = xinfo[g & (XR - 1)];
                         const uint32_t rw = rec.x;
                         uint32_t inF, inY;
-                        if (w == 0) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
+                        if constexpr (decltype(FW)::value) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
                             inF = shr_old(payF, rec.y);
                             inY = shr_old(payY, NEG16X2);
                         } else {
@@ -438,7 +429,11 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             inF = shr_old(payF, o.x);
                             inY = shr_old(payY, o.y);
                         }
-                        if ((rw & (A2_NONE | (A2_NONE << 16))) != (A2_NONE | (A2_NONE << 16))) {
+                        // Rows without a pair ("no row": before a lane's first row, after a stream's
+                        // last) are computed anyway: their halves are garbage that is never read and
+                        // is reset by the next first row, and a skip branch cost phi copies of the
+                        // whole column state on every step.
+                        {
                             if (rw & (A2_FIRST | (A2_FIRST << 16))) {  // a new pair starts in a stream
                                 uint32_t m = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
                                 int jb = tid * K;
@@ -546,8 +541,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     for (int q = 0; q < KW; ++q) dst[q] = acc[q];
                                 }
                             }
-                            if (W > 1 && ring_out != nullptr && lane == 63)
-                                ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
+                            if constexpr (decltype(HO)::value)
+                                if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
                             if ((rw & (A2_LAST | (A2_LAST << 16))) && tid == (nB - 1) / K) {  // owner of column nB
                                 const int out_k = (nB - 1) % K;
                                 uint32_t eG = stG[0], eX = stX[0];
@@ -564,6 +559,26 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             }
                         }
                         carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1
+        };
+
+        const int rmax = max(rows0, rows1);
+        const int nsteps = rmax + 63;
+        const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
+        const int nint = nblk + WAVE_LAG * (W - 1);
+        for (int it = 0; it < nint; ++it) {
+            if (walker) {
+                walk_run(pb, hops, W * (it + 1));
+            } else {
+                const int blk = it - WAVE_LAG * w;
+                if (blk >= 0 && blk < nblk) {
+                    const int s0 = blk * INTERVAL;
+                    const int s1 = min(s0 + INTERVAL, nsteps);
+                    if (w == 0) {
+                        for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
+                    } else if (w == W - 1) {
+                        for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
+                    } else {
+                        for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, s);
                     }
                 }
             }
