@@ -59,7 +59,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 19, help="unordered pairs per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=4096, help="pairs timed on the host oracle")
+    ap.add_argument("--cpu-sample", type=int, default=16384,
+                    help="pairs timed on the host oracle (~12 s on 16 host threads)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores (max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
