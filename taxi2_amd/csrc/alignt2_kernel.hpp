@@ -35,7 +35,25 @@ namespace taxi2 {
 
 typedef short at_s2 __attribute__((ext_vector_type(2)));
 
-constexpr int AT2_CHUNK = 8;          // pairs per cursor step (both streams)
+// Debug build only (-DTAXI2_GUARD, `make guard`): every global access and risky LDS index of
+// k_alignt2 is range-checked; a violation is recorded in at_guard_err (a code per site) and the
+// access skipped, so an out-of-bounds bug is located without faulting the GPU.
+#ifdef TAXI2_GUARD
+__device__ unsigned int at_guard_err;
+#define AT_OK(cond, code) ((cond) ? true : (atomicOr(&at_guard_err, (unsigned)(code)), false))
+// event counters of one launch: chains, pairs, thread-0 trace stores, fin writes, finished walks,
+// thread-0 first rows, steps, column counts
+__device__ unsigned int at_diag[8];
+#define AT_DIAG(k, v) atomicAdd(&at_diag[k], (unsigned)(v))
+#else
+#define AT_OK(cond, code) true
+#define AT_DIAG(k, v) ((void)0)
+#endif
+
+#ifndef TAXI2_AT2_CHUNK
+#define TAXI2_AT2_CHUNK 8
+#endif
+constexpr int AT2_CHUNK = TAXI2_AT2_CHUNK;  // pairs per cursor step (both streams): 2 AT2_CHUNK walks per walker wave
 constexpr int NEG16 = -16384;
 constexpr uint32_t NEG16X2 = 0xC000C000u;
 
@@ -96,7 +114,7 @@ __device__ __forceinline__ uint32_t a2_row_word(const ChainPair* __restrict__ ta
         if (tab[t].r0 <= g) k = t;
     const ChainPair& cp = tab[k];
     const int i = g - cp.r0;
-    const uint32_t c = cp.rseq[i];
+    const uint32_t c = AT_OK(i >= 0 && i < cp.nA, 16) ? cp.rseq[i] : 'A';
     const uint32_t ec = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
     uint32_t v = c | (ec < 4u ? ec << 11 : A2_OTHER);
     if (i == 0) v |= A2_FIRST;
@@ -185,7 +203,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         int st = lane < 2 * AT2_CHUNK ? W_.st : AT_DONE;
         if (!__any(st != AT_DONE)) return;
         const int pi = W_.pi;
-        const ChainPair& cp = tab[pb][pi];
+        const ChainPair& cp = tab[pb][AT_OK(st == AT_DONE || (pi >= 0 && pi < chs[pb].n), 64) ? pi : 0];
         const AtChain& ch = chs[pb];
         const int fx = cp.fx, lx = cp.lx, fy = ch.fy, ly = ch.ly, r0 = cp.r0, sm = cp.pad;
         const int prio = W_.prio;
@@ -227,9 +245,11 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 double* o;
                 if (out_mode == OUT_BOTH) o = out + (p * 2 + ((prio ^ cp.swp) ? 1 : 0)) * nm;
                 else o = out + p * nm;
+                AT_DIAG(4, 1);
+                if (AT_OK(p >= 0 && p < total, 128))
                 for (int m = 0; m < nm; ++m)
                     o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
-                if (sout && (out_mode != OUT_BOTH || !prio))  // undo the drift of cell (nA, nB)
+                if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK, 32))  // undo the drift of cell (nA, nB)
                     sout[p] = (fin[pb][pi] + (cp.nA + chs[pb].nB) * dz) >> 1;
                 st = AT_DONE;
                 continue;
@@ -239,10 +259,11 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 const int t = (nj - 1) / K;
                 const int k = nj - 1 - t * K;
                 const int s = r0 + ni - 1 + (t & 63);
-                nb = *(const volatile uint8_t*)(tr + ((size_t)s * NT + t) * (2 * K) + 2 * k);
+                const size_t off = ((size_t)s * NT + t) * (2 * K) + 2 * k + sm;
+                if (AT_OK(off < (size_t)buf_bytes, 2)) nb = *(const volatile uint8_t*)(tr - sm + off);
             }
-            xa = ni >= 1 ? rs[ni - 1] : 0u;
-            yb = nj >= 1 ? cs[nj - 1] : 0u;
+            xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, 4)) ? rs[ni - 1] : 0u;
+            yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, 8)) ? cs[nj - 1] : 0u;
             // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa, digits sa in [-2, 1],
             // sb, sc in [-1, 1] (balanced base 4: u = code + 22 has digits sa + 2, sb + 1, sc + 1)
             const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 22;
@@ -339,6 +360,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                         ccol = cseq;
                         chs[cur] = AtChain{cseq, 0, cm.x, cm.y, cm.z};
                     }
+                    if (!AT_OK(n < AT2_CHUNK, 256)) break;
                     tab[cur][n] = ChainPair{swp ? YS.bytes + YS.offs[b] : XS.bytes + XS.offs[a], p, rm.x, rm.y,
                                             rm.z, rows[sm], swp ? 1 : 0, sm};
                     rows[sm] += rm.x;
@@ -347,6 +369,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 s_qc = q;
             }
             if (n > 0) chs[cur].n = n;
+            if (n > 0) {
+                AT_DIAG(0, 1);
+                AT_DIAG(1, n);
+                AT_DIAG(6, max(rows[0], rows[1]) + 63);
+                AT_DIAG(7, chs[cur].nB);
+            }
             s_n = n;
             s_rows[0] = rows[0];
             s_rows[1] = rows[1];
@@ -434,6 +462,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                         // is reset by the next first row, and a skip branch cost phi copies of the
                         // whole column state on every step.
                         {
+                            if (tid == 0 && (rw & (A2_FIRST | (A2_FIRST << 16)))) AT_DIAG(5, 1);
                             if (rw & (A2_FIRST | (A2_FIRST << 16))) {  // a new pair starts in a stream
                                 uint32_t m = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
                                 int jb = tid * K;
@@ -532,8 +561,9 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             const at_s2 F = F1;
                             payF = as_u32(F);
                             payY = as_u32(Y);
-                            if (j0 <= nB) {
+                            if (j0 <= nB && AT_OK(((size_t)s * NT + tid + 1) * (2 * K) <= (size_t)buf_bytes, 1)) {
                                 uint32_t* dst = (uint32_t*)(trb + ((size_t)s * NT + tid) * (2 * K));
+                                if (tid == 0) AT_DIAG(2, 1);
                                 if constexpr (K == 8) {
                                     *(uint4*)dst = make_uint4(acc[0], acc[1], acc[2], acc[3]);
                                 } else {
@@ -554,8 +584,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     eX = (stX[k] & m) | (eX & ~m);
                                 }
                                 const at_s2 e = pmax(as_s2(eG), as_s2(eX));
-                                if (rw & A2_LAST) fin[cur][2 * fin_n[0]++] = (int)e.x;
-                                if (rw & (A2_LAST << 16)) fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
+                                if (rw & (A2_LAST | (A2_LAST << 16))) AT_DIAG(3, 1);
+                                if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, 32)) fin[cur][2 * fin_n[0]++] = (int)e.x;
+                                if ((rw & (A2_LAST << 16)) && AT_OK(2 * fin_n[1] + 1 < AT2_CHUNK, 32))
+                                    fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
                             }
                         }
                         carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1

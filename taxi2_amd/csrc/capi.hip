@@ -435,6 +435,25 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), ps, k, ms, chunk, out_mode, d_out,
              d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next);
     HIP_TRY(ctx, hipGetLastError());
+#ifdef TAXI2_GUARD
+    if (packed) {  // debug build: report (and clear) out-of-range accesses the guards skipped
+        unsigned int e = 0;
+        HIP_TRY(ctx, hipStreamSynchronize(st));
+        HIP_TRY(ctx, hipMemcpyFromSymbol(&e, HIP_SYMBOL(at_guard_err), sizeof e));
+        unsigned int dg[8] = {0}, z8[8] = {0};
+        HIP_TRY(ctx, hipMemcpyFromSymbol(dg, HIP_SYMBOL(at_diag), sizeof dg));
+        HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(at_diag), z8, sizeof z8));
+        fprintf(stderr, "taxi2 diag: k_alignt2<%d,%d,%d> grid %lld chunk %d count %lld: chains %u pairs %u t0stores %u "
+                "fin %u walks %u t0first %u steps %u nB %u\n", v.K, v.W, (int)v.def, (long long)grid, chunk,
+                (long long)ps.count, dg[0], dg[1], dg[2], dg[3], dg[4], dg[5], dg[6], dg[7]);
+        if (e) {
+            fprintf(stderr, "taxi2 guard: k_alignt2<%d,%d,%d> codes 0x%x (grid %lld, chunk %d, cap_rows %d, buf %zu, "
+                    "count %lld)\n", v.K, v.W, (int)v.def, e, (long long)grid, chunk, cap_rows, bb, (long long)ps.count);
+            const unsigned int z = 0;
+            HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(at_guard_err), &z, sizeof z));
+        }
+    }
+#endif
     return 0;
 }
 
