@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
           double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
           int cap_rows, int hops, unsigned long long* __restrict__ next) {
-    static_assert(K % 2 == 0 && K <= 8, "16-bit score fields: K / 2 words per stream and base");
+    static_assert(K % 2 == 0 && K <= 16, "16-bit score fields: K / 2 words per stream and base");
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
     constexpr int KW = K / 2;
@@ -314,316 +314,329 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         W_.gap = gap;
     };
 
-    for (;;) {
-        // ---- cut the next chain (thread 0); its pairs alternate between the two streams
-        __syncthreads();
-        if (tid == 0) {
-            int n = 0, rows[2] = {0, 0};
-            const uint8_t* ccol = nullptr;
-            while (n == 0) {
-                if (s_qc >= s_qend) {
-                    const int64_t q0 = (int64_t)atomicAdd(next, (unsigned long long)chunk);
-                    if (q0 >= total) break;
-                    s_qc = q0;
-                    s_qend = min(q0 + chunk, total);
-                }
-                int64_t q = s_qc;
-                for (; q < s_qend; ++q) {
-                    const int64_t p = q;
-                    int64_t a, b;
-                    decode_pair(ps, p, a, b);
-                    const int4 ma = XS.meta[a];
-                    const int4 mb = YS.meta[b];
-                    if (ma.x == 0 || mb.x == 0) {
-                        if (n > 0) break;
-                        for (int m = 0; m < nm; ++m) {
-                            if (out_mode == OUT_BOTH) {
-                                out[(p * 2 + 0) * nm + m] = __builtin_nan("");
-                                out[(p * 2 + 1) * nm + m] = __builtin_nan("");
-                            } else {
-                                out[p * nm + m] = __builtin_nan("");
-                            }
-                        }
-                        if (sout) {
-                            const int ne = ma.x + mb.x;
-                            sout[p] = ne == 0 ? 0 : sc0.eo + sc0.ee * (ne - 1);
-                        }
-                        continue;
-                    }
-                    const bool swp = mb.x <= ma.x;
-                    const uint8_t* cseq = swp ? XS.bytes + XS.offs[a] : YS.bytes + YS.offs[b];
-                    const int4 rm = swp ? mb : ma;
-                    const int sm = n & 1;
-                    if (n > 0 && (cseq != ccol || rows[sm] + rm.x > cap_rows)) break;
-                    if (n == 0) {
-                        const int4 cm = swp ? ma : mb;
-                        ccol = cseq;
-                        chs[cur] = AtChain{cseq, 0, cm.x, cm.y, cm.z};
-                    }
-                    if (!AT_OK(n < AT2_CHUNK, 256)) break;
-                    tab[cur][n] = ChainPair{swp ? YS.bytes + YS.offs[b] : XS.bytes + XS.offs[a], p, rm.x, rm.y,
-                                            rm.z, rows[sm], swp ? 1 : 0, sm};
-                    rows[sm] += rm.x;
-                    ++n;
-                }
-                s_qc = q;
-            }
-            if (n > 0) chs[cur].n = n;
-            if (n > 0) {
-                AT_DIAG(0, 1);
-                AT_DIAG(1, n);
-                AT_DIAG(6, max(rows[0], rows[1]) + 63);
-                AT_DIAG(7, chs[cur].nB);
-            }
-            s_n = n;
-            s_rows[0] = rows[0];
-            s_rows[1] = rows[1];
-            fin_n[0] = fin_n[1] = 0u;
-            s_fill = 0;
-        }
-        __syncthreads();
-        const int n = s_n;
-        const int rows0 = s_rows[0], rows1 = s_rows[1];
-        const int pb = cur ^ 1;
-        if (walker) walk_init(pb, prev_n);
-        if (n == 0) {
-            if (walker) walk_run(pb, -1, 0);
-            break;
-        }
-        const int nB = chs[cur].nB;
-
-        // ---- fill-lane column constants (once per chain)
-        const int j0 = (w * 64 + lane) * K + 1;
-        if (!walker) {
-            const uint8_t* cseq = chs[cur].cseq;
-            uint32_t ew[4][KW];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int q = 0; q < KW; ++q) ew[r][q] = 0u;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int j = j0 + k;
-                uint32_t c = 0u;
-                if (j <= nB) c = cseq[j - 1];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int s = ((j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi) - 2 * dz;
-                    ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
-                }
-                colc[k][tid] = (uint16_t)(((j == nB) ? sc.eo : sc.io) - dz);
-                if (!DEF) colx[DEF ? 0 : k][tid] = (uint16_t)((j == nB) ? sc.ee : sc.ie);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int q = 0; q < KW; ++q) eqt[r][tid][q] = ew[r][q];
-        }
-        // rows 0..63, and "no row" for the ring slots read as rows -63..-1 by the lanes the
-        // wavefront has not reached yet (overwritten only when row XR-64 is prefetched)
-        if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, sc, dz);
-        else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(A2_NONE | (A2_NONE << 16), 0u);
-        uint32_t stG[K], stX[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int g0 = sc.eo + sc.ee * (j0 + k - 1) - (j0 + k) * dz;
-            stG[k] = pk2(g0, g0);
-            stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
-        }
-        uint32_t payF = NEG16X2 | 0x00010001u, payY = NEG16X2;
-        uint32_t carry = 0u;
-        const uint2* ring_in = (w > 0 && !walker) ? ring + (size_t)(w - 1) * RING : nullptr;
-        uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
-        uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
-        __syncthreads();  // xinfo block 0, column tables
-
-        // One systolic step of a fill wave, specialised on the wave's role: FW = wave 0 (column-0
-        // boundary from the row record, no ring read), HO = writes the ring to the next wave.  Per-step
-        // uniform branches on w cost spilled SGPR masks (v_readlane) on every step.
-        auto step = [&](auto FW, auto HO, const int s) {
-                        // lane id recomputed (two v_mbcnt) rather than kept live across the chain
-                        // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
-                        int ln;
-                        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-                        const int g = s - ln;
-                        const uint2 rec = xinfo[g & (XR - 1)];
-                        const uint32_t rw = rec.x;
-                        uint32_t inF, inY;
-                        if constexpr (decltype(FW)::value) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
-                            inF = shr_old(payF, rec.y);
-                            inY = shr_old(payY, NEG16X2);
-                        } else {
-                            const uint2 o = ring_in[(s + 1) & (RING - 1)];
-                            inF = shr_old(payF, o.x);
-                            inY = shr_old(payY, o.y);
-                        }
-                        // Rows without a pair ("no row": before a lane's first row, after a stream's
-                        // last) are computed anyway: their halves are garbage that is never read and
-                        // is reset by the next first row, and a skip branch cost phi copies of the
-                        // whole column state on every step.
-                        {
-                            if (tid == 0 && (rw & (A2_FIRST | (A2_FIRST << 16)))) AT_DIAG(5, 1);
-                            if (rw & (A2_FIRST | (A2_FIRST << 16))) {  // a new pair starts in a stream
-                                uint32_t m = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
-                                int jb = tid * K;
-                                asm volatile("" : "+v"(jb), "+v"(m));
-#pragma unroll
-                                for (int k = 0; k < K; ++k) {
-                                    const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
-                                    stG[k] = (pk2(g0, g0) & m) | (stG[k] & ~m);
-                                    stX[k] = ((NEG16X2 | 0x00010001u) & m) | (stX[k] & ~m);
-                                }
-                                // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
-                                const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1) - jb * dz) | 1;
-                                carry = (pk2(c0, c0) & m) | (carry & ~m);
-                            }
-                            // substitution words of both rows
-                            uint32_t eq0[KW], eq1[KW];
-                            {
-                                // the per-thread table address is recomputed here (one op) rather
-                                // than kept live across the chain loop (it was spilled to scratch)
-                                const int tq = w * 64 + ln;
-                                const uint32_t* t0 = eqt[(rw >> 11) & 3u][tq];
-                                const uint32_t* t1 = eqt[(rw >> 27) & 3u][tq];
-#pragma unroll
-                                for (int q = 0; q < KW; ++q) {
-                                    eq0[q] = t0[q];
-                                    eq1[q] = t1[q];
-                                }
-                            }
-                            if (rw & (A2_OTHER | (A2_OTHER << 16))) {  // a row byte other than A/C/G/T
-                                const uint8_t* cseq = chs[cur].cseq;
-                                const uint32_t b0 = rw & 0xFFu, b1 = (rw >> 16) & 0xFFu;
-#pragma unroll
-                                for (int q = 0; q < KW; ++q) {
-                                    uint32_t v0 = 0u, v1 = 0u;
-#pragma unroll
-                                    for (int h = 0; h < 2; ++h) {
-                                        const int jc = j0 + 2 * q + h;
-                                        const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
-                                        const int s0_ = ((cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi) - 2 * dz;
-                                        const int s1_ = ((cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi) - 2 * dz;
-                                        v0 |= ((uint32_t)s0_ & 0xFFFFu) << (16 * h);
-                                        v1 |= ((uint32_t)s1_ & 0xFFFFu) << (16 * h);
-                                    }
-                                    if (rw & A2_OTHER) eq0[q] = v0;
-                                    if (rw & (A2_OTHER << 16)) eq1[q] = v1;
-                                }
-                            }
-                            // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
-                            // minus 1 because the F payload is kept odd (below)
-                            const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
-                            const uint32_t oy1 = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
-                                                        (at_s2){(short)(sc.io - dz - 1), (short)(sc.io - dz - 1)});
-                            const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
-                                                    : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
-                                                             (at_s2){(short)sc.ie, (short)sc.ie});
-                            // Representation (doubled scores): G = max(M, Iy) tagged (M odd, Iy even);
-                            // Ix and F = max(M, Ix) kept ODD (2v + 1, no tag): then the diagonal
-                            // max(G, Ix) | 1 = max(G | 1, X1) needs no fix-up, Ix candidates built on G | 1
-                            // and X1 stay odd and F + (oy - 1) stays even, so no "& ~1" either.  Ties the
-                            // tags used to break inside cg - cx and cf - cy now show as 0 signs, and the
-                            // walker breaks them with the neighbour's tag (it reads that byte anyway).
-                            at_s2 d1 = as_s2(carry);
-                            at_s2 F1 = as_s2(inF), Y = as_s2(inY);
-                            uint32_t acc[KW];
-#pragma unroll
-                            for (int k = 0; k < K; ++k) {
-                                const at_s2 G = as_s2(stG[k]), X1 = as_s2(stX[k]);
-                                const at_s2 G1 = as_s2(as_u32(G) | 0x00010001u);
-                                const at_s2 nd1 = pmax(G1, X1);
-                                const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
-                                const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-                                const at_s2 M = d1 + sM;
-                                const at_s2 cg = padd_lo(G1, colc[k][tid]);
-                                const at_s2 cx = DEF ? X1 : padd_lo(X1, colx[DEF ? 0 : k][tid]);  // drift: + ie - dz = 0
-                                const at_s2 Xn1 = pmax(cg, cx);
-                                const at_s2 cf = F1 + as_s2(oy1), cy = DEF ? Y : Y + as_s2(ey);
-                                const at_s2 Yn = pmax(cf, cy);
-                                const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
-                                const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
-                                const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
-                                uint32_t code;
-                                if constexpr (DEF) {  // tagF is implied (see the walker): one v_bfi
-                                    code = (as_u32(Gn) & 0x00010001u) | (t4 & ~0x00010001u);
-                                } else {  // tagF = M >= Ix  <=>  M - X1 >= 0 (both odd)
-                                    const uint32_t ge = ~as_u32(M - Xn1) >> 14;  // bit 15 / 31 -> bit 1 / 17
-                                    code = t4 | (as_u32(Gn) & 0x00010001u) | (ge & 0x00020002u);
-                                }
-                                if (k % 2 == 0) acc[k / 2] = code;
-                                else acc[k / 2] = __builtin_amdgcn_perm(code, acc[k / 2], 0x06040200u);
-                                stG[k] = as_u32(Gn);
-                                stX[k] = as_u32(Xn1);
-                                F1 = Fn1;
-                                Y = Yn;
-                                d1 = nd1;
-                            }
-                            const at_s2 F = F1;
-                            payF = as_u32(F);
-                            payY = as_u32(Y);
-                            if (j0 <= nB && AT_OK(((size_t)s * NT + tid + 1) * (2 * K) <= (size_t)buf_bytes, 1)) {
-                                uint32_t* dst = (uint32_t*)(trb + ((size_t)s * NT + tid) * (2 * K));
-                                if (tid == 0) AT_DIAG(2, 1);
-                                if constexpr (K == 8) {
-                                    *(uint4*)dst = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-                                } else {
-#pragma unroll
-                                    for (int q = 0; q < KW; ++q) dst[q] = acc[q];
-                                }
-                            }
-                            if constexpr (decltype(HO)::value)
-                                if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
-                            if ((rw & (A2_LAST | (A2_LAST << 16))) && tid == (nB - 1) / K) {  // owner of column nB
-                                const int out_k = (nB - 1) % K;
-                                uint32_t eG = stG[0], eX = stX[0];
-#pragma unroll
-                                for (int k = 1; k < K; ++k) {
-                                    uint32_t m = (k == out_k) ? ~0u : 0u;
-                                    asm volatile("" : "+v"(m));
-                                    eG = (stG[k] & m) | (eG & ~m);
-                                    eX = (stX[k] & m) | (eX & ~m);
-                                }
-                                const at_s2 e = pmax(as_s2(eG), as_s2(eX));
-                                if (rw & (A2_LAST | (A2_LAST << 16))) AT_DIAG(3, 1);
-                                if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, 32)) fin[cur][2 * fin_n[0]++] = (int)e.x;
-                                if ((rw & (A2_LAST << 16)) && AT_OK(2 * fin_n[1] + 1 < AT2_CHUNK, 32))
-                                    fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
-                            }
-                        }
-                        carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1
-        };
-
-        const int rmax = max(rows0, rows1);
-        const int nsteps = rmax + 63;
-        const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
-        const int nint = nblk + WAVE_LAG * (W - 1);
-        for (int it = 0; it < nint; ++it) {
-            if (walker) {
-                walk_run(pb, hops, W * (it + 1));
-            } else {
-                const int blk = it - WAVE_LAG * w;
-                if (blk >= 0 && blk < nblk) {
-                    const int s0 = blk * INTERVAL;
-                    const int s1 = min(s0 + INTERVAL, nsteps);
-                    if (w == 0) {
-                        for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
-                    } else if (w == W - 1) {
-                        for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
-                    } else {
-                        for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, s);
-                    }
-                }
-            }
-            const int gpre = (it + 1) * INTERVAL + tid;
-            if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, sc, dz);
-            if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
-            if (!walker && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
+    // The fill waves and the walker wave run separate copies of the chain loop (same barrier
+    // sequence): the fill state (columns, carries) is then not live across the walker code,
+    // which kept it in registers for the whole loop and spilled both to scratch.
+    auto chain_loop = [&](auto WK) {
+        constexpr bool IS_W = decltype(WK)::value;
+        for (;;) {
+            // ---- cut the next chain (thread 0); its pairs alternate between the two streams
             __syncthreads();
+            if (!IS_W && tid == 0) {
+                int n = 0, rows[2] = {0, 0};
+                const uint8_t* ccol = nullptr;
+                while (n == 0) {
+                    if (s_qc >= s_qend) {
+                        const int64_t q0 = (int64_t)atomicAdd(next, (unsigned long long)chunk);
+                        if (q0 >= total) break;
+                        s_qc = q0;
+                        s_qend = min(q0 + chunk, total);
+                    }
+                    int64_t q = s_qc;
+                    for (; q < s_qend; ++q) {
+                        const int64_t p = q;
+                        int64_t a, b;
+                        decode_pair(ps, p, a, b);
+                        const int4 ma = XS.meta[a];
+                        const int4 mb = YS.meta[b];
+                        if (ma.x == 0 || mb.x == 0) {
+                            if (n > 0) break;
+                            for (int m = 0; m < nm; ++m) {
+                                if (out_mode == OUT_BOTH) {
+                                    out[(p * 2 + 0) * nm + m] = __builtin_nan("");
+                                    out[(p * 2 + 1) * nm + m] = __builtin_nan("");
+                                } else {
+                                    out[p * nm + m] = __builtin_nan("");
+                                }
+                            }
+                            if (sout) {
+                                const int ne = ma.x + mb.x;
+                                sout[p] = ne == 0 ? 0 : sc0.eo + sc0.ee * (ne - 1);
+                            }
+                            continue;
+                        }
+                        const bool swp = mb.x <= ma.x;
+                        const uint8_t* cseq = swp ? XS.bytes + XS.offs[a] : YS.bytes + YS.offs[b];
+                        const int4 rm = swp ? mb : ma;
+                        const int sm = n & 1;
+                        if (n > 0 && (cseq != ccol || rows[sm] + rm.x > cap_rows)) break;
+                        if (n == 0) {
+                            const int4 cm = swp ? ma : mb;
+                            ccol = cseq;
+                            chs[cur] = AtChain{cseq, 0, cm.x, cm.y, cm.z};
+                        }
+                        if (!AT_OK(n < AT2_CHUNK, 256)) break;
+                        tab[cur][n] = ChainPair{swp ? YS.bytes + YS.offs[b] : XS.bytes + XS.offs[a], p, rm.x, rm.y,
+                                                rm.z, rows[sm], swp ? 1 : 0, sm};
+                        rows[sm] += rm.x;
+                        ++n;
+                    }
+                    s_qc = q;
+                }
+                if (n > 0) chs[cur].n = n;
+                if (n > 0) {
+                    AT_DIAG(0, 1);
+                    AT_DIAG(1, n);
+                    AT_DIAG(6, max(rows[0], rows[1]) + 63);
+                    AT_DIAG(7, chs[cur].nB);
+                }
+                s_n = n;
+                s_rows[0] = rows[0];
+                s_rows[1] = rows[1];
+                fin_n[0] = fin_n[1] = 0u;
+                s_fill = 0;
+            }
+            __syncthreads();
+            const int n = s_n;
+            const int rows0 = s_rows[0], rows1 = s_rows[1];
+            const int pb = cur ^ 1;
+            if constexpr (IS_W) walk_init(pb, prev_n);
+            if (n == 0) {
+                if constexpr (IS_W) walk_run(pb, -1, 0);
+                break;
+            }
+            const int nB = chs[cur].nB;
+
+            // ---- fill-lane column constants (once per chain)
+            const int j0 = (w * 64 + lane) * K + 1;
+            if constexpr (!IS_W) {
+                const uint8_t* cseq = chs[cur].cseq;
+                uint32_t ew[4][KW];
+    #pragma unroll
+                for (int r = 0; r < 4; ++r)
+    #pragma unroll
+                    for (int q = 0; q < KW; ++q) ew[r][q] = 0u;
+    #pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int j = j0 + k;
+                    uint32_t c = 0u;
+                    if (j <= nB) c = cseq[j - 1];
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int s = ((j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi) - 2 * dz;
+                        ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
+                    }
+                    colc[k][tid] = (uint16_t)(((j == nB) ? sc.eo : sc.io) - dz);
+                    if (!DEF) colx[DEF ? 0 : k][tid] = (uint16_t)((j == nB) ? sc.ee : sc.ie);
+                }
+    #pragma unroll
+                for (int r = 0; r < 4; ++r)
+    #pragma unroll
+                    for (int q = 0; q < KW; ++q) eqt[r][tid][q] = ew[r][q];
+            }
+            // rows 0..63, and "no row" for the ring slots read as rows -63..-1 by the lanes the
+            // wavefront has not reached yet (overwritten only when row XR-64 is prefetched)
+            if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, sc, dz);
+            else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(A2_NONE | (A2_NONE << 16), 0u);
+            uint32_t stG[K], stX[K];
+    #pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int g0 = sc.eo + sc.ee * (j0 + k - 1) - (j0 + k) * dz;
+                stG[k] = pk2(g0, g0);
+                stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
+            }
+            uint32_t payF = NEG16X2 | 0x00010001u, payY = NEG16X2;
+            uint32_t carry = 0u;
+            const uint2* ring_in = (w > 0 && !IS_W) ? ring + (size_t)(w - 1) * RING : nullptr;
+            uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
+            uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
+            __syncthreads();  // xinfo block 0, column tables
+
+            // One systolic step of a fill wave, specialised on the wave's role: FW = wave 0 (column-0
+            // boundary from the row record, no ring read), HO = writes the ring to the next wave.  Per-step
+            // uniform branches on w cost spilled SGPR masks (v_readlane) on every step.
+            auto step = [&](auto FW, auto HO, const int s) {
+                            // lane id recomputed (two v_mbcnt) rather than kept live across the chain
+                            // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
+                            int ln;
+                            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+                            const int g = s - ln;
+                            const uint2 rec = xinfo[g & (XR - 1)];
+                            const uint32_t rw = rec.x;
+                            uint32_t inF, inY;
+                            if constexpr (decltype(FW)::value) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
+                                inF = shr_old(payF, rec.y);
+                                inY = shr_old(payY, NEG16X2);
+                            } else {
+                                const uint2 o = ring_in[(s + 1) & (RING - 1)];
+                                inF = shr_old(payF, o.x);
+                                inY = shr_old(payY, o.y);
+                            }
+                            // Rows without a pair ("no row": before a lane's first row, after a stream's
+                            // last) are computed anyway: their halves are garbage that is never read and
+                            // is reset by the next first row, and a skip branch cost phi copies of the
+                            // whole column state on every step.
+                            {
+                                if (tid == 0 && (rw & (A2_FIRST | (A2_FIRST << 16)))) AT_DIAG(5, 1);
+                                if (rw & (A2_FIRST | (A2_FIRST << 16))) {  // a new pair starts in a stream
+                                    uint32_t m = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
+                                    int jb = tid * K;
+                                    asm volatile("" : "+v"(jb), "+v"(m));
+    #pragma unroll
+                                    for (int k = 0; k < K; ++k) {
+                                        const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
+                                        stG[k] = (pk2(g0, g0) & m) | (stG[k] & ~m);
+                                        stX[k] = ((NEG16X2 | 0x00010001u) & m) | (stX[k] & ~m);
+                                    }
+                                    // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
+                                    const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1) - jb * dz) | 1;
+                                    carry = (pk2(c0, c0) & m) | (carry & ~m);
+                                }
+                                // substitution words of both rows
+                                uint32_t eq0[KW], eq1[KW];
+                                {
+                                    // the per-thread table address is recomputed here (one op) rather
+                                    // than kept live across the chain loop (it was spilled to scratch)
+                                    const int tq = w * 64 + ln;
+                                    const uint32_t* t0 = eqt[(rw >> 11) & 3u][tq];
+                                    const uint32_t* t1 = eqt[(rw >> 27) & 3u][tq];
+    #pragma unroll
+                                    for (int q = 0; q < KW; ++q) {
+                                        eq0[q] = t0[q];
+                                        eq1[q] = t1[q];
+                                    }
+                                }
+                                if (rw & (A2_OTHER | (A2_OTHER << 16))) {  // a row byte other than A/C/G/T
+                                    const uint8_t* cseq = chs[cur].cseq;
+                                    const uint32_t b0 = rw & 0xFFu, b1 = (rw >> 16) & 0xFFu;
+    #pragma unroll
+                                    for (int q = 0; q < KW; ++q) {
+                                        uint32_t v0 = 0u, v1 = 0u;
+    #pragma unroll
+                                        for (int h = 0; h < 2; ++h) {
+                                            const int jc = j0 + 2 * q + h;
+                                            const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
+                                            const int s0_ = ((cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi) - 2 * dz;
+                                            const int s1_ = ((cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi) - 2 * dz;
+                                            v0 |= ((uint32_t)s0_ & 0xFFFFu) << (16 * h);
+                                            v1 |= ((uint32_t)s1_ & 0xFFFFu) << (16 * h);
+                                        }
+                                        if (rw & A2_OTHER) eq0[q] = v0;
+                                        if (rw & (A2_OTHER << 16)) eq1[q] = v1;
+                                    }
+                                }
+                                // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
+                                // minus 1 because the F payload is kept odd (below)
+                                const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
+                                const uint32_t oy1 = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
+                                                            (at_s2){(short)(sc.io - dz - 1), (short)(sc.io - dz - 1)});
+                                const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
+                                                        : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
+                                                                 (at_s2){(short)sc.ie, (short)sc.ie});
+                                // Representation (doubled scores): G = max(M, Iy) tagged (M odd, Iy even);
+                                // Ix and F = max(M, Ix) kept ODD (2v + 1, no tag): then the diagonal
+                                // max(G, Ix) | 1 = max(G | 1, X1) needs no fix-up, Ix candidates built on G | 1
+                                // and X1 stay odd and F + (oy - 1) stays even, so no "& ~1" either.  Ties the
+                                // tags used to break inside cg - cx and cf - cy now show as 0 signs, and the
+                                // walker breaks them with the neighbour's tag (it reads that byte anyway).
+                                at_s2 d1 = as_s2(carry);
+                                at_s2 F1 = as_s2(inF), Y = as_s2(inY);
+                                uint32_t acc[KW];
+    #pragma unroll
+                                for (int k = 0; k < K; ++k) {
+                                    const at_s2 G = as_s2(stG[k]), X1 = as_s2(stX[k]);
+                                    const at_s2 G1 = as_s2(as_u32(G) | 0x00010001u);
+                                    const at_s2 nd1 = pmax(G1, X1);
+                                    const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
+                                    const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
+                                    const at_s2 M = d1 + sM;
+                                    const at_s2 cg = padd_lo(G1, colc[k][tid]);
+                                    const at_s2 cx = DEF ? X1 : padd_lo(X1, colx[DEF ? 0 : k][tid]);  // drift: + ie - dz = 0
+                                    const at_s2 Xn1 = pmax(cg, cx);
+                                    const at_s2 cf = F1 + as_s2(oy1), cy = DEF ? Y : Y + as_s2(ey);
+                                    const at_s2 Yn = pmax(cf, cy);
+                                    const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
+                                    const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
+                                    const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
+                                    uint32_t code;
+                                    if constexpr (DEF) {  // tagF is implied (see the walker): one v_bfi
+                                        code = (as_u32(Gn) & 0x00010001u) | (t4 & ~0x00010001u);
+                                    } else {  // tagF = M >= Ix  <=>  M - X1 >= 0 (both odd)
+                                        const uint32_t ge = ~as_u32(M - Xn1) >> 14;  // bit 15 / 31 -> bit 1 / 17
+                                        code = t4 | (as_u32(Gn) & 0x00010001u) | (ge & 0x00020002u);
+                                    }
+                                    if (k % 2 == 0) acc[k / 2] = code;
+                                    else acc[k / 2] = __builtin_amdgcn_perm(code, acc[k / 2], 0x06040200u);
+                                    stG[k] = as_u32(Gn);
+                                    stX[k] = as_u32(Xn1);
+                                    F1 = Fn1;
+                                    Y = Yn;
+                                    d1 = nd1;
+                                }
+                                const at_s2 F = F1;
+                                payF = as_u32(F);
+                                payY = as_u32(Y);
+                                if (j0 <= nB && AT_OK(((size_t)s * NT + tid + 1) * (2 * K) <= (size_t)buf_bytes, 1)) {
+                                    // 32-bit offset from the uniform buffer base (one VGPR, saddr store; a
+                                    // buffer is at most a few tens of MB)
+                                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tid) * (2u * K)));
+                                    if (tid == 0) AT_DIAG(2, 1);
+                                    if constexpr (K == 16) {
+                                        ((uint4*)dst)[0] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+                                        ((uint4*)dst)[1] = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+                                    } else if constexpr (K == 8) {
+                                        *(uint4*)dst = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+                                    } else {
+    #pragma unroll
+                                        for (int q = 0; q < KW; ++q) dst[q] = acc[q];
+                                    }
+                                }
+                                if constexpr (decltype(HO)::value)
+                                    if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
+                                if ((rw & (A2_LAST | (A2_LAST << 16))) && tid == (nB - 1) / K) {  // owner of column nB
+                                    const int out_k = (nB - 1) % K;
+                                    uint32_t eG = stG[0], eX = stX[0];
+    #pragma unroll
+                                    for (int k = 1; k < K; ++k) {
+                                        uint32_t m = (k == out_k) ? ~0u : 0u;
+                                        asm volatile("" : "+v"(m));
+                                        eG = (stG[k] & m) | (eG & ~m);
+                                        eX = (stX[k] & m) | (eX & ~m);
+                                    }
+                                    const at_s2 e = pmax(as_s2(eG), as_s2(eX));
+                                    if (rw & (A2_LAST | (A2_LAST << 16))) AT_DIAG(3, 1);
+                                    if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, 32)) fin[cur][2 * fin_n[0]++] = (int)e.x;
+                                    if ((rw & (A2_LAST << 16)) && AT_OK(2 * fin_n[1] + 1 < AT2_CHUNK, 32))
+                                        fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
+                                }
+                            }
+                            carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1
+            };
+
+            const int rmax = max(rows0, rows1);
+            const int nsteps = rmax + 63;
+            const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
+            const int nint = nblk + WAVE_LAG * (W - 1);
+            for (int it = 0; it < nint; ++it) {
+                if constexpr (IS_W) {
+                    walk_run(pb, hops, W * (it + 1));
+                } else {
+                    const int blk = it - WAVE_LAG * w;
+                    if (blk >= 0 && blk < nblk) {
+                        const int s0 = blk * INTERVAL;
+                        const int s1 = min(s0 + INTERVAL, nsteps);
+                        if (w == 0) {
+                            for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
+                        } else if (w == W - 1) {
+                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
+                        } else {
+                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, s);
+                        }
+                    }
+                }
+                const int gpre = (it + 1) * INTERVAL + tid;
+                if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, sc, dz);
+                if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
+                if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
+                __syncthreads();
+            }
+            if constexpr (IS_W) walk_run(pb, -1, 0);
+            prev_n = n;
+            cur ^= 1;
         }
-        if (walker) walk_run(pb, -1, 0);
-        prev_n = n;
-        cur ^= 1;
-    }
+    };
+    if (walker) chain_loop(std::true_type{});
+    else chain_loop(std::false_type{});
 }
 
 }  // namespace taxi2
