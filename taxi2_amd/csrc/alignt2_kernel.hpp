@@ -97,6 +97,13 @@ __host__ __device__ inline bool at_fits16(const KScores& k, int max_len) {
     return lo + 2 * O + 2 * P - NEG16 + 8 < 32767 && hi + 2 * O + 2 * P - NEG16 + 8 < 32767;
 }
 
+// Walker loads through global-address-space pointers (global_load, not flat_load: the pointers
+// come from LDS structs, so the compiler cannot infer their space).  Trace bytes bypass the
+// vector L1 (the buffer was rewritten two chains ago).
+typedef const __attribute__((address_space(1))) uint8_t a2_gbyte;
+__device__ __forceinline__ uint32_t a2_load_byte(const uint8_t* p) { return *(a2_gbyte*)p; }
+__device__ __forceinline__ uint32_t a2_load_trace(const uint8_t* p) { return *(const volatile a2_gbyte*)p; }
+
 // Row records.  One 8-byte LDS entry per step row g holds both streams: .x = two 16-bit row
 // words (stream 0 low, stream 1 high), .y = the packed column-0 boundary Ix(i, 0) = eo + ee (i-1)
 // of both rows (what wave 0's lane 0 receives from the left).  Row word bits: 0-7 the row byte,
@@ -215,7 +222,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
         for (int h = 0; budget < 0 || h < budget; ++h) {
             if (!__any(st != AT_DONE)) break;
-            if (target > 0 && *(volatile int*)&s_fill >= target) break;
+            if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
             if (st == AT_DONE) continue;
             int ni, nj;
             if (st == AT_M) {
@@ -260,10 +267,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 const int k = nj - 1 - t * K;
                 const int s = r0 + ni - 1 + (t & 63);
                 const size_t off = ((size_t)s * NT + t) * (2 * K) + 2 * k + sm;
-                if (AT_OK(off < (size_t)buf_bytes, 2)) nb = *(const volatile uint8_t*)(tr - sm + off);
+                if (AT_OK(off < (size_t)buf_bytes, 2)) nb = a2_load_trace(tr - sm + off);
             }
-            xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, 4)) ? rs[ni - 1] : 0u;
-            yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, 8)) ? cs[nj - 1] : 0u;
+            xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, 4)) ? a2_load_byte(rs + ni - 1) : 0u;
+            yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, 8)) ? a2_load_byte(cs + nj - 1) : 0u;
             // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa, digits sa in [-2, 1],
             // sb, sc in [-1, 1] (balanced base 4: u = code + 22 has digits sa + 2, sb + 1, sc + 1)
             const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 22;
