@@ -43,9 +43,9 @@ INT_VALU_PEAK = 256 * 64 * 2.4e9
 # VALU lane-ops per USEFUL cell of the bench workload, measured: SQ_INSTS_VALU x 64 / (pairs x
 # 1000 x 1000) over one launch of the packed k_alignt2<8,2> (two pairs per lane in 16-bit halves:
 # one instruction serves two cells; fill + walker, column padding 1024/1000 and the systolic skew
-# included; profiles/r1/pmc_valu_alignt2.csv).  The kernel issues 0.226 VALU instructions per
-# SIMD-clock, 90 % of the one-per-4-clocks wave64 issue ceiling.
-OPS_PER_CELL = 15.8
+# included; profiles/r1/pmc_valu_alignt2.csv).  The kernel issues 0.228 VALU instructions per
+# SIMD-clock, 91 % of the one-per-4-clocks wave64 issue ceiling.
+OPS_PER_CELL = 15.6
 
 
 def b_pair(L: int, M: int) -> int:
