@@ -362,8 +362,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             }
                             continue;
                         }
-                        const bool swp = mb.x <= ma.x;
-                        const uint8_t* cseq = swp ? XS.bytes + XS.offs[a] : YS.bytes + YS.offs[b];
+                        const uint8_t* xa_ = XS.bytes + XS.offs[a];
+                        const uint8_t* yb_ = YS.bytes + YS.offs[b];
+                        const bool swp = at_swap(xa_, yb_, ma.x, mb.x, ccol, n);
+                        const uint8_t* cseq = swp ? xa_ : yb_;
                         const int4 rm = swp ? mb : ma;
                         const int sm = n & 1;
                         if (n > 0 && (cseq != ccol || rows[sm] + rm.x > cap_rows)) break;
@@ -373,7 +375,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             chs[cur] = AtChain{cseq, 0, cm.x, cm.y, cm.z};
                         }
                         if (!AT_OK(n < AT2_CHUNK, 256)) break;
-                        tab[cur][n] = ChainPair{swp ? YS.bytes + YS.offs[b] : XS.bytes + XS.offs[a], p, rm.x, rm.y,
+                        tab[cur][n] = ChainPair{swp ? yb_ : xa_, p, rm.x, rm.y,
                                                 rm.z, rows[sm], swp ? 1 : 0, sm};
                         rows[sm] += rm.x;
                         ++n;

@@ -80,6 +80,18 @@ struct AtWalk {  // one walk: position, state, its cell's trace byte, bytes of t
     int valid, ts, tv, gap;
 };
 
+// Orientation of a pair cut into a chain (true: columns = X[a], rows = Y[b]).  A pair that
+// contains the chain's column sequence keeps it on the columns, so the chain goes on.  A chain
+// starts with X[a] on the columns (the sequence consecutive pairs share: a triangle row, a
+// query against its references) unless Y[b] is more than 1/8 longer (then the shorter rows
+// save more steps than the chain would).  Equal lengths: X[a] always.
+__device__ __forceinline__ bool at_swap(const uint8_t* xa, const uint8_t* yb, int la, int lb, const uint8_t* ccol,
+                                        int n) {
+    if (n > 0 && xa == ccol) return true;
+    if (n > 0 && yb == ccol) return false;
+    return 8 * lb <= 9 * la;
+}
+
 template <int K, int W, bool DEF, int OCC>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
@@ -280,8 +292,10 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
                         }
                         continue;
                     }
-                    const bool swp = mb.x <= ma.x;  // rows = b, columns = a
-                    const uint8_t* cseq = swp ? XS.bytes + XS.offs[a] : YS.bytes + YS.offs[b];
+                    const uint8_t* xa_ = XS.bytes + XS.offs[a];
+                    const uint8_t* yb_ = YS.bytes + YS.offs[b];
+                    const bool swp = at_swap(xa_, yb_, ma.x, mb.x, ccol, n);  // rows = b, columns = a
+                    const uint8_t* cseq = swp ? xa_ : yb_;
                     const int4 rm = swp ? mb : ma;
                     if (n > 0 && (cseq != ccol || rows + rm.x > cap_rows)) break;
                     if (n == 0) {
