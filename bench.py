@@ -37,17 +37,15 @@ N_SEQS = 50_000
 SEQ_LEN = 1000
 SEED = 0x7A12
 HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz -- one wave64 int32 VALU instruction per 4 clk per
-# SIMD, measured with tools/valu_peak.hip (DESIGN.md "Compute ceiling")
-INT_VALU_PEAK = 256 * 64 * 2.4e9
-# VALU lane-ops per USEFUL cell of the bench workload, measured: SQ_INSTS_VALU x 64 / (pairs x
-# 1000 x 1000) over one launch of the packed k_alignt2<8,2> (two pairs per lane in 16-bit halves:
-# one instruction serves two cells; fill + walker, column padding 1024/1000 and the systolic skew
-# included; profiles/r1/pmc_valu_alignt2.csv).  The kernel issues 0.228 VALU instructions per
-# SIMD-clock, 91 % of the one-per-4-clocks wave64 issue ceiling.
-OPS_PER_CELL = 15.6
-
-
+N_SIMDS = 256 * 4                   # 256 CUs x 4 SIMDs
+# The aligner's compute roofline is the VALU issue rate of ITS instruction mix, not a nominal
+# lane-op peak: tools/valu_peak (profiles/r2/valu_peak.txt) measures 2.28 SIMD-cycles per wave64
+# instruction for 32-bit add / logic / mov and the VOP2 16-bit ops, but 4.09 for every v_pk_* op,
+# max / min / shifts and every 3-source VOP3 (v_perm, v_bfi, v_med3, ...), which is most of the
+# fill.  tools/issue_ceiling.py weights the measured costs by the kernel's step-loop instruction
+# histogram (gfx950 ISA) and combines them with the rocprofv3 PMC pass of the same build
+# (SQ_INSTS_VALU, GRBM_GUI_ACTIVE) into this file; the bench reads it for the roofline.
+COMPUTE_CEILING_JSON = ROOT / "profiles" / "compute_ceiling.json"
 def b_pair(L: int, M: int) -> int:
     """SURVEY.md §8(d) canonical algorithmic bytes per unordered pair: 2 * ceil(L/4) + 8 * M."""
     return 2 * math.ceil(L / 4) + 8 * M
@@ -59,8 +57,10 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 19, help="unordered pairs per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=16384,
-                    help="pairs timed on the host oracle (~12 s on 16 host threads)")
+    ap.add_argument("--cpu-sample", type=int, default=8192,
+                    help="pairs timed on the host oracle on all host threads (~6 s on 16 threads)")
+    ap.add_argument("--cpu-sample-1t", type=int, default=512,
+                    help="pairs timed on ONE host thread, the reference's serial loop shape (~6 s)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores (max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
@@ -151,6 +151,7 @@ def main() -> None:
             traffic = None
     cells = float(SEQ_LEN) * SEQ_LEN
     gcups = B * cells / (kern_ms * 1e-3) / 1e9
+    compute = compute_roofline(gcups)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -168,7 +169,9 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32",
+            # the fill computes in packed int16 halves (two DP cells per 32-bit register), admitted
+            # only when every DP difference fits int16 (at_fits16): exact, not reduced precision
+            "dtype": "int16x2 (packed, range-checked exact)",
             "data": "synthetic",
             "config": {
                 "workload": "config3: versusAll 50 000 x 1 000 bp synthetic, Gotoh align (default "
@@ -189,14 +192,7 @@ def main() -> None:
                 "bytes_per_pair": bp,
                 "kernel_ms": kern_ms,
             },
-            "compute_roofline": {
-                "bound": "valu-int32",
-                "gcups": gcups,
-                "ops_per_cell": OPS_PER_CELL,
-                "achieved_tops": gcups * 1e9 * OPS_PER_CELL / 1e12,
-                "peak_tops": INT_VALU_PEAK / 1e12,
-                "frac": gcups * 1e9 * OPS_PER_CELL / INT_VALU_PEAK,
-            },
+            "compute_roofline": compute,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -204,19 +200,50 @@ def main() -> None:
         dist.destroy_process_group()
 
 
+def compute_roofline(gcups: float) -> dict | None:
+    """VALU issue roofline of the timed kernel (see COMPUTE_CEILING_JSON): the ceiling is the
+    issue rate of the kernel's measured instruction mix; achieved = the live GCUPS x the PMC
+    instructions per cell, per SIMD-cycle at the PMC pass's clock."""
+    if not COMPUTE_CEILING_JSON.exists():
+        return None
+    c = json.loads(COMPUTE_CEILING_JSON.read_text())
+    if c.get("workload") != "config3":
+        return None
+    instr_per_cell = c["valu_instr_per_cell"]          # SQ_INSTS_VALU / useful cells (PMC)
+    clock = c["clock_ghz"] * 1e9                          # GRBM_GUI_ACTIVE / 8 / kernel time (PMC)
+    achieved = gcups * 1e9 * instr_per_cell / (N_SIMDS * clock)  # wave-instructions per SIMD-cycle
+    peak = c["ceiling_instr_per_simd_clk"]
+    return {
+        "bound": "valu-issue",
+        "unit": "wave64 VALU instructions per SIMD-cycle",
+        "achieved": achieved,
+        "peak": peak,
+        "frac": achieved / peak,
+        "gcups": gcups,
+        "ops_per_cell": instr_per_cell * 64,
+        "source": c["source"],
+    }
+
+
 def cpu_baseline(args, buf, offs, eng, seqset):
-    """Oracle (C restatement, kind "port") on the first `--cpu-sample` pairs of the bench's pair
-    space, on the host cores; the same pairs' GPU results are checked against it."""
+    """Oracle (C restatement, kind "port") on the first pairs of the bench's pair space, on all
+    host cores and on ONE core (the reference's serial per-pair loop, versus_all.py:746-769); the
+    same pairs' GPU results are checked against it."""
     from oracle import oracle_c
     from taxi2_amd._native import tri_pairs
 
+    def timed(S: int, threads: int):
+        a, b = tri_pairs(N_SEQS, 0, S)
+        t0 = time.perf_counter()
+        exp, _ = oracle_c.batch((buf, offs), a, b, align=True, scores=(1, -1, -8, -1, -1, -1),
+                                metrics=METRICS, threads=threads)
+        return exp, time.perf_counter() - t0
+
     S = int(args.cpu_sample)
     threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
-    a, b = tri_pairs(N_SEQS, 0, S)
-    t0 = time.perf_counter()
-    exp, _ = oracle_c.batch((buf, offs), a, b, align=True, scores=(1, -1, -8, -1, -1, -1),
-                            metrics=METRICS, threads=threads)
-    dt = time.perf_counter() - t0
+    exp, dt = timed(S, threads)
+    S1 = int(args.cpu_sample_1t)
+    _, dt1 = timed(S1, 1)
     got = eng.all_pairs(seqset, 0, S, METRICS)
     fin = np.isfinite(exp)
     same = bool(np.array_equal(np.isfinite(got), fin)
@@ -229,6 +256,13 @@ def cpu_baseline(args, buf, offs, eng, seqset):
         "sample": f"first {S} pairs of the config3 pair space (row 0), C restatement "
                   f"(oracle/taxi2_oracle.c, gcc -O2) on {threads} host threads; GPU==CPU on the "
                   f"sample: {same}",
+        "single_thread": {
+            "value": S1 / dt1,
+            "unit": "pairs/s",
+            "cores": 1,
+            "sample": f"first {S1} pairs of the same pair space on one host thread (the reference's "
+                      f"serial loop shape, versus_all.py:746-769)",
+        },
     }
 
 

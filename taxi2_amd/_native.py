@@ -19,7 +19,9 @@ from typing import Iterable, NamedTuple, Sequence as Seq
 import numpy as np
 
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
-LIB_PATH = LIB_DIR / "libtaxi2_mi355x.so"
+# TAXI2_LIB selects another in-tree build of the same ABI (the debug builds of
+# taxi2_amd/csrc/Makefile: `make guard`, `make chunk16`), by file name inside _lib/.
+LIB_PATH = LIB_DIR / os.path.basename(os.environ.get("TAXI2_LIB", "libtaxi2_mi355x.so"))
 HEADER_PATH = Path(__file__).resolve().parent.parent / "include" / "taxi2_mi355x.h"
 
 # Every symbol include/taxi2_mi355x.h declares.

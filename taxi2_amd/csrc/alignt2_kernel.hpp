@@ -37,7 +37,13 @@ typedef short at_s2 __attribute__((ext_vector_type(2)));
 
 // Debug build only (-DTAXI2_GUARD, `make guard`): every global access and risky LDS index of
 // k_alignt2 is range-checked; a violation is recorded in at_guard_err (a code per site) and the
-// access skipped, so an out-of-bounds bug is located without faulting the GPU.
+// access skipped, so an out-of-bounds bug is located without faulting the GPU.  The guard build
+// also POISONS what a launch must never read before writing it, so a read of stale state shows up
+// on the first launch of a process instead of depending on what earlier kernels left behind:
+// every LDS array at kernel start and the row ring / wave ring at every chain start (0xA5 bytes;
+// a row record, ring entry or walk state still holding the pattern when read sets a code), and
+// the chain's trace buffer before its fill (0x7F bytes: outside the valid trace-byte range
+// [-88, 87], so the walker flags any byte the fill of ITS chain did not store).
 #ifdef TAXI2_GUARD
 __device__ unsigned int at_guard_err;
 #define AT_OK(cond, code) ((cond) ? true : (atomicOr(&at_guard_err, (unsigned)(code)), false))
@@ -49,6 +55,17 @@ __device__ unsigned int at_diag[8];
 #define AT_OK(cond, code) true
 #define AT_DIAG(k, v) ((void)0)
 #endif
+constexpr uint32_t AT_POISON_LDS = 0xA5A5A5A5u;
+// guard codes (bit per site)
+enum : unsigned {
+    AG_STORE = 1, AG_LOAD = 2, AG_ROWSEQ = 4, AG_COLSEQ = 8, AG_ROWBYTE = 16, AG_FIN = 32, AG_PI = 64, AG_OUT = 128,
+    AG_CHUNK = 256, AG_TRACE_POISON = 512, AG_ROW_POISON = 1024, AG_RING_POISON = 2048, AG_WALK_POISON = 4096,
+};
+// fill `bytes` bytes of LDS at p with the poison pattern (all threads of the workgroup)
+__device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
+    uint32_t* w = (uint32_t*)p;
+    for (size_t k = threadIdx.x; k < bytes / 4; k += blockDim.x) w[k] = AT_POISON_LDS;
+}
 
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
@@ -121,7 +138,7 @@ __device__ __forceinline__ uint32_t a2_row_word(const ChainPair* __restrict__ ta
         if (tab[t].r0 <= g) k = t;
     const ChainPair& cp = tab[k];
     const int i = g - cp.r0;
-    const uint32_t c = AT_OK(i >= 0 && i < cp.nA, 16) ? cp.rseq[i] : 'A';
+    const uint32_t c = AT_OK(i >= 0 && i < cp.nA, AG_ROWBYTE) ? cp.rseq[i] : 'A';
     const uint32_t ec = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
     uint32_t v = c | (ec < 4u ? ec << 11 : A2_OTHER);
     if (i == 0) v |= A2_FIRST;
@@ -167,6 +184,20 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     __shared__ int s_fill;  // fill waves done with the current interval (cumulative per chain)
     __shared__ AtWalk wks[2 * AT2_CHUNK];
 
+#ifdef TAXI2_GUARD
+    at_poison_lds(xinfo, sizeof xinfo);
+    at_poison_lds(tab, sizeof tab);
+    at_poison_lds(fin, sizeof fin);
+    at_poison_lds(fin_n, sizeof fin_n);
+    at_poison_lds(chs, sizeof chs);
+    at_poison_lds(ring, sizeof ring);
+    at_poison_lds(colc, sizeof colc);
+    at_poison_lds(colx, sizeof colx);
+    at_poison_lds(eqt, sizeof eqt);
+    at_poison_lds(wks, sizeof wks);
+    if (threadIdx.x == 0) s_n = s_rows[0] = s_rows[1] = s_fill = (int)AT_POISON_LDS;
+    __syncthreads();
+#endif
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring pointers etc. in SGPRs
@@ -187,8 +218,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     auto walk_init = [&](int pb, int n) {
         const int nw = out_mode == OUT_BOTH ? 2 * n : n;
         if (lane >= 2 * AT2_CHUNK) return;
+        // every field of every walk slot is written, idle slots included (an idle slot's pi
+        // indexes tab[] in walk_run; it must not be whatever an earlier kernel left in LDS)
         AtWalk& W_ = wks[lane];
-        W_.st = AT_DONE;
+        W_ = AtWalk{0, 0, AT_DONE, 0, 0, 0, 0u, 0u, 0u, 0, 0, 0, 0};
         if (lane < nw) {
             const int pi = lane < n ? lane : lane - n;
             const ChainPair& cp = tab[pb][pi];
@@ -198,8 +231,6 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             W_.j = chs[pb].nB + 1;
             W_.st = AT_M;
             W_.first = 1;
-            W_.valid = W_.ts = W_.tv = W_.gap = 0;
-            W_.cb = W_.xa = W_.yb = 0u;
         }
     };
     // hop until `budget` hops (< 0: unbounded) or, with target > 0, until the fill waves have
@@ -208,9 +239,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     auto walk_run = [&](int pb, int budget, int target) {
         AtWalk& W_ = wks[lane < 2 * AT2_CHUNK ? lane : 0];
         int st = lane < 2 * AT2_CHUNK ? W_.st : AT_DONE;
+        if (!AT_OK(st != (int)AT_POISON_LDS && W_.pi != (int)AT_POISON_LDS, AG_WALK_POISON)) st = AT_DONE;
         if (!__any(st != AT_DONE)) return;
         const int pi = W_.pi;
-        const ChainPair& cp = tab[pb][AT_OK(st == AT_DONE || (pi >= 0 && pi < chs[pb].n), 64) ? pi : 0];
+        const ChainPair& cp = tab[pb][AT_OK(st == AT_DONE || (pi >= 0 && pi < chs[pb].n), AG_PI) ? pi : 0];
         const AtChain& ch = chs[pb];
         const int fx = cp.fx, lx = cp.lx, fy = ch.fy, ly = ch.ly, r0 = cp.r0, sm = cp.pad;
         const int prio = W_.prio;
@@ -253,10 +285,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 if (out_mode == OUT_BOTH) o = out + (p * 2 + ((prio ^ cp.swp) ? 1 : 0)) * nm;
                 else o = out + p * nm;
                 AT_DIAG(4, 1);
-                if (AT_OK(p >= 0 && p < total, 128))
+                if (AT_OK(p >= 0 && p < total, AG_OUT))
                 for (int m = 0; m < nm; ++m)
                     o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
-                if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK, 32))  // undo the drift of cell (nA, nB)
+                if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK && fin[pb][pi] != (int)AT_POISON_LDS, AG_FIN))  // undo the drift of cell (nA, nB)
                     sout[p] = (fin[pb][pi] + (cp.nA + chs[pb].nB) * dz) >> 1;
                 st = AT_DONE;
                 continue;
@@ -267,10 +299,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 const int k = nj - 1 - t * K;
                 const int s = r0 + ni - 1 + (t & 63);
                 const size_t off = ((size_t)s * NT + t) * (2 * K) + 2 * k + sm;
-                if (AT_OK(off < (size_t)buf_bytes, 2)) nb = a2_load_trace(tr - sm + off);
+                if (AT_OK(off < (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace(tr - sm + off);
+                // guard build: the fill of this chain stored every byte the walk reads
+                (void)AT_OK((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87, AG_TRACE_POISON);
             }
-            xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, 4)) ? a2_load_byte(rs + ni - 1) : 0u;
-            yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, 8)) ? a2_load_byte(cs + nj - 1) : 0u;
+            xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, AG_ROWSEQ)) ? a2_load_byte(rs + ni - 1) : 0u;
+            yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, AG_COLSEQ)) ? a2_load_byte(cs + nj - 1) : 0u;
             // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa, digits sa in [-2, 1],
             // sb, sc in [-1, 1] (balanced base 4: u = code + 22 has digits sa + 2, sb + 1, sc + 1)
             const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 22;
@@ -374,7 +408,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             ccol = cseq;
                             chs[cur] = AtChain{cseq, 0, cm.x, cm.y, cm.z};
                         }
-                        if (!AT_OK(n < AT2_CHUNK, 256)) break;
+                        if (!AT_OK(n < AT2_CHUNK, AG_CHUNK)) break;
                         tab[cur][n] = ChainPair{swp ? yb_ : xa_, p, rm.x, rm.y,
                                                 rm.z, rows[sm], swp ? 1 : 0, sm};
                         rows[sm] += rm.x;
@@ -405,6 +439,20 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 break;
             }
             const int nB = chs[cur].nB;
+#ifdef TAXI2_GUARD
+            {  // poison the row ring, the wave ring and this chain's trace buffer (see AT_OK)
+                at_poison_lds(xinfo, sizeof xinfo);
+                at_poison_lds(ring, sizeof ring);
+                if constexpr (!IS_W) {
+                    uint4* tb = (uint4*)(bufs + (size_t)cur * (size_t)buf_bytes);
+                    const size_t nv = ((size_t)(max(rows0, rows1) + 63) * NT * (2 * K) + 15) / 16;
+                    const uint4 pz = make_uint4(0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu);
+                    for (size_t v = tid; v < nv && AT_OK(v * 16 + 16 <= (size_t)buf_bytes, AG_STORE); v += NT) tb[v] = pz;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+#endif
 
             // ---- fill-lane column constants (once per chain)
             const int j0 = (w * 64 + lane) * K + 1;
@@ -462,12 +510,15 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             const int g = s - ln;
                             const uint2 rec = xinfo[g & (XR - 1)];
                             const uint32_t rw = rec.x;
+                            (void)AT_OK(rw != AT_POISON_LDS, AG_ROW_POISON);
                             uint32_t inF, inY;
                             if constexpr (decltype(FW)::value) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
                                 inF = shr_old(payF, rec.y);
                                 inY = shr_old(payY, NEG16X2);
                             } else {
                                 const uint2 o = ring_in[(s + 1) & (RING - 1)];
+                                // lane 0 reads row s; rows past the chain's last are never read back
+                                (void)AT_OK(s >= max(rows0, rows1) || o.x != AT_POISON_LDS, AG_RING_POISON);
                                 inF = shr_old(payF, o.x);
                                 inY = shr_old(payY, o.y);
                             }
@@ -575,7 +626,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 const at_s2 F = F1;
                                 payF = as_u32(F);
                                 payY = as_u32(Y);
-                                if (j0 <= nB && AT_OK(((size_t)s * NT + tid + 1) * (2 * K) <= (size_t)buf_bytes, 1)) {
+                                if (j0 <= nB && AT_OK(((size_t)s * NT + tid + 1) * (2 * K) <= (size_t)buf_bytes, AG_STORE)) {
                                     // 32-bit offset from the uniform buffer base (one VGPR, saddr store; a
                                     // buffer is at most a few tens of MB)
                                     uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tid) * (2u * K)));
@@ -604,8 +655,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     }
                                     const at_s2 e = pmax(as_s2(eG), as_s2(eX));
                                     if (rw & (A2_LAST | (A2_LAST << 16))) AT_DIAG(3, 1);
-                                    if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, 32)) fin[cur][2 * fin_n[0]++] = (int)e.x;
-                                    if ((rw & (A2_LAST << 16)) && AT_OK(2 * fin_n[1] + 1 < AT2_CHUNK, 32))
+                                    if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, AG_FIN)) fin[cur][2 * fin_n[0]++] = (int)e.x;
+                                    if ((rw & (A2_LAST << 16)) && AT_OK(2 * fin_n[1] + 1 < AT2_CHUNK, AG_FIN))
                                         fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
                                 }
                             }

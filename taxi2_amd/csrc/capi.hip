@@ -66,6 +66,11 @@ struct taxi2_ctx {
     void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
     void* d_zslabs = nullptr;
     int64_t z_threads = 0;
+    // The aligners' shared buffers (d_trace, d_work) are used on ctx->stream by the host-buffer
+    // entry points and on the CALLER's stream by the *_dev ones: the last stream that used them
+    // and an event recorded after that use order the next launch on another stream behind it.
+    hipStream_t shared_st = nullptr;
+    hipEvent_t shared_ev = nullptr;
 };
 
 namespace {
@@ -88,12 +93,28 @@ int fail(taxi2_ctx* ctx, const char* fmt, ...) {
 
 int ensure(taxi2_ctx* ctx, void** p, size_t* cap, size_t need) {
     if (*cap >= need) return 0;
+    // regrowth: nothing enqueued on any stream (a *_dev caller's included) may still use the old
+    // buffer when it is released
+    if (*p) HIP_TRY(ctx, hipDeviceSynchronize());
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
     size_t want = std::max(need, (size_t)1 << 20);
     HIP_TRY(ctx, hipMalloc(p, want));
     *cap = want;
+    return 0;
+}
+
+// Before a launch on `st` that uses d_trace / d_work: wait for their last use on another stream.
+int shared_acquire(taxi2_ctx* ctx, hipStream_t st) {
+    if (ctx->shared_st && ctx->shared_st != st) HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->shared_ev, 0));
+    return 0;
+}
+// After it: remember the stream and mark the point the next user on another stream waits for.
+int shared_release(taxi2_ctx* ctx, hipStream_t st) {
+    if (!ctx->shared_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->shared_ev, hipEventDisableTiming));
+    HIP_TRY(ctx, hipEventRecord(ctx->shared_ev, st));
+    ctx->shared_st = st;
     return 0;
 }
 
@@ -308,6 +329,7 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
     if (lds > 64 * 1024)
         for (int k = 0; k < 2; ++k)
             HIP_TRY(ctx, hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (shared_acquire(ctx, st)) return -1;
     // d_work: [u32 worklist count, pad] [u64 pass-1 cursor] [u64 pass-2 cursor] [u32 worklist...]
     if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32 + (size_t)ps.count * 4)) return -1;
     uint32_t* wcount = (uint32_t*)ctx->d_work;
@@ -331,6 +353,7 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
     launch[1](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, arg, out_mode, d_out,
               nullptr, wlist, wcount, next + 1);
     HIP_TRY(ctx, hipGetLastError());
+    if (shared_release(ctx, st)) return -1;
     if (getenv("TAXI2_A1_STATS")) {  // diagnostics: share of pairs re-run in orientation B
         uint32_t n2 = 0;
         HIP_TRY(ctx, hipMemcpyAsync(&n2, wcount, 4, hipMemcpyDeviceToHost, st));
@@ -423,6 +446,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
         return at_buf_bytes((int)per_stream * std::max(1, max_len), packed ? 2 * v.K : v.K, v.W);
     };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
+    if (shared_acquire(ctx, st)) return -1;
     chunk = (int)eff;  // the kernel must cut chains with the same bound the buffers were sized for
     const int cap_rows = (int)(packed ? (eff + 1) / 2 : eff) * std::max(1, max_len);
     const size_t bb = buf_bytes(eff);
@@ -435,6 +459,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), ps, k, ms, chunk, out_mode, d_out,
              d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next);
     HIP_TRY(ctx, hipGetLastError());
+    if (shared_release(ctx, st)) return -1;
 #ifdef TAXI2_GUARD
     if (packed) {  // debug build: report (and clear) out-of-range accesses the guards skipped
         unsigned int e = 0;
@@ -451,6 +476,8 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
                     "count %lld)\n", v.K, v.W, (int)v.def, e, (long long)grid, chunk, cap_rows, bb, (long long)ps.count);
             const unsigned int z = 0;
             HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(at_guard_err), &z, sizeof z));
+            return fail(ctx, "guard build: k_alignt2<%d,%d,%d> guard codes 0x%x (see alignt2_kernel.hpp AG_*)", v.K,
+                        v.W, (int)v.def, e);
         }
     }
 #endif
@@ -749,6 +776,7 @@ int taxi2_ctx_create(int device, taxi2_ctx** out) {
 void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();  // *_dev work on caller streams may still use the buffers
     for (int i = 0; i < (int)ctx->sets.size(); ++i) taxi2_set_destroy(ctx, i);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
@@ -757,6 +785,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
     if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
     if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
+    if (ctx->shared_ev) (void)hipEventDestroy(ctx->shared_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

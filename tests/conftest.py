@@ -26,7 +26,13 @@ def oracle_c():
 
 @pytest.fixture(scope="session")
 def engine():
-    """One engine context on cuda:0 for the whole GPU session."""
+    """One engine context on cuda:0 for the whole GPU session.  torch (when present) is imported
+    first so that the engine and torch share one HIP runtime (taxi2_amd._native.Engine) and torch
+    stream / tensor pointers can be handed to the *_dev entry points."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     from taxi2_amd._native import Engine
 
     return Engine.default(0)
