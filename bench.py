@@ -51,6 +51,30 @@ def b_pair(L: int, M: int) -> int:
     return 2 * math.ceil(L / 4) + 8 * M
 
 
+def step_block(step: int, rank: int, world: int, batch: int, total_pairs: int) -> int:
+    """First pair of the block rank `rank` runs at `step`: consecutive steps and ranks take
+    consecutive, disjoint blocks of the config-3 pair space (weak scaling: `batch` pairs per rank
+    and step), wrapping before the end of the space."""
+    return ((step * world + rank) * batch) % (total_pairs - batch)
+
+
+def max_over_ranks(elapsed: float, world: int, device=None) -> float:
+    """The slowest rank's wall time (all-reduce MAX; RCCL on GPUs, gloo in tests)."""
+    if world <= 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_value(steps: int, batch: int, world: int, elapsed: float) -> float:
+    """Whole-job throughput: the pairs every rank processed / the slowest rank's time."""
+    return steps * batch * world / elapsed
+
+
 def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,7 +123,7 @@ def main() -> None:
     torch.cuda.set_stream(stream)
 
     def block(step: int) -> int:
-        return ((step * world + rank) * B) % (total_pairs - B)
+        return step_block(step, rank, world, B, total_pairs)
 
     ev = []
 
@@ -129,15 +153,10 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, "cuda")
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
-    pairs = args.steps * B * world
-    value = pairs / elapsed
+    value = job_value(args.steps, B, world, elapsed)
     bp = b_pair(SEQ_LEN, M)
     achieved_gbs = B * bp / (kern_ms * 1e-3) / 1e9
     traffic = None

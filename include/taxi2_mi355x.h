@@ -51,12 +51,18 @@ typedef struct {
     int32_t end_extend_gap_score;
 } taxi2_scores;
 
-/* distances.py:319-348 metric labels p, p-gaps, jc, k2p. */
+/* distances.py:319-348 metric labels p, p-gaps, jc, k2p.
+ * TAXI2_METRIC_COUNTS is not a metric: accepted ALONE by the pair entry points (all_pairs[_dev],
+ * rect_pairs, list_pairs) for sequences of at most 32 767 bp, it writes the four column counters of
+ * every ordered pair packed into its 8-byte output slot (uint64: valid | ts << 16 | tv << 32 |
+ * gap << 48) -- a quarter of the bytes of four f64 metrics, and every metric is a function of them
+ * (taxi2_counts_metrics_dev).  Used by the streamed versusAll (taxi2_amd/streaming.py). */
 enum {
     TAXI2_METRIC_P = 0,
     TAXI2_METRIC_P_GAPS = 1,
     TAXI2_METRIC_JC = 2,
-    TAXI2_METRIC_K2P = 3
+    TAXI2_METRIC_K2P = 3,
+    TAXI2_METRIC_COUNTS = 16
 };
 
 /* Sequence set modes.
@@ -101,6 +107,13 @@ int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const ta
 int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count,
                         const taxi2_scores* sc, const int32_t* metrics, int nmetrics,
                         double* d_out, int32_t* d_scores, void* stream);
+
+/* Metrics from TAXI2_METRIC_COUNTS slots (device buffers, asynchronous on `stream` or the context's
+ * own): d_out[k][m] = scale * metric m of d_counts[k] for k < n (metrics 0..3; scale 100 is
+ * versus_all.py:554-562's percentage adjustment, 1 leaves the values alone).  Bit-identical to the
+ * same metrics written directly by the pair entry points. */
+int taxi2_counts_metrics_dev(taxi2_ctx* ctx, const uint64_t* d_counts, int64_t n, const int32_t* metrics,
+                             int nmetrics, double scale, double* d_out, void* stream);
 
 /* ---- rectangle (versus_reference.py:225-229, decontaminate.py:336-371 shape) ---------- *
  * Pairs (q, r) for q in [q0, q1) of set_q and every r of set_r, row-major:
@@ -214,6 +227,17 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
  * x subset, so each key's summation order is the reference's. */
 int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* code, int32_t ns, double* sum,
                            double* mn, double* mx, int64_t* count, int threads);
+
+/* Same aggregation on the device, one row block at a time (the streamed versusAll,
+ * taxi2_amd/streaming.py): d_vals[nrows][ncols][m] = the block's adjusted values, d_row_code[nrows]
+ * the block rows' subset codes, the columns grouped by subset as a CSR (d_col_start[ns + 1],
+ * d_col_idx[ncols]: each subset's columns in ascending order).  The state arrays [ns][ns][m] are
+ * initialised first when init != 0, else accumulated into; blocks fed in ascending row order give
+ * exactly taxi2_subset_aggregate's (= the reference's x-major) sums.  Asynchronous on `stream`. */
+int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,
+                               const int32_t* d_row_code, const int64_t* d_col_start, const int32_t* d_col_idx,
+                               int32_t ns, int init, double* d_sum, double* d_min, double* d_max, int64_t* d_count,
+                               void* stream);
 
 /* ---- Dereplicate's greedy walk (dereplicate.py:180-196 drop_*_pairs, 289-337 find_replicates,
  * 393-425 the lazily pulled chain that interleaves them) ------------------------------------ *

@@ -36,6 +36,7 @@ EXPORTS = (
     "taxi2_set_info",
     "taxi2_all_pairs",
     "taxi2_all_pairs_dev",
+    "taxi2_counts_metrics_dev",
     "taxi2_rect_pairs",
     "taxi2_list_pairs",
     "taxi2_closest",
@@ -46,6 +47,7 @@ EXPORTS = (
     "taxi2_format_ragged",
     "taxi2_format_summary",
     "taxi2_subset_aggregate",
+    "taxi2_subset_aggregate_dev",
     "taxi2_dereplicate_walk",
 )
 
@@ -53,6 +55,10 @@ MODE_PREALIGNED = 0
 MODE_ALIGN = 1
 
 METRIC_CODES = {"p": 0, "p-gaps": 1, "jc": 2, "k2p": 3}
+# Pseudo-metric: the packed column counters of each ordered pair (uint64 in the f64 slot:
+# valid | ts << 16 | tv << 32 | gap << 48); must be the only metric of a call (taxi2_mi355x.h).
+COUNTS = "counts"
+COUNTS_CODE = 16
 MAX_METRICS = 8
 
 
@@ -87,6 +93,7 @@ _SIGNATURES = {
     "taxi2_set_info": (_INT, [_P, _INT, ctypes.POINTER(_I64), ctypes.POINTER(_I32), ctypes.POINTER(_INT)]),
     "taxi2_all_pairs": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_all_pairs_dev": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
+    "taxi2_counts_metrics_dev": (_INT, [_P, _P, _I64, _P, _INT, ctypes.c_double, _P, _P]),
     "taxi2_rect_pairs": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
@@ -101,6 +108,7 @@ _SIGNATURES = {
     "taxi2_format_summary": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _INT, _INT,
                                     _P, _P, _INT, _P, _I32, _P, _I64, ctypes.POINTER(_I64)]),
     "taxi2_subset_aggregate": (_INT, [_P, _I64, _INT, _P, _I32, _P, _P, _P, _P, _INT]),
+    "taxi2_subset_aggregate_dev": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _I32, _INT, _P, _P, _P, _P, _P]),
     "taxi2_dereplicate_walk": (_INT, [_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, ctypes.POINTER(_I64), _P,
                                       _P, _I64, ctypes.POINTER(_I64), _P]),
 }
@@ -122,6 +130,8 @@ def load_library() -> ctypes.CDLL:
             )
         lib = ctypes.CDLL(str(LIB_PATH))
         for name in EXPORTS:
+            if "TAXI2_LIB" in os.environ and not hasattr(lib, name):
+                continue  # a debug build of an older tree (tools/fault_*.sh): its own ABI subset
             fn = getattr(lib, name)  # AttributeError = missing export
             res, args = _SIGNATURES[name]
             fn.restype = res
@@ -168,6 +178,9 @@ def metric_codes(metrics: Iterable) -> np.ndarray:
     codes = []
     for m in metrics:
         label = m if isinstance(m, str) else str(m)
+        if label == COUNTS:
+            codes.append(COUNTS_CODE)
+            continue
         if label not in METRIC_CODES:
             raise NativeError(f"metric {label!r} is not computed by the MI355X engine")
         codes.append(METRIC_CODES[label])
@@ -324,6 +337,37 @@ class Engine:
                     ctypes.c_void_p(stream) if stream else None,
                 ),
                 "taxi2_all_pairs_dev",
+            )
+
+    def counts_metrics_dev(self, counts_ptr: int, n: int, metrics, out_ptr: int, scale: float = 1.0,
+                           stream: int | None = None) -> None:
+        """out[k][m] = scale * metric m of the packed counters counts[k] (device pointers;
+        asynchronous on ``stream``): the metrics of a TAXI2_METRIC_COUNTS launch."""
+        codes = metric_codes(metrics)
+        if COUNTS_CODE in codes:
+            raise NativeError("counts_metrics_dev evaluates real metrics only")
+        with self._lock:
+            self._check(
+                self._lib.taxi2_counts_metrics_dev(
+                    self._ctx, ctypes.c_void_p(counts_ptr), int(n), codes.ctypes.data, len(codes), float(scale),
+                    ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_counts_metrics_dev",
+            )
+
+    def subset_aggregate_dev(self, vals_ptr: int, nrows: int, ncols: int, m: int, row_code_ptr: int,
+                             col_start_ptr: int, col_idx_ptr: int, ns: int, init: bool, sum_ptr: int, min_ptr: int,
+                             max_ptr: int, count_ptr: int, stream: int | None = None) -> None:
+        """taxi2_subset_aggregate_dev on device buffers (see taxi2_amd/streaming.py)."""
+        with self._lock:
+            self._check(
+                self._lib.taxi2_subset_aggregate_dev(
+                    self._ctx, ctypes.c_void_p(vals_ptr), int(nrows), int(ncols), int(m), ctypes.c_void_p(row_code_ptr),
+                    ctypes.c_void_p(col_start_ptr), ctypes.c_void_p(col_idx_ptr), int(ns), 1 if init else 0,
+                    ctypes.c_void_p(sum_ptr), ctypes.c_void_p(min_ptr), ctypes.c_void_p(max_ptr),
+                    ctypes.c_void_p(count_ptr), ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_subset_aggregate_dev",
             )
 
     def rect_pairs(self, q: SeqSet, r: SeqSet, q0: int, q1: int, metrics, scores=None, *, with_scores=False):
@@ -559,6 +603,12 @@ class Engine:
                             oy[k, o, end - L:end].tobytes().decode("latin-1")))
             out.append(tuple(res) if both else res[0])
         return out
+
+
+def unpack_counts(c: np.ndarray) -> np.ndarray:
+    """TAXI2_METRIC_COUNTS slots (f64 or uint64 array) -> (..., 4) int64 (valid, ts, tv, gap)."""
+    u = np.ascontiguousarray(c).view(np.uint64)
+    return np.stack([(u >> np.uint64(s)) & np.uint64(0xFFFF) for s in (0, 16, 32, 48)], axis=-1).astype(np.int64)
 
 
 def tri_index(a: np.ndarray, b: np.ndarray, n: int) -> np.ndarray:

@@ -401,8 +401,8 @@ k_align(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int xca
         if (nA == 0 || nB == 0) {  // one side empty: no ACGT column can exist
             if (threadIdx.x == 0) {
                 for (int m = 0; m < nm; ++m) {
-                    o_ab[m] = __builtin_nan("");
-                    if (o_ba) o_ba[m] = __builtin_nan("");
+                    o_ab[m] = metric_value(ms.code[m], 0u, 0u, 0u, 0u);
+                    if (o_ba) o_ba[m] = metric_value(ms.code[m], 0u, 0u, 0u, 0u);
                 }
                 if (sout) {
                     const int n = nA + nB;

@@ -280,10 +280,10 @@ k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int ch
                         if (n > 0) break;
                         for (int m = 0; m < nm; ++m) {
                             if (out_mode == OUT_BOTH) {
-                                out[(p * 2 + 0) * nm + m] = __builtin_nan("");
-                                out[(p * 2 + 1) * nm + m] = __builtin_nan("");
+                                out[(p * 2 + 0) * nm + m] = metric_value(ms.code[m], 0u, 0u, 0u, 0u);
+                                out[(p * 2 + 1) * nm + m] = metric_value(ms.code[m], 0u, 0u, 0u, 0u);
                             } else {
-                                out[p * nm + m] = __builtin_nan("");
+                                out[p * nm + m] = metric_value(ms.code[m], 0u, 0u, 0u, 0u);
                             }
                         }
                         if (sout) {

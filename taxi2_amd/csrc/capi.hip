@@ -20,6 +20,7 @@
 #include "align_kernel.hpp"
 #include "alignt_kernel.hpp"
 #include "alignt2_kernel.hpp"
+#include "alignlong_kernel.hpp"
 #include "ncd_kernels.hpp"
 #include "format_kernels.hpp"
 #include "common.hpp"
@@ -61,6 +62,8 @@ struct taxi2_ctx {
     size_t d_work_bytes = 0;
     void* d_trace = nullptr;  // trace-and-walk aligner: two chain trace buffers per workgroup
     size_t d_trace_bytes = 0;
+    void* d_bnd = nullptr;  // column-tiled aligner: per-workgroup tile boundary columns
+    size_t d_bnd_bytes = 0;
     void* d_fmt = nullptr;  // text formatter staging
     size_t d_fmt_bytes = 0;
     void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
@@ -125,12 +128,19 @@ DevSet* get_set(taxi2_ctx* ctx, int id) {
 
 SetView view(const DevSet& s) { return SetView{s.bytes, s.offs, s.meta, s.planes, s.n}; }
 
-int check_metrics(taxi2_ctx* ctx, const int32_t* metrics, int nm, MetricSpec& ms) {
+// allow_counts: the pair entry points also accept TAXI2_METRIC_COUNTS, alone, for sequences of at
+// most 32 767 bp (every counter then fits its 16-bit field).
+int check_metrics(taxi2_ctx* ctx, const int32_t* metrics, int nm, MetricSpec& ms, bool allow_counts = false,
+                  int max_len = 0) {
     if (nm < 1 || nm > MAX_METRICS) return fail(ctx, "nmetrics must be in [1, %d]", MAX_METRICS);
     ms.n = nm;
     for (int m = 0; m < nm; ++m) {
-        if (metrics[m] < TAXI2_METRIC_P || metrics[m] > TAXI2_METRIC_K2P)
+        if (metrics[m] == TAXI2_METRIC_COUNTS && allow_counts) {
+            if (nm != 1) return fail(ctx, "TAXI2_METRIC_COUNTS must be the only metric of a call");
+            if (max_len > 32767) return fail(ctx, "TAXI2_METRIC_COUNTS needs sequences of at most 32767 bp");
+        } else if (metrics[m] < TAXI2_METRIC_P || metrics[m] > TAXI2_METRIC_K2P) {
             return fail(ctx, "unknown metric code %d", metrics[m]);
+        }
         ms.code[m] = metrics[m];
     }
     return 0;
@@ -484,12 +494,83 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     return 0;
 }
 
+// ---------------------------------------------------------------- column-tiled (any length)
+struct VariantL {
+    int K, W, occ;
+    const void* fn;
+    void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int, double*, int32_t*,
+                   uint8_t*, int64_t, uint2*, int64_t, unsigned long long*, uint8_t*, uint8_t*, int32_t*, int);
+};
+
+template <int K, int W, int OCC>
+void launch_alignlong(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
+                      int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, uint2* bnd, int64_t brows,
+                      unsigned long long* nx, uint8_t* sx, uint8_t* sy, int32_t* slen, int cap) {
+    hipLaunchKernelGGL((k_alignlong<K, W, OCC>), g, b, 0, st, x, y, ps, sc, ms, om, out, so, tr, bb, bnd, brows, nx,
+                       sx, sy, slen, cap);
+}
+
+#define T2_VARIANTL(K, W, OCC) VariantL{K, W, OCC, (const void*)&k_alignlong<K, W, OCC>, &launch_alignlong<K, W, OCC>}
+// tile widths 64 K W: 2 048 (production), 1 024 and 256 (TAXI2_LONG_TILE: tests cover many tiles
+// with short sequences)
+const VariantL kAlignLong[] = {T2_VARIANTL(8, 4, 2), T2_VARIANTL(8, 2, 2), T2_VARIANTL(4, 1, 2)};
+
+// Gotoh pairs of any length (alignlong_kernel.hpp): rows = X sequences, columns = Y sequences.
+int launch_alignlong_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps, const KScores& k,
+                           const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores, hipStream_t st,
+                           uint8_t* sx = nullptr, uint8_t* sy = nullptr, int32_t* slen = nullptr, int cap = 0) {
+    if (ps.count <= 0) return 0;
+    const VariantL* v = &kAlignLong[0];
+    if (const char* t = getenv("TAXI2_LONG_TILE")) {
+        const int tc = atoi(t);
+        for (const auto& c : kAlignLong)
+            if (64 * c.K * c.W == tc) v = &c;
+    }
+    const int64_t TC = 64 * v->K * v->W;
+    const int64_t rows = std::max(1, X.max_len), cols = std::max(1, Y.max_len);
+    const int64_t ntile = (cols + TC - 1) / TC;
+    const size_t bb = ((size_t)ntile * (size_t)(rows + 63) * (size_t)TC + 255) / 256 * 256;
+    int per_cu = 0;
+    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v->fn, 64 * (v->W + 1), 0));
+    double budget_gb = 40.0;
+    if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
+    const int64_t fit = (int64_t)(budget_gb * 1e9 / (2.0 * (double)bb));
+    if (2.0 * (double)bb > 200e9)
+        return fail(ctx, "pair trace of %lld x %lld bp needs %.1f GB (limit 200 GB)", (long long)rows,
+                    (long long)cols, 2.0 * (double)bb / 1e9);
+    const int64_t grid = std::max<int64_t>(1, std::min({ps.count, (int64_t)ctx->num_cus * std::max(1, per_cu), fit}));
+    if (shared_acquire(ctx, st)) return -1;
+    if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
+    const int64_t brows = rows + 64;
+    if (ensure(ctx, &ctx->d_bnd, &ctx->d_bnd_bytes, (size_t)grid * (size_t)brows * sizeof(uint2))) return -1;
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32)) return -1;
+    unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 32, st));
+    v->launch(dim3((unsigned)grid), dim3(64 * (v->W + 1)), st, view(X), view(Y), ps, k, ms, out_mode, d_out, d_scores,
+              (uint8_t*)ctx->d_trace, (int64_t)bb, (uint2*)ctx->d_bnd, brows, next, sx, sy, slen, cap);
+    HIP_TRY(ctx, hipGetLastError());
+    if (shared_release(ctx, st)) return -1;
+    return 0;
+}
+
 int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                        const taxi2_scores* sc, const MetricSpec& ms, int out_mode, double* d_out,
                        int32_t* d_scores, hipStream_t st) {
     const KScores k = kscores(sc);
     const int max_len = std::max(X.max_len, Y.max_len);
-    if (max_len > 4095) return fail(ctx, "sequence length %d exceeds the aligner's limit of 4095", max_len);
+    // int DP range check (32-bit, doubled and tie-tagged): every finite score stays far above NEG_INF
+    {
+        const long long mag = std::max({std::llabs(k.ma), std::llabs(k.mi), std::llabs(k.io),
+                                        std::llabs(k.ie), std::llabs(k.eo), std::llabs(k.ee)});
+        if (mag * (2LL * max_len + 2) >= (1LL << 26))
+            return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
+    }
+    // past every register-resident shape (and on request, TAXI2_LONG=1): the column-tiled aligner
+    if (max_len > 4095 || getenv("TAXI2_LONG")) {
+        if (is_linear(k))
+            return fail(ctx, "sequence length %d: linear (open == extend) scores are aligned up to 4095 bp", max_len);
+        return launch_alignlong_pairs(ctx, X, Y, ps, k, ms, out_mode, d_out, d_scores, st);
+    }
     const Variant* v = pick_variant(k, max_len);
     if (!v) return fail(ctx, "sequence length %d exceeds the aligner's column capacity", max_len);
     // int DP range check: every finite (doubled, tie-tagged) score stays far above NEG_INF
@@ -782,6 +863,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
+    if (ctx->d_bnd) (void)hipFree(ctx->d_bnd);
     if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
     if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
     if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
@@ -879,7 +961,7 @@ int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const ta
     DevSet* s = get_set(ctx, set);
     if (!s) return fail(ctx, "unknown set %d", set);
     MetricSpec ms;
-    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, s->max_len)) return -1;
     const int64_t total = s->n * (s->n - 1) / 2;
     if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
     if (s->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
@@ -896,7 +978,7 @@ int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, cons
     DevSet* s = get_set(ctx, set);
     if (!s) return fail(ctx, "unknown set %d", set);
     MetricSpec ms;
-    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, s->max_len)) return -1;
     const int64_t total = s->n * (s->n - 1) / 2;
     if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -909,6 +991,21 @@ int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, cons
     return launch_prealigned(ctx, *s, *s, ps, ms, d_out, st);
 }
 
+int taxi2_counts_metrics_dev(taxi2_ctx* ctx, const uint64_t* d_counts, int64_t n, const int32_t* metrics,
+                             int nmetrics, double scale, double* d_out, void* stream) {
+    if (!ctx) return -1;
+    if (n < 0 || (n > 0 && (!d_counts || !d_out))) return fail(ctx, "invalid arguments to taxi2_counts_metrics_dev");
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (n == 0) return 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, (int64_t)ctx->num_cus * 32);
+    hipLaunchKernelGGL(k_counts_metrics, dim3((unsigned)blocks), dim3(256), 0, st, d_counts, n, ms, scale, d_out);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
 int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
                      const int32_t* metrics, int nmetrics, double* out, int32_t* scores_out) {
     if (!ctx) return -1;
@@ -917,7 +1014,7 @@ int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q
     if (!Q || !R) return fail(ctx, "unknown set");
     if (Q->mode != R->mode) return fail(ctx, "query and reference sets differ in mode");
     MetricSpec ms;
-    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, std::max(Q->max_len, R->max_len))) return -1;
     if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
     if (Q->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
     if (Q->mode == TAXI2_MODE_PREALIGNED && scores_out) return fail(ctx, "no scores in PREALIGNED mode");
@@ -935,7 +1032,7 @@ int taxi2_list_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, co
     if (!X || !Y) return fail(ctx, "unknown set");
     if (X->mode != Y->mode) return fail(ctx, "sets differ in mode");
     MetricSpec ms;
-    if (check_metrics(ctx, metrics, nmetrics, ms)) return -1;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, std::max(X->max_len, Y->max_len))) return -1;
     if (count < 0) return fail(ctx, "negative count");
     if (count == 0) return 0;
     if (X->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
@@ -1038,6 +1135,54 @@ int taxi2_closest(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, 
     return 0;
 }
 
+// Aligned strings of pairs longer than the register-resident trace kernel takes: the column-tiled
+// aligner's walkers write them (both slots), in chunks of pairs bounded by the output staging.
+int align_strings_long(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
+                       int64_t count, const KScores& k, int32_t cap, uint8_t* out_x, uint8_t* out_y,
+                       int32_t* out_len) {
+    if (is_linear(k)) return fail(ctx, "aligned strings past 4095 bp need Gotoh (open != extend) scores");
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)1 << 30) / (4 * (int64_t)cap)));
+    uint8_t* d_s = nullptr;
+    int64_t* d_idx = nullptr;
+    int32_t* d_len = nullptr;
+    int rc = 0;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(ctx->stream);
+        if (d_s) (void)hipFree(d_s);
+        if (d_idx) (void)hipFree(d_idx);
+        if (d_len) (void)hipFree(d_len);
+    };
+    if (hipMalloc(&d_s, (size_t)chunk * 4 * cap) != hipSuccess || hipMalloc(&d_idx, (size_t)chunk * 16) != hipSuccess ||
+        hipMalloc(&d_len, (size_t)chunk * 8) != hipSuccess) {
+        cleanup();
+        return fail(ctx, "aligned strings: device allocation failed");
+    }
+    MetricSpec none{};
+    for (int64_t c0 = 0; c0 < count && rc == 0; c0 += chunk) {
+        const int64_t n = std::min(chunk, count - c0);
+        if (hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+            rc = fail(ctx, "aligned strings: index upload failed");
+            break;
+        }
+        PairSrc ps{PAIRS_LIST, 0, n, 0, 0, d_idx, d_idx + chunk};
+        rc = launch_alignlong_pairs(ctx, X, Y, ps, k, none, OUT_BOTH, nullptr, nullptr, ctx->stream, d_s,
+                                    d_s + (size_t)chunk * 2 * cap, d_len, cap);
+        if (rc) break;
+        if (hipMemcpyAsync(out_x + c0 * 2 * cap, d_s, (size_t)n * 2 * cap, hipMemcpyDeviceToHost, ctx->stream) !=
+                hipSuccess ||
+            hipMemcpyAsync(out_y + c0 * 2 * cap, d_s + (size_t)chunk * 2 * cap, (size_t)n * 2 * cap,
+                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(out_len + c0 * 2, d_len, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            rc = fail(ctx, "aligned strings: copy back failed");
+            break;
+        }
+    }
+    cleanup();
+    return rc;
+}
+
 int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                         int64_t count, const taxi2_scores* sc, int both, int32_t cap, uint8_t* out_x,
                         uint8_t* out_y, int32_t* out_len) {
@@ -1050,6 +1195,8 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
     if (cap < X->max_len + Y->max_len) return fail(ctx, "cap %d < longest x + longest y", cap);
     if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (std::max(X->max_len, Y->max_len) > 4095 || getenv("TAXI2_LONG"))
+        return align_strings_long(ctx, *X, *Y, xs, ys, count, kscores(sc), cap, out_x, out_y, out_len);
     Tracer tr;
     if (tr.setup(ctx, *X, *Y, kscores(sc), cap)) return -1;
     for (int64_t c0 = 0; c0 < count; c0 += tr.chunk) {
@@ -1346,6 +1493,25 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
                          has_genera ? 1 : 0, has_species ? 1 : 0, labels, label_offs};
     return format_impl(ctx, 2, vals, nrows, ncols, nm, nullptr, nullptr, row_pre, row_offs, col_pre, col_offs,
                        decimals, missing, missing_len, out, cap, out_len, &sm);
+}
+
+int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,
+                               const int32_t* d_row_code, const int64_t* d_col_start, const int32_t* d_col_idx,
+                               int32_t ns, int init, double* d_sum, double* d_min, double* d_max, int64_t* d_count,
+                               void* stream) {
+    if (!ctx) return -1;
+    if (nrows < 0 || ncols < 0 || m < 1 || ns < 0) return fail(ctx, "invalid sizes to taxi2_subset_aggregate_dev");
+    const int64_t nk = (int64_t)ns * ns * m;
+    if (nk == 0) return 0;
+    if (!d_sum || !d_min || !d_max || !d_count || !d_col_start || (nrows > 0 && (!d_vals || !d_row_code)) ||
+        (ncols > 0 && !d_col_idx))
+        return fail(ctx, "null pointer passed to taxi2_subset_aggregate_dev");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    hipLaunchKernelGGL(k_subset_aggregate_rows, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, st, d_vals, nrows,
+                       ncols, m, d_row_code, d_col_start, d_col_idx, ns, init ? 1 : 0, d_sum, d_min, d_max, d_count);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
 }
 
 int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* code, int32_t ns, double* sum,

@@ -42,6 +42,10 @@ struct KScores {
 };
 
 constexpr int MAX_METRICS = 8;
+// Pseudo-metric (TAXI2_METRIC_COUNTS): a launch writes the four column counters of each ordered pair
+// packed into the 8 bytes of its f64 slot (valid | ts << 16 | tv << 32 | gap << 48); every metric
+// is a function of them (metric_value), evaluated later by k_counts_metrics.
+constexpr int METRIC_COUNTS = 16;
 struct MetricSpec {
     int n;
     int code[MAX_METRICS];
@@ -104,6 +108,9 @@ __device__ __forceinline__ double metric_value(int code, uint32_t valid, uint32_
             const double Q = (double)tv / v;
             return -0.5 * log(1.0 - 2.0 * P - Q) - 0.25 * log(1.0 - 2.0 * Q);
         }
+        case METRIC_COUNTS:  // the counters themselves, 16 bits each (max_len <= 32767 checked by the host)
+            return __longlong_as_double((long long)((uint64_t)valid | (uint64_t)ts << 16 | (uint64_t)tv << 32 |
+                                                    (uint64_t)gap << 48));
         default:
             return __builtin_nan("");
     }

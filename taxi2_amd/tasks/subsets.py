@@ -123,6 +123,32 @@ def write_summary(path: Path, seqs: list, A: np.ndarray, metrics: list, genera, 
             )) + "\n")
 
 
+def summary_lines(A: np.ndarray, x0: int, seqs: list, metrics: list, genera, species, fmt: str,
+                  missing: str) -> str:
+    """summary.tsv lines of the rows [x0, x0 + len(A)) x all columns, unique ids (one line per
+    ordered pair: no (x.id, y.id) run spans two pairs), for the streamed writer."""
+    ids = [s.id for s in seqs]
+    gx = [genera.get(i, None) for i in ids] if genera else None
+    sx = [species.get(i, None) for i in ids] if species else None
+    text = _values_text(A, fmt, missing)
+    out = []
+    for r in range(A.shape[0]):
+        i = x0 + r
+        x = seqs[i]
+        for j, y in enumerate(seqs):
+            g = SubsetPair(gx[i], gx[j]) if gx is not None else None
+            s = SubsetPair(sx[i], sx[j]) if sx is not None else None
+            out.append("\t".join((
+                x.id, y.id, *text[r, j],
+                *[v if v is not None else missing for v in x.extras.values()],
+                *[v if v is not None else missing for v in y.extras.values()],
+                (g.x if g else None) or "-", (s.x if s else None) or "-",
+                (g.y if g else None) or "-", (s.y if s else None) or "-",
+                comparison_type(g, s),
+            )) + "\n")
+    return "".join(out)
+
+
 def _values_text(A: np.ndarray, fmt: str, missing: str) -> np.ndarray:
     from .common import format_values
 
@@ -149,6 +175,47 @@ def aggregate(A: np.ndarray, ids: list[str], partition) -> SubsetStats:
     mn = np.where(agg.count > 0, agg.min, np.nan)
     mx = np.where(agg.count > 0, agg.max, np.nan)
     return SubsetStats(subsets, mean, mn, mx, agg.count)
+
+
+class SubsetAggregatorDev:
+    """DistanceAggregator state of one partition on the GPU (versus_all.py:57-96, 617-640), fed the
+    streamed row blocks in ascending order (taxi2_subset_aggregate_dev): the N x N values never
+    exist on the host.  Same result as :func:`aggregate` over the full matrix, bit for bit."""
+
+    def __init__(self, eng, ids: list[str], partition, m: int):
+        import torch
+
+        code, self.subsets = subset_codes(ids, partition)
+        ns = len(self.subsets)
+        dev = torch.device("cuda", eng.device)
+        order = np.argsort(code, kind="stable")  # columns grouped by subset, ascending within one
+        start = np.zeros(ns + 1, dtype=np.int64)
+        start[1:] = np.cumsum(np.bincount(code, minlength=ns))
+        self.eng, self.m, self.ns, self.n = eng, m, ns, len(ids)
+        self.row_code = torch.as_tensor(code, dtype=torch.int32, device=dev)
+        self.col_start = torch.as_tensor(start, dtype=torch.int64, device=dev)
+        self.col_idx = torch.as_tensor(order.astype(np.int32), dtype=torch.int32, device=dev)
+        shape = (ns, ns, m)
+        self.sum = torch.zeros(shape, dtype=torch.float64, device=dev)
+        self.min = torch.full(shape, float("inf"), dtype=torch.float64, device=dev)
+        self.max = torch.zeros(shape, dtype=torch.float64, device=dev)
+        self.count = torch.zeros(shape, dtype=torch.int64, device=dev)
+        self.torch = torch
+
+    def add(self, D, x0: int, x1: int) -> None:
+        """D: (x1 - x0, n, m) float64 device tensor of the rows' adjusted values (NaN = None)."""
+        D = D.contiguous()
+        st = self.torch.cuda.current_stream(D.device).cuda_stream
+        self.eng.subset_aggregate_dev(D.data_ptr(), x1 - x0, self.n, self.m, self.row_code[x0:x1].data_ptr(),
+                                      self.col_start.data_ptr(), self.col_idx.data_ptr(), self.ns, False,
+                                      self.sum.data_ptr(), self.min.data_ptr(), self.max.data_ptr(),
+                                      self.count.data_ptr(), st)
+
+    def result(self) -> SubsetStats:
+        s, lo, hi, c = (t.cpu().numpy() for t in (self.sum, self.min, self.max, self.count))
+        with np.errstate(invalid="ignore", divide="ignore"):
+            mean = np.where(c > 0, s / np.maximum(c, 1), np.nan)
+        return SubsetStats(self.subsets, mean, np.where(c > 0, lo, np.nan), np.where(c > 0, hi, np.nan), c)
 
 
 def _text(v: float, fmt: str) -> str:

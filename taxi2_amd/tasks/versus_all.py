@@ -80,6 +80,14 @@ class VersusAll:
         self.params.stats.species = False
         self.params.stats.genera = False
 
+        # MI355X engine options (no reference counterpart).  stream: None = automatic (row-block
+        # streaming when the dense N x N x M host matrix would exceed dense_limit bytes, or with
+        # more than one rank), True / False force it; block_bytes sizes the streamed row blocks.
+        self.params.engine = AttrDict()
+        self.params.engine.stream = None
+        self.params.engine.dense_limit = 4 << 30
+        self.params.engine.block_bytes = 256 << 20
+
         self.distances: np.ndarray | None = None  # (N, N, M) after start(), NaN = None
 
     # ------------------------------------------------------------------ reference steps
@@ -322,6 +330,140 @@ class VersusAll:
                                         self.params.distances.metrics, self.params.format.float,
                                         self.params.format.stats_template)
 
+    # ------------------------------------------------------------------ streamed driver
+    def _streaming(self, seqs: list) -> bool:
+        """Row-block streaming (taxi2_amd/streaming.py) instead of the dense (N, N, M) matrix."""
+        from ..sharding import world_info
+
+        n, M = len(seqs), len(self.params.distances.metrics)
+        want = self.params.engine.stream
+        if want is None:
+            want = world_info()[0] or n * n * M * 8 > self.params.engine.dense_limit
+        if not want or n == 0:
+            return False
+        ids = [s.id for s in seqs]
+        ok = len(set(ids)) == n and fixed_decimals(self.params.format.float) is not None
+        if not ok and self.params.engine.stream:
+            raise NotImplementedError("streamed versusAll needs unique ids and a '{:.Nf}' formatter "
+                                      "(the reference's line grouping of duplicate ids spans row blocks)")
+        return ok and max((len(s.seq) for s in seqs), default=0) <= 32767
+
+    def _start_streaming(self, seqs: list) -> None:
+        """versus_all.py:732-773 with bounded memory: every rank computes its triangle rows into a
+        TriangleStore (packed counters, + NCD), then the ordered product is assembled on rank 0 one
+        row block at a time (x-major) and every writer / aggregator consumes the block."""
+        import torch
+
+        from ..sharding import world_info
+        from ..streaming import TriangleStore
+
+        dist_on, rank = world_info()
+        world = 1
+        group_backend = None
+        if dist_on:
+            import torch.distributed as dist
+
+            world = dist.get_world_size()
+            group_backend = dist.get_backend()
+        labels = [str(m) for m in self.params.distances.metrics]
+        M = len(labels)
+        cidx = [k for k, lab in enumerate(labels) if lab != "ncd"]
+        nidx = [k for k, lab in enumerate(labels) if lab == "ncd"]
+        clabels = [labels[k] for k in cidx]
+        align = bool(self.params.pairs.align)
+        scores = Scores(**(self.params.pairs.scores or {})).as_tuple()
+        n = len(seqs)
+        total = M * n * n
+        if nidx:
+            check_ncd_strings(s.seq for s in seqs)
+        eng = self._engine()
+        cuda = torch.device("cuda", eng.device)
+        store_dev = cuda if group_backend in (None, "nccl") else torch.device("cpu")
+        store = TriangleStore(n, world, rank, device=store_dev)
+        st = eng.upload([s.seq for s in seqs], align=align)
+        # one real stream for the torch ops and the engine's *_dev calls of this path (the legacy
+        # default stream has handle 0, which the engine would read as "its own stream")
+        stream = torch.cuda.Stream(cuda)
+        with torch.cuda.stream(stream):
+            self._stream_blocks(seqs, eng, st, store, stream, align, scores, labels, cidx, nidx, clabels,
+                                world, rank, total)
+
+    def _stream_blocks(self, seqs, eng, st, store, stream, align, scores, labels, cidx, nidx, clabels, world,
+                       rank, total) -> None:
+        import torch
+
+        from .._native import tri_pairs
+        from ..streaming import block_rows
+
+        n, M = len(seqs), len(labels)
+        cuda = stream.device
+        store_dev = store.device
+        try:
+            # ---- 1. this rank's triangle rows
+            cpl = store.add_plane("counts", torch.int64) if cidx else None
+            npl = store.add_plane("ncd", torch.float64) if nidx else None
+            step = 1 << 22
+            for c0 in range(0, store.count, step):
+                c = min(step, store.count - c0)
+                k = store.k0 + c0
+                if cpl is not None:
+                    out = torch.empty((c, 2 if align else 1), dtype=torch.float64, device=cuda)
+                    eng.all_pairs_dev(st, k, c, ("counts",), out.data_ptr(), scores, None, stream.cuda_stream)
+                    v = out.view(torch.int64)
+                    cpl[c0 : c0 + c] = (v if align else v.expand(c, 2)).to(store_dev)
+                if npl is not None:
+                    a, b = tri_pairs(n, k, c)
+                    npl[c0 : c0 + c] = torch.from_numpy(eng.ncd_pairs(st, st, a, b, scores, aligned=align, both=True))
+                report(self.progress_handler, "distance.x.id", min(total, 2 * M * (k + c) * world), total)
+            torch.cuda.synchronize(cuda)
+            # ---- 2. diagonal rule inputs (rank 0): identical full tuples -> None, unless the
+            # alignment of the sequence with itself is not the identity (non-default scores)
+            sink = _BlockWriters(self, seqs, eng) if rank == 0 else None
+            if sink is not None:
+                groups: dict = {}
+                for i, s in enumerate(seqs):
+                    groups.setdefault(seq_key(s), []).append(i)
+                dup = list(groups.values())
+                self_vals = None
+                if align:
+                    reps = np.array([g[0] for g in dup], dtype=np.int64)
+                    strings = eng.align_strings(st, st, reps, reps, scores)
+                    self_vals = np.empty((len(reps), M))
+                    if cidx:
+                        self_vals[:, cidx] = eng.list_pairs(st, st, reps, reps, clabels, scores)[:, 0, :]
+                    if nidx:
+                        sv = eng.ncd_pairs(st, st, reps, reps, scores, aligned=True, both=False)
+                        for kk in nidx:
+                            self_vals[:, kk] = sv
+                sink.diag = (dup, self_vals, strings if align else None)
+            # ---- 3. row blocks, x-major
+            per_entry = 8 * (len(store.planes) + M)
+            B = block_rows(n, per_entry, int(self.params.engine.block_bytes))
+            for x0 in range(0, n, B):
+                x1 = min(n, x0 + B)
+                blk = store.assemble(x0, x1)
+                if sink is None:
+                    continue
+                D = torch.empty((x1 - x0, n, M), dtype=torch.float64, device=cuda)
+                scale = 100.0 if self.params.format.percentage_multiply else 1.0
+                if cidx:
+                    cnt = blk["counts"].to(cuda).contiguous()
+                    tmp = torch.empty((cnt.numel(), len(cidx)), dtype=torch.float64, device=cuda)
+                    eng.counts_metrics_dev(cnt.data_ptr(), cnt.numel(), clabels, tmp.data_ptr(), scale,
+                                           stream.cuda_stream)
+                    D[:, :, cidx] = tmp.view(x1 - x0, n, len(cidx))
+                if nidx:
+                    nv = blk["ncd"].to(cuda)
+                    for kk in nidx:
+                        D[:, :, kk] = nv * scale if scale != 1.0 else nv
+                sink.consume(x0, x1, D, scale)
+                del D
+                report(self.progress_handler, "distance.x.id", min(total, M * n * x1), total)
+            if sink is not None:
+                sink.close()
+        finally:
+            st.free()
+
     # ------------------------------------------------------------------ driver
     def start(self) -> Results:
         ts = perf_counter()
@@ -331,6 +473,13 @@ class VersusAll:
         seqs = list(self.input.sequences)
         if self.params.pairs.align:
             seqs = [s.normalize() for s in seqs]
+        if self._streaming(seqs):
+            self.distances = None
+            self._start_streaming(seqs)
+            n = len(seqs)
+            total = len(self.params.distances.metrics) * n * n
+            report(self.progress_handler, "Finalizing...", total, total)
+            return Results(self.work_dir, perf_counter() - ts)
         D = self.compute_distances(seqs)
         self.distances = D
         rank0 = True
@@ -351,3 +500,143 @@ class VersusAll:
         total = len(self.params.distances.metrics) * n * n
         report(self.progress_handler, "Finalizing...", total, total)
         return Results(self.work_dir, perf_counter() - ts)
+
+
+class _BlockWriters:
+    """Rank 0's consumers of the streamed row blocks: aligned_pairs.txt, linear.tsv, matricial
+    files, summary.tsv (GPU text formatter, unique ids) and the subset aggregators (on the GPU,
+    taxi2_subset_aggregate_dev), each fed the rows [x0, x1) in x-major order -- the file contents
+    are those of the dense path (tests/test_gpu_streaming.py)."""
+
+    def __init__(self, task: VersusAll, seqs: list, eng):
+        import torch
+
+        from .subsets import SubsetAggregatorDev, subset_codes
+
+        self.task, self.seqs, self.eng = task, seqs, eng
+        p = task.params
+        self.metrics = p.distances.metrics
+        self.fmt, self.missing = p.format.float, p.format.missing
+        self.dec = fixed_decimals(self.fmt)
+        self.ids = [s.id for s in seqs]
+        n = len(seqs)
+        self.diag = None
+        self.files = []
+        ex0 = list(seqs[0].extras.keys())
+        self.pre = ["\t".join([s.id, *[v if v is not None else self.missing for v in s.extras.values()]])
+                    for s in seqs]
+        self.lin = self.mats = None
+        if p.distances.write_linear:
+            create_parents(task.paths.distances_linear)
+            self.lin = open(task.paths.distances_linear, "wb")
+            head = ["seqid (query)", *[k + " (query)" for k in ex0], "seqid (reference)",
+                    *[k + " (reference)" for k in ex0], *[str(m) for m in self.metrics]]
+            self.lin.write(("\t".join(head) + "\n").encode("utf-8"))
+        if p.distances.write_matricial:
+            create_parents(task.paths.distances_matricial)
+            self.mats = []
+            for metric in self.metrics:
+                fh = open(task.paths.distances_matricial / f"{metric}.tsv", "wb")
+                fh.write(("\t".join(["", *self.ids]) + "\n").encode("utf-8"))
+                self.mats.append(fh)
+        # summary.tsv (always)
+        genera, species = task.input.genera, task.input.species
+        self.genera, self.species = genera, species
+        gx = [genera.get(i, None) for i in self.ids] if genera else None
+        sx = [species.get(i, None) for i in self.ids] if species else None
+        ext = ["".join("\t" + (v if v is not None else self.missing) for v in s.extras.values()) for s in seqs]
+        gs = ["\t" + ((gx[k] if gx else None) or "-") + "\t" + ((sx[k] if sx else None) or "-") for k in range(n)]
+        self.suf = [t for pair in zip(ext, gs) for t in pair]
+        gcode = subset_codes(self.ids, genera)[0] if genera else np.zeros(n, np.int32)
+        scode = subset_codes(self.ids, species)[0] if species else np.zeros(n, np.int32)
+        self.codes = np.stack([gcode, scode], axis=1)
+        create_parents(task.paths.summary)
+        self.summ = open(task.paths.summary, "wb")
+        head = ["seqid (query 1)", "seqid (query 2)", *[str(m) for m in self.metrics],
+                *[k + " (query 1)" for k in ex0], *[k + " (query 2)" for k in ex0],
+                "genus (query 1)", "species (query 1)", "genus (query 2)", "species (query 2)", "comparison_type"]
+        self.summ.write(("\t".join(head) + "\n").encode("utf-8"))
+        self.aggs = [(name, SubsetAggregatorDev(eng, self.ids, part, len(self.metrics)))
+                     for part, name in ((genera, "genera"), (species, "species")) if part]
+        self.pairs_fh = None
+        if p.pairs.write:
+            create_parents(task.paths.aligned_pairs)
+            self.pairs_fh = SequencePairHandler.Formatted(task.paths.aligned_pairs, "w")
+            self.aligner = (PairwiseAligner.Biopython(p.pairs.scores, engine=eng) if p.pairs.align else None)
+        self.torch = torch
+
+    def consume(self, x0: int, x1: int, D, scale: float) -> None:
+        """D: (x1 - x0, n, M) device tensor of the rows' values, x100 applied, diagonal not yet."""
+        torch = self.torch
+        dup, self_vals, strings = self.diag
+        # diagonal rule (versus_all.py:549): per group of identical full tuples
+        for gi, g in enumerate(dup):
+            rows = [i for i in g if x0 <= i < x1]
+            if not rows:
+                continue
+            if strings is not None and strings[gi][0] != strings[gi][1]:
+                sv = torch.as_tensor(self_vals[gi] * scale if scale != 1.0 else self_vals[gi], device=D.device)
+                for i in rows:
+                    D[i - x0, i] = sv
+                continue
+            cols = torch.as_tensor(g, device=D.device)
+            for i in rows:
+                D[i - x0, cols] = float("nan")
+        for _, agg in self.aggs:
+            agg.add(D, x0, x1)
+        A = D.cpu().numpy()
+        seqs, ids = self.seqs, self.ids
+        if self.pairs_fh is not None:
+            for x in seqs[x0:x1]:
+                if self.aligner is None:
+                    for y in seqs:
+                        self.pairs_fh.write(SequencePair(x, y))
+                else:
+                    for pair in self.aligner.align_many([SequencePair(x, y) for y in seqs]):
+                        self.pairs_fh.write(pair)
+        ok = gpu_text_ok(A, self.dec)
+        if self.lin is not None:
+            if ok:
+                write_rows_gpu(self.lin, self.eng, A, self.pre[x0:x1], self.pre, self.dec, self.missing)
+            else:
+                text = format_values(A, self.fmt, self.missing)
+                for i in range(x1 - x0):
+                    rows = ["\t".join((self.pre[x0 + i], self.pre[j], *text[i, j])) for j in range(len(seqs))]
+                    self.lin.write(("\n".join(rows) + "\n").encode("utf-8"))
+        if self.mats is not None:
+            for m, fh in enumerate(self.mats):
+                Am = np.ascontiguousarray(A[:, :, m])
+                if ok:
+                    write_rows_gpu(fh, self.eng, Am, ids[x0:x1], None, self.dec, self.missing)
+                else:
+                    text = format_values(Am, self.fmt, self.missing)
+                    for i in range(x1 - x0):
+                        fh.write(("\t".join((ids[x0 + i], *text[i])) + "\n").encode("utf-8"))
+        if ok:
+            from .subsets import SUMMARY_CHUNK_VALUES
+
+            step = max(1, SUMMARY_CHUNK_VALUES // max(1, A.shape[1] * A.shape[2]))
+            for r0 in range(0, x1 - x0, step):
+                r1 = min(x1 - x0, r0 + step)
+                self.summ.write(self.eng.format_summary(
+                    A[r0:r1], ids[x0 + r0 : x0 + r1], ids, self.suf[2 * (x0 + r0) : 2 * (x0 + r1)], self.suf,
+                    self.codes[x0 + r0 : x0 + r1], self.codes, has_genera=bool(self.genera),
+                    has_species=bool(self.species), decimals=self.dec, missing=self.missing))
+        else:
+            from .subsets import summary_lines
+
+            self.summ.write(summary_lines(A, x0, seqs, self.metrics, self.genera, self.species, self.fmt,
+                                          self.missing).encode("utf-8"))
+
+    def close(self) -> None:
+        from .subsets import write_subset_statistics
+
+        for fh in [self.lin, self.summ, *(self.mats or [])]:
+            if fh is not None:
+                fh.close()
+        if self.pairs_fh is not None:
+            self.pairs_fh.close()
+        p = self.task.params
+        for name, agg in self.aggs:
+            write_subset_statistics(self.task.paths.subsets / name, agg.result(), self.metrics, p.format.float,
+                                    p.format.stats_template)

@@ -1,0 +1,57 @@
+"""bench.py's multi-GPU arithmetic with 2 ranks over gloo on CPU (the driver runs the real thing on
+an 8-GPU node with RCCL): every rank's blocks are disjoint from every other rank's and step's, the
+slowest rank's time is the job time (all-reduce MAX), and value = all ranks' pairs / that time."""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import textwrap
+
+from tests.conftest import ROOT
+from tests.test_sharding_gloo import free_port
+
+WORKER = textwrap.dedent(
+    """
+    import json, os, sys
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, {root!r})
+    import bench
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    total, B, steps, warm = bench.N_SEQS * (bench.N_SEQS - 1) // 2, 1 << 19, 6, 2
+    mine = [bench.step_block(s, rank, world, B, total) for s in range(warm + steps)]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    elapsed = bench.max_over_ranks(1.0 + rank, world)    # rank 1 is the slow one
+    value = bench.job_value(steps, B, world, elapsed)
+    with open(os.environ["OUT"] + f".{{rank}}", "w") as fh:
+        json.dump({{"blocks": got, "elapsed": elapsed, "value": value}}, fh)
+    dist.destroy_process_group()
+    """
+)
+
+
+def test_bench_two_ranks_gloo(tmp_path):
+    import json
+
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=str(ROOT)))
+    out = tmp_path / "res"
+    env = dict(os.environ, OUT=str(out), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = [json.loads((tmp_path / f"res.{k}").read_text()) for k in range(2)]
+    B = 1 << 19
+    starts = [b for blocks in res[0]["blocks"] for b in blocks]
+    assert len(set(starts)) == len(starts)
+    spans = sorted(starts)
+    assert all(b - a >= B for a, b in zip(spans, spans[1:]))  # no two blocks overlap
+    for rec in res:
+        assert rec["elapsed"] == 2.0                        # the slower rank's time on both
+        assert rec["value"] == 6 * B * 2 / 2.0              # all ranks' pairs / that time
