@@ -213,6 +213,13 @@ def main() -> None:
             },
             "compute_roofline": compute,
             "cpu_baseline": cpu,
+            "assumptions": [
+                "Biopython 1.85's tie order among equal-scoring alignments is restated (end state M>Ix>Iy, "
+                "each backward step the first tied predecessor; (y, x) = Ix/Iy swapped), not pinned: every "
+                "reference alignment vector accepts all tied optima (DESIGN.md §2)",
+                "the workload is the config-3 generator (synthetic, seeded); no reference number exists "
+                "(BASELINE.json published = {})",
+            ],
         }
         print(json.dumps(line), flush=True)
     if world > 1:

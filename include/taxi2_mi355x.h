@@ -163,13 +163,14 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
  * out[k*2+1] = value of (y, x).  With scores (ALIGN sets): x, y are the first Biopython
  * alignment's gapped strings of that ordered pair, as VersusAll feeds them to the metric
  * (versus_all.py:532, 546-552); scores == NULL: the sequences as stored.  Raw sequences must
- * satisfy len(x) + len(y) <= 16382 (one deflate block). */
+ * satisfy len(x) + len(y) <= 65273 and aligned strings 2 (len(x) + len(y)) <= 65273 (one deflate window;
+ * the length accounts for every deflate block, deflate_len.hpp). */
 int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                     int64_t count, const taxi2_scores* sc, int both, double* out);
 
 /* ---- compressed length (alfpy ncd.complexity) --------------------------------------------- *
  * out[k] = len(zlib.compress(upper(x[xs[k]]) + upper(y[ys[k]]))), zlib 1.2.11 level 6;
- * ys == NULL compresses x[xs[k]] alone.  Inputs up to 16382 bytes. */
+ * ys == NULL compresses x[xs[k]] alone.  Inputs up to 65273 bytes. */
 int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                        int64_t count, int32_t* out);
 

@@ -312,7 +312,10 @@ k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int
                                 uint2 o = make_uint2((uint32_t)NEG_INF, (uint32_t)NEG_INF);
                                 if (lane == 0 && g < nA) {
                                     if (tile == 0) o = make_uint2((uint32_t)(sc.eo + sc.ee * g), (uint32_t)NEG_INF);
-                                    else o = *(const volatile uint2*)(bnd + g);
+                                    else {
+                                        const unsigned long long v = *(const volatile unsigned long long*)(bnd + g);
+                                        o = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                                    }
                                 }
                                 inF = (int)shr_old((uint32_t)payF, o.x);
                                 inY = (int)shr_old((uint32_t)payY, o.y);

@@ -669,6 +669,7 @@ struct Tracer {
     size_t lds = 0;
     KScores k{};
     bool lin = false;
+    bool longp = false;  // pairs past 4 095 bp (or TAXI2_LONG): the column-tiled aligner's walkers
 
     ~Tracer() {
         if (d_trace) (void)hipFree(d_trace);
@@ -681,10 +682,18 @@ struct Tracer {
     int setup(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const KScores& ks, int cap_) {
         if (X.mode != TAXI2_MODE_ALIGN || Y.mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need ALIGN sets");
         const int max_len = std::max(X.max_len, Y.max_len);
-        if (max_len > 4095) return fail(ctx, "sequence length %d exceeds 4095", max_len);
         k = ks;
         lin = is_linear(k);
         cap = cap_;
+        longp = max_len > 4095 || getenv("TAXI2_LONG");
+        if (longp) {  // strings from k_alignlong's walkers: only the index and output staging
+            if (lin) return fail(ctx, "aligned strings past 4095 bp need Gotoh (open != extend) scores");
+            chunk = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 30) / (4 * (int64_t)std::max(cap, 1))));
+            HIP_TRY(ctx, hipMalloc(&d_idx, (size_t)chunk * 2 * sizeof(int64_t)));
+            HIP_TRY(ctx, hipMalloc(&d_out, (size_t)chunk * 2 * cap * 2));
+            HIP_TRY(ctx, hipMalloc(&d_len, (size_t)chunk * 2 * sizeof(int32_t)));
+            return 0;
+        }
         if (max_len <= 256) K = 4, W = 1;
         else if (max_len <= 512) W = 1;
         else if (max_len <= 1024) W = 2;
@@ -711,6 +720,12 @@ struct Tracer {
             int both) {
         HIP_TRY(ctx, hipMemcpyAsync(d_idx, xs, n * 8, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(d_idx + chunk, ys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (longp) {  // both slots, whatever `both` asks (slot 1 is then simply not read)
+            PairSrc ps{PAIRS_LIST, 0, n, 0, 0, d_idx, d_idx + chunk};
+            MetricSpec none{};
+            return launch_alignlong_pairs(ctx, X, Y, ps, k, none, OUT_BOTH, nullptr, nullptr, ctx->stream, d_out,
+                                          d_out + chunk * 2 * cap, d_len, cap);
+        }
         const dim3 grid((unsigned)n), block(64 * W);
 #define T2_FILL(KK, WW, LIN)                                                                         \
     hipLaunchKernelGGL((k_trace_fill<KK, WW, LIN>), grid, block, lds, ctx->stream, view(X), view(Y), d_idx, \
@@ -1135,54 +1150,6 @@ int taxi2_closest(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, 
     return 0;
 }
 
-// Aligned strings of pairs longer than the register-resident trace kernel takes: the column-tiled
-// aligner's walkers write them (both slots), in chunks of pairs bounded by the output staging.
-int align_strings_long(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
-                       int64_t count, const KScores& k, int32_t cap, uint8_t* out_x, uint8_t* out_y,
-                       int32_t* out_len) {
-    if (is_linear(k)) return fail(ctx, "aligned strings past 4095 bp need Gotoh (open != extend) scores");
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)1 << 30) / (4 * (int64_t)cap)));
-    uint8_t* d_s = nullptr;
-    int64_t* d_idx = nullptr;
-    int32_t* d_len = nullptr;
-    int rc = 0;
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(ctx->stream);
-        if (d_s) (void)hipFree(d_s);
-        if (d_idx) (void)hipFree(d_idx);
-        if (d_len) (void)hipFree(d_len);
-    };
-    if (hipMalloc(&d_s, (size_t)chunk * 4 * cap) != hipSuccess || hipMalloc(&d_idx, (size_t)chunk * 16) != hipSuccess ||
-        hipMalloc(&d_len, (size_t)chunk * 8) != hipSuccess) {
-        cleanup();
-        return fail(ctx, "aligned strings: device allocation failed");
-    }
-    MetricSpec none{};
-    for (int64_t c0 = 0; c0 < count && rc == 0; c0 += chunk) {
-        const int64_t n = std::min(chunk, count - c0);
-        if (hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
-            hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
-            rc = fail(ctx, "aligned strings: index upload failed");
-            break;
-        }
-        PairSrc ps{PAIRS_LIST, 0, n, 0, 0, d_idx, d_idx + chunk};
-        rc = launch_alignlong_pairs(ctx, X, Y, ps, k, none, OUT_BOTH, nullptr, nullptr, ctx->stream, d_s,
-                                    d_s + (size_t)chunk * 2 * cap, d_len, cap);
-        if (rc) break;
-        if (hipMemcpyAsync(out_x + c0 * 2 * cap, d_s, (size_t)n * 2 * cap, hipMemcpyDeviceToHost, ctx->stream) !=
-                hipSuccess ||
-            hipMemcpyAsync(out_y + c0 * 2 * cap, d_s + (size_t)chunk * 2 * cap, (size_t)n * 2 * cap,
-                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-            hipMemcpyAsync(out_len + c0 * 2, d_len, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-            hipStreamSynchronize(ctx->stream) != hipSuccess) {
-            rc = fail(ctx, "aligned strings: copy back failed");
-            break;
-        }
-    }
-    cleanup();
-    return rc;
-}
-
 int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                         int64_t count, const taxi2_scores* sc, int both, int32_t cap, uint8_t* out_x,
                         uint8_t* out_y, int32_t* out_len) {
@@ -1195,8 +1162,6 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
     if (cap < X->max_len + Y->max_len) return fail(ctx, "cap %d < longest x + longest y", cap);
     if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (std::max(X->max_len, Y->max_len) > 4095 || getenv("TAXI2_LONG"))
-        return align_strings_long(ctx, *X, *Y, xs, ys, count, kscores(sc), cap, out_x, out_y, out_len);
     Tracer tr;
     if (tr.setup(ctx, *X, *Y, kscores(sc), cap)) return -1;
     for (int64_t c0 = 0; c0 < count; c0 += tr.chunk) {
@@ -1222,10 +1187,13 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
     if (!out || !xs || !ys) return fail(ctx, "null argument");
     if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
     const bool aligned = sc != nullptr;
-    // aligned strings are <= nA + nB <= 2 * 4095 each, so a concatenation fits one deflate block;
-    // raw sequences must fit it too
-    if (!aligned && (int64_t)X->max_len + Y->max_len > zl::ZMAX_INPUT)
-        return fail(ctx, "NCD: sequences longer than %d bytes together exceed one deflate block", zl::ZMAX_INPUT);
+    // the compressed streams (one sequence or aligned string, and a concatenation of two) must fit
+    // one 64 KiB deflate window (deflate_len.hpp): raw x + y, or two aligned strings of up to
+    // nA + nB bytes each
+    const int64_t longest = aligned ? 2 * ((int64_t)X->max_len + Y->max_len) : (int64_t)X->max_len + Y->max_len;
+    if (longest > zl::ZMAX_INPUT)
+        return fail(ctx, "NCD: compressed inputs up to %lld bytes exceed the %d-byte deflate window", (long long)longest,
+                    zl::ZMAX_INPUT);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int no = both ? 2 : 1;
     const int cap = X->max_len + Y->max_len;
@@ -1287,7 +1255,7 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
             return fail(ctx, "stream %lld index out of bounds", (long long)k);
     }
     if ((int64_t)X->max_len + (ys ? Y->max_len : 0) > zl::ZMAX_INPUT)
-        return fail(ctx, "zlib lengths: inputs longer than %d bytes exceed one deflate block", zl::ZMAX_INPUT);
+        return fail(ctx, "zlib lengths: inputs longer than %d bytes exceed the deflate window", zl::ZMAX_INPUT);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int64_t chunk = (int64_t)1 << 18;
     if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)chunk * 2 * 8)) return -1;

@@ -10,10 +10,15 @@
 // _tr_flush_block's stored / fixed / dynamic choice).  Only lengths are tracked: the output size
 // of one final block is 2 (zlib header) + block bytes + 4 (Adler-32).
 //
-// Inputs up to ZMAX_INPUT (16 382) bytes are one deflate block (fewer than lit_bufsize - 1 = 16383
-// symbols) inside one window (no sliding), which is what makes this closed-form accounting exact.
+// Blocks: deflate_slow flushes a block whenever _tr_tally has buffered lit_bufsize - 1 = 16 383
+// symbols (literals + matches, memLevel 8), at the position zlib's FLUSH_BLOCK macros use (after
+// the match's strstart++ for a match, before it for a literal), and a final block at the end; each
+// block is stored, fixed or dynamic by _tr_flush_block's byte comparison, and the bits of all
+// blocks are summed exactly (3-bit headers, stored blocks' byte alignment + LEN/NLEN, the final
+// bi_windup).  Inputs up to ZMAX_INPUT (65 273) bytes: the whole input sits in the 64 KiB window
+// and fill_window never slides it (a slide moves block_start below 0 and rebases the hash chains).
 // Pinned against Python's zlib.compress (zlib 1.2.11) by tests/test_ncd.py on random,
-// low-entropy and DNA-like inputs.
+// low-entropy and DNA-like inputs, single- and multi-block.
 #pragma once
 #include <stdint.h>
 
@@ -37,13 +42,13 @@ constexpr int LITERALS = 256, END_BLOCK = 256, L_CODES = 286, D_CODES = 30, BL_C
 constexpr int HEAP_SIZE = 2 * L_CODES + 1, MAX_BITS = 15, MAX_BL_BITS = 7;
 constexpr int REP_3_6 = 16, REPZ_3_10 = 17, REPZ_11_138 = 18;
 constexpr int LIT_BUFSIZE = 1 << (8 + 6);  // memLevel 8
-constexpr int ZMAX_INPUT = LIT_BUFSIZE - 2;  // one block, one window
+constexpr int ZMAX_INPUT = WSIZE + MAX_DIST - 1;  // one window: fill_window never slides
 constexpr int WIN_BYTES = ZMAX_INPUT + MAX_MATCH + 2;
 
 // Per-stream scratch the caller provides.  head[] must be all zero on entry; it is left all zero.
 struct Scratch {
     uint8_t* win;    // >= n + MAX_MATCH + 2 bytes
-    uint16_t* prev;  // >= n entries
+    uint16_t* prev;  // WSIZE entries (indexed pos & WMASK, as zlib's)
     uint16_t* head;  // HASH_SIZE entries
 };
 
@@ -231,8 +236,10 @@ __host__ __device__ ZL_COLD inline void scan_tree(Trees& t, uint16_t* dl, int ma
     }
 }
 
-// Bytes of the final block (_tr_flush_block + bi_windup) for `stored_len` input bytes.
-__host__ __device__ ZL_COLD inline int flush_block_bytes(Trees& t, int stored_len) {
+// _tr_flush_block for one block of `stored_len` input bytes: adds its bits to `bits` (the
+// stream's bit count so far; a stored block pads to a byte first) and, for the last block, the
+// final bi_windup.  Leaves the block statistics for init_block to reset.
+__host__ __device__ ZL_COLD inline void flush_block(Trees& t, int stored_len, bool last, int64_t& bits) {
     const int lmax = build_tree(t, T_LIT);
     const int dmax = build_tree(t, T_DIST);
     scan_tree(t, t.ldl, lmax);
@@ -246,9 +253,23 @@ __host__ __device__ ZL_COLD inline int flush_block_bytes(Trees& t, int stored_le
     const int64_t dyn_b = (t.opt_len + 3 + 7) >> 3;
     const int64_t static_b = (t.static_len + 3 + 7) >> 3;
     const int64_t opt_b = static_b <= dyn_b ? static_b : dyn_b;
-    if ((int64_t)stored_len + 4 <= opt_b) return stored_len + 5;  // stored: 3 bits + windup + LEN/NLEN
-    if (static_b == opt_b) return (int)static_b;                   // fixed trees
-    return (int)dyn_b;                                             // dynamic trees
+    if ((int64_t)stored_len + 4 <= opt_b) {  // stored: header, bi_windup, LEN, NLEN, the bytes
+        bits = ((bits + 3 + 7) & ~(int64_t)7) + 32 + 8 * (int64_t)stored_len;
+    } else if (static_b == opt_b) {  // fixed trees
+        bits += 3 + t.static_len;
+    } else {  // dynamic trees (opt_len includes the tree description)
+        bits += 3 + t.opt_len;
+    }
+    if (last) bits = (bits + 7) & ~(int64_t)7;
+}
+
+// init_block: empty statistics, END_BLOCK counted once.
+__host__ __device__ inline void init_block(Trees& t) {
+    for (int i = 0; i < L_CODES; i++) t.lfc[i] = 0;
+    for (int i = 0; i < D_CODES; i++) t.dfc[i] = 0;
+    for (int i = 0; i < BL_CODES; i++) t.bfc[i] = 0;
+    t.lfc[END_BLOCK] = 1;
+    t.opt_len = t.static_len = 0;
 }
 
 // longest_match (deflate.c) for the current position.
@@ -299,11 +320,10 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
     }
     for (int i = 0; i < MAX_MATCH + 2; i++) win[n + i] = 0;  // fill_window's WIN_INIT zeroing
 
-    for (int i = 0; i < L_CODES; i++) t.lfc[i] = 0;
-    for (int i = 0; i < D_CODES; i++) t.dfc[i] = 0;
-    for (int i = 0; i < BL_CODES; i++) t.bfc[i] = 0;
-    t.lfc[END_BLOCK] = 1;
-    t.opt_len = t.static_len = 0;
+    init_block(t);
+    int64_t bits = 0;        // deflate stream bits so far (after the 2-byte zlib header)
+    int block_start = 0;     // first input byte of the open block
+    int last_lit = 0;        // symbols buffered in the open block (_tr_tally's s->last_lit)
 
     uint32_t ins_h = 0;
     if (n >= MIN_MATCH) ins_h = (((uint32_t)win[0] << HASH_SHIFT) ^ win[1]) & HASH_MASK;
@@ -317,10 +337,21 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
         z.head[ins_h] = (uint16_t)str;
         return head;
     };
-    auto tally_lit = [&](int c) { t.lfc[c]++; };
-    auto tally_dist = [&](int dist, int lc) {
+    // _tr_tally: true when the symbol buffer is full (a block must be flushed)
+    auto tally_lit = [&](int c) -> bool {
+        t.lfc[c]++;
+        return ++last_lit == LIT_BUFSIZE - 1;
+    };
+    auto tally_dist = [&](int dist, int lc) -> bool {
         t.lfc[length_code(lc) + LITERALS + 1]++;
         t.dfc[dist_code(dist - 1)]++;
+        return ++last_lit == LIT_BUFSIZE - 1;
+    };
+    auto flush = [&](bool last) {  // FLUSH_BLOCK_ONLY
+        flush_block(t, strstart - block_start, last, bits);
+        block_start = strstart;
+        init_block(t);
+        last_lit = 0;
     };
 
     while (lookahead != 0) {
@@ -336,7 +367,7 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
         }
         if (prev_length >= MIN_MATCH && match_length <= prev_length) {
             const int max_insert = strstart + lookahead - MIN_MATCH;
-            tally_dist(strstart - 1 - prev_match, prev_length - MIN_MATCH);
+            const bool bflush = tally_dist(strstart - 1 - prev_match, prev_length - MIN_MATCH);
             lookahead -= prev_length - 1;
             prev_length -= 2;
             do {
@@ -345,8 +376,9 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
             match_available = false;
             match_length = MIN_MATCH - 1;
             strstart++;
+            if (bflush) flush(false);
         } else if (match_available) {
-            tally_lit(win[strstart - 1]);
+            if (tally_lit(win[strstart - 1])) flush(false);
             strstart++;
             lookahead--;
         } else {
@@ -356,6 +388,7 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
         }
     }
     if (match_available) tally_lit(win[strstart - 1]);
+    flush(true);
 
     // leave head[] all zero for the next stream
     if (n >= MIN_MATCH) {
@@ -365,7 +398,7 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
             z.head[h] = 0;
         }
     }
-    return 2 + flush_block_bytes(t, n) + 4;
+    return 2 + (int)(bits >> 3) + 4;
 }
 
 }  // namespace zl

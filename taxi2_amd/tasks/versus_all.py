@@ -87,6 +87,13 @@ class VersusAll:
         self.params.engine.stream = None
         self.params.engine.dense_limit = 4 << 30
         self.params.engine.block_bytes = 256 << 20
+        # reductions instead of (or beside) the N x N text: write_summary False skips summary.tsv
+        # (the reference always writes it); row_minima = a metric label gathers, per sequence, the
+        # closest other sequence by that metric (first minimum, None skipped) into
+        # task.row_minima = (index, value) and distances/row_minima.tsv (streamed path)
+        self.params.engine.write_summary = True
+        self.params.engine.row_minima = None
+        self.row_minima = None
 
         self.distances: np.ndarray | None = None  # (N, N, M) after start(), NaN = None
 
@@ -315,6 +322,9 @@ class VersusAll:
 
     def write_summary(self, seqs: list, A: np.ndarray):
         from .subsets import write_summary
+
+        if not self.params.engine.write_summary:
+            return
 
         write_summary(self.paths.summary, seqs, A, self.params.distances.metrics, self.input.genera,
                       self.input.species, self.params.format.float, self.params.format.missing,
@@ -550,12 +560,23 @@ class _BlockWriters:
         gcode = subset_codes(self.ids, genera)[0] if genera else np.zeros(n, np.int32)
         scode = subset_codes(self.ids, species)[0] if species else np.zeros(n, np.int32)
         self.codes = np.stack([gcode, scode], axis=1)
-        create_parents(task.paths.summary)
-        self.summ = open(task.paths.summary, "wb")
-        head = ["seqid (query 1)", "seqid (query 2)", *[str(m) for m in self.metrics],
-                *[k + " (query 1)" for k in ex0], *[k + " (query 2)" for k in ex0],
-                "genus (query 1)", "species (query 1)", "genus (query 2)", "species (query 2)", "comparison_type"]
-        self.summ.write(("\t".join(head) + "\n").encode("utf-8"))
+        self.summ = None
+        if p.engine.write_summary:
+            create_parents(task.paths.summary)
+            self.summ = open(task.paths.summary, "wb")
+            head = ["seqid (query 1)", "seqid (query 2)", *[str(m) for m in self.metrics],
+                    *[k + " (query 1)" for k in ex0], *[k + " (query 2)" for k in ex0],
+                    "genus (query 1)", "species (query 1)", "genus (query 2)", "species (query 2)",
+                    "comparison_type"]
+            self.summ.write(("\t".join(head) + "\n").encode("utf-8"))
+        self.rmin_k = None
+        if p.engine.row_minima is not None:
+            labels = [str(m) for m in self.metrics]
+            if str(p.engine.row_minima) not in labels:
+                raise ValueError(f"row_minima metric {p.engine.row_minima} is not one of {labels}")
+            self.rmin_k = labels.index(str(p.engine.row_minima))
+            self.rmin_idx = np.full(n, -1, dtype=np.int64)
+            self.rmin_d = np.full(n, np.nan)
         self.aggs = [(name, SubsetAggregatorDev(eng, self.ids, part, len(self.metrics)))
                      for part, name in ((genera, "genera"), (species, "species")) if part]
         self.pairs_fh = None
@@ -584,6 +605,13 @@ class _BlockWriters:
                 D[i - x0, cols] = float("nan")
         for _, agg in self.aggs:
             agg.add(D, x0, x1)
+        if self.rmin_k is not None:  # first minimum over defined values (-0.0 == 0.0), None skipped
+            v = D[:, :, self.rmin_k]
+            v = torch.where(torch.isfinite(v), v, torch.full_like(v, float("inf")))
+            d, idx = torch.min(v, dim=1)
+            ok = torch.isfinite(d)
+            self.rmin_idx[x0:x1] = torch.where(ok, idx, torch.full_like(idx, -1)).cpu().numpy()
+            self.rmin_d[x0:x1] = torch.where(ok, d, torch.full_like(d, float("nan"))).cpu().numpy()
         A = D.cpu().numpy()
         seqs, ids = self.seqs, self.ids
         if self.pairs_fh is not None:
@@ -612,6 +640,8 @@ class _BlockWriters:
                     text = format_values(Am, self.fmt, self.missing)
                     for i in range(x1 - x0):
                         fh.write(("\t".join((ids[x0 + i], *text[i])) + "\n").encode("utf-8"))
+        if self.summ is None:
+            return
         if ok:
             from .subsets import SUMMARY_CHUNK_VALUES
 
@@ -634,6 +664,16 @@ class _BlockWriters:
         for fh in [self.lin, self.summ, *(self.mats or [])]:
             if fh is not None:
                 fh.close()
+        if self.rmin_k is not None:
+            self.task.row_minima = (self.rmin_idx, self.rmin_d)
+            path = self.task.paths.distances_linear.parent / "row_minima.tsv"
+            create_parents(path)
+            fmt, missing = self.fmt, self.missing
+            with open(path, "w") as fh:
+                fh.write(f"seqid\tclosest\t{self.metrics[self.rmin_k]}\n")
+                for i, (j, d) in enumerate(zip(self.rmin_idx, self.rmin_d)):
+                    fh.write(f"{self.ids[i]}\t{self.ids[j] if j >= 0 else missing}\t"
+                             f"{fmt.format(float(d)) if np.isfinite(d) else missing}\n")
         if self.pairs_fh is not None:
             self.pairs_fh.close()
         p = self.task.params

@@ -168,3 +168,38 @@ def test_scratch_regrowth_interleaved(engine):
         assert engine.zlib_lengths(st, idx).tolist() == [len(zlib.compress(seqs[i].encode())) for i in idx]
         assert engine.format_rows(vals, ["a", "b"], None, decimals=2).decode() == "a\t0.50\tNA\nb\t1.25\t-0.00\n"
     st.free()
+
+
+def test_zlib_lengths_multi_block(engine):
+    """Concatenations of 10-32 kB (several deflate blocks, one window) against Python's zlib."""
+    rng = random.Random(23)
+    seqs = ["".join(rng.choice("ACGT") for _ in range(L)) for L in (9000, 10000, 12000, 16383, 20000, 32000)]
+    seqs += ["".join(rng.choice("ACGTN-") for _ in range(11000)), "ACGT" * 4000]
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    got1 = engine.zlib_lengths(st, np.arange(n))
+    assert got1.tolist() == [len(zlib.compress(s.upper().encode())) for s in seqs]
+    xs = np.array([0, 1, 2, 3, 6, 7, 1, 4])
+    ys = np.array([1, 0, 3, 2, 0, 6, 6, 5])
+    got2 = engine.zlib_lengths(st, xs, st, ys)
+    assert got2.tolist() == [len(zlib.compress((seqs[a] + seqs[b]).upper().encode())) for a, b in zip(xs, ys)]
+    st.free()
+
+
+def test_ncd_aligned_long_sequences(engine):
+    """NCD on the aligned strings of 9 000-10 000 bp pairs: ~20 kB concatenations (multi-block), from
+    the column-tiled aligner's strings, against Python's zlib on those same strings."""
+    from oracle import restatement as R
+
+    fam = family_sequences(3, 10000, 0x56, ancestors=1, max_sub=0.1, indel_rate=0.01)
+    seqs = [fam[0], fam[1][:9000], fam[2]]
+    st = engine.upload(seqs, align=True)
+    xs, ys = np.array([0, 1, 2]), np.array([1, 2, 0])
+    got = engine.ncd_pairs(st, st, xs, ys, DEFAULT, aligned=True, both=True)
+    strings = engine.align_strings(st, st, xs, ys, DEFAULT, both=True)
+    for k, pair in enumerate(strings):
+        (ax, ay), (bx, by) = pair
+        assert len(ax) + len(ay) > 16383
+        assert got[k, 0] == R.ncd(ax, ay)
+        assert got[k, 1] == R.ncd(by, bx)
+    st.free()

@@ -196,3 +196,53 @@ def test_streamed_task_two_ranks(tmp_path, engine, backend):
     assert files and files == _files(tmp_path / "dist")
     for f in files:
         assert (tmp_path / "dist" / f).read_bytes() == (tmp_path / "single" / f).read_bytes(), f
+
+
+def test_streamed_reductions_only(tmp_path, engine):
+    """Reductions without the N x N text (config 5's "gather only reductions" mode): per-row minima
+    and the subset aggregates, with linear / matricial / summary / aligned-pairs output off."""
+    ns: dict = {}
+    exec(TASK.format(root=str(ROOT)), ns)
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.partitions import Partition
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    raw = random_sequences(14, 60, 300, 91, "ACGTN", n_rate=0.02)
+    raw = raw + mutate(raw[:6], 92, rate=0.05) + [raw[3]]
+    seqs = Sequences([Sequence(f"s{k}", s) for k, s in enumerate(raw)])
+    part = Partition({f"s{k}": "g%d" % (k % 3) for k in range(len(raw))})
+
+    def task(out, stream):
+        t = VersusAll()
+        t.engine, t.progress_handler, t.work_dir = engine, None, out
+        t.input.sequences = seqs
+        t.input.genera = part
+        t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.Kimura2P()]
+        t.params.engine.stream = stream
+        t.params.engine.block_bytes = 4 * len(raw) * 8 * 8
+        if stream:
+            t.params.engine.row_minima = "k2p"
+            t.params.engine.write_summary = False
+            t.params.distances.write_linear = False
+            t.params.distances.write_matricial = False
+            t.params.pairs.write = False
+        t.start()
+        return t
+
+    dense = task(tmp_path / "dense", False)
+    red = task(tmp_path / "red", True)
+    D = dense.distances[:, :, 1]
+    for i in range(len(raw)):
+        row = np.where(np.isfinite(D[i]), D[i], np.inf)
+        j = int(np.argmin(row))
+        if not np.isfinite(row[j]):
+            assert red.row_minima[0][i] == -1
+        else:
+            assert red.row_minima[0][i] == j and red.row_minima[1][i] == row[j]
+    assert not (tmp_path / "red" / "summary.tsv").exists()
+    assert not (tmp_path / "red" / "distances" / "linear.tsv").exists()
+    assert (tmp_path / "red" / "distances" / "row_minima.tsv").read_text().count("\n") == len(raw) + 1
+    for f in sorted((tmp_path / "dense" / "subsets").rglob("*.tsv")):
+        rel = f.relative_to(tmp_path / "dense")
+        assert (tmp_path / "red" / rel).read_bytes() == f.read_bytes(), rel

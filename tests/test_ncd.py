@@ -63,7 +63,31 @@ def test_deflate_len_block_limit(zlen_host):
     big = bytes(random.Random(3).choice(b"ACGT") for _ in range(16382))
     assert zlen_host(big) == len(zlib.compress(big))
     assert zlen_host(big[:16381], b"G") == len(zlib.compress(big[:16381] + b"G"))
-    assert zlen_host(big + b"A") == -1  # more than one deflate block: refused, not approximated
+
+
+def _multi_block_inputs():
+    """Inputs of 16 383 to 65 273 bytes: several deflate blocks (a block holds 16 383 symbols),
+    random (one symbol per byte: blocks of exactly 16 383 bytes), DNA-like, low-entropy (long
+    matches: blocks of many more bytes), binary (stored blocks), and aligned-string-like gappy text."""
+    rng = random.Random(17)
+    dna = bytes(rng.choice(b"ACGT") for _ in range(65273))
+    rnd = bytes(rng.randrange(256) for _ in range(65273))
+    rep = (dna[:97] * 700)[:65273]
+    mut = bytearray(rep)
+    for i in range(0, len(mut), 53):
+        mut[i] = rng.choice(b"ACGT-")
+    gappy = bytes(c if rng.random() > 0.05 else ord("-") for c in dna)
+    for src in (dna, rnd, bytes(mut), gappy):
+        for L in (16383, 16384, 16385, 20000, 32768, 32769, 40000, 49149, 49150, 65273):
+            yield src[:L]
+
+
+def test_deflate_len_multi_block(zlen_host):
+    bad = [len(x) for x in _multi_block_inputs() if zlen_host(x) != len(zlib.compress(x.upper()))]
+    assert not bad, bad[:10]
+    a = bytes(random.Random(5).choice(b"ACGT-") for _ in range(21000))
+    assert zlen_host(a[:10500], a[10500:]) == len(zlib.compress(a))  # a 21 kB aligned-string concatenation
+    assert zlen_host(b"A" * 65274) == -1  # past one window: refused, not approximated
 
 
 def test_oracle_ncd_formula():

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Long sequences (1 025 - 2 048 bp): the packed trace-and-walk aligner (k_alignt2<8,4>) against
-the forward-carry kernels (TAXI2_NO_ALIGNT=1) on the config-3 generator, same pairs, outputs
-compared bit for bit.  Prints one JSON line per length.
+"""Long sequences: the default dispatch (packed trace-and-walk up to 2 048 columns, forward-carry
+k_align1c to 4 095 bp, column-tiled k_alignlong beyond) against the forward-carry kernels
+(TAXI2_NO_ALIGNT=1, <= 4 095 bp) and the column-tiled aligner forced (TAXI2_LONG=1), on the
+config-3 generator, same pairs, outputs compared bit for bit.  One JSON line per length.
 
 usage: python tools/bench_long.py [--lens 1200 1500 2000] [--batch 16384] [--nseq 4000]
 """
@@ -60,17 +61,23 @@ def main() -> None:
         buf, offs = family_packed(args.nseq, L, 0x7A12)
         st = eng.upload_packed(buf, offs, align=True)
         B = args.batch
-        outs, times = [], []
-        for env in ({}, {"TAXI2_NO_ALIGNT": "1"}):
+        outs, times = {}, {}
+        envs = {"default": {}, "tiled": {"TAXI2_LONG": "1"}}
+        if L <= 4095:
+            envs["forward_carry"] = {"TAXI2_NO_ALIGNT": "1"}
+        for name, env in envs.items():
             out = torch.empty((B, 2, 4), dtype=torch.float64, device="cuda")
             sc = torch.empty((B,), dtype=torch.int32, device="cuda")
-            times.append(run(eng, st, 0, B, env, out, sc))
-            outs.append((out.cpu().numpy(), sc.cpu().numpy()))
-        same = bool(np.array_equal(np.nan_to_num(outs[0][0], nan=9.0), np.nan_to_num(outs[1][0], nan=9.0))
-                    and np.array_equal(outs[0][1], outs[1][1]))
-        print(json.dumps({"len": L, "pairs": B, "trace_walk_pairs_per_s": B / times[0],
-                          "forward_carry_pairs_per_s": B / times[1], "speedup": times[1] / times[0],
-                          "gcups_trace_walk": B * L * L / times[0] / 1e9, "identical": same}), flush=True)
+            times[name] = run(eng, st, 0, B, env, out, sc)
+            outs[name] = (out.cpu().numpy(), sc.cpu().numpy())
+        ref = outs["default"]
+        same = all(bool(np.array_equal(np.nan_to_num(o[0], nan=9.0), np.nan_to_num(ref[0], nan=9.0))
+                        and np.array_equal(o[1], ref[1])) for o in outs.values())
+        rec = {"len": L, "pairs": B, "identical": same}
+        for name, t in times.items():
+            rec[f"{name}_pairs_per_s"] = B / t
+            rec[f"{name}_gcups"] = B * L * L / t / 1e9
+        print(json.dumps(rec), flush=True)
         st.free()
 
 
