@@ -72,12 +72,29 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 #endif
 constexpr int AT2_CHUNK = TAXI2_AT2_CHUNK;  // pairs per cursor step (both streams): 2 AT2_CHUNK walks per walker wave
 constexpr int NEG16 = -16384;
-constexpr uint32_t NEG16X2 = 0xC000C000u;
+// Cells are stored BIASED: each 16-bit half holds v + 32768 (unsigned, never wrapping under
+// at_fits16).  Maxima are then unsigned (v_pk_max_u16), differences of two cells are the signed
+// differences (the bias cancels), and adding a constant pair (c_hi, c_lo) to both halves at once is
+// ONE 32-bit v_add_u32 of the integer c_hi * 65536 + c_lo: no half leaves [0, 65535], so no carry
+// crosses between the halves.  v_add_u32 issues in 2.28 SIMD cycles, v_pk_add_u16 in 4.09
+// (profiles/r2/valu_peak.txt).
+constexpr int BIAS16 = 32768;
+constexpr uint32_t NEG16X2 = 0x40004000u;  // -16384 + 32768 in both halves
 
 __device__ __forceinline__ at_s2 as_s2(uint32_t v) { return __builtin_bit_cast(at_s2, v); }
 __device__ __forceinline__ uint32_t as_u32(at_s2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ at_s2 pmax(at_s2 a, at_s2 b) { return __builtin_elementwise_max(a, b); }
+typedef unsigned short at_u2 __attribute__((ext_vector_type(2)));
+// maximum of biased cells: unsigned per half
+__device__ __forceinline__ at_s2 pmax(at_s2 a, at_s2 b) {
+    return __builtin_bit_cast(at_s2, __builtin_elementwise_max(__builtin_bit_cast(at_u2, a), __builtin_bit_cast(at_u2, b)));
+}
 __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16); }
+// a biased cell pair from two unbiased values
+__device__ __forceinline__ uint32_t pk2b(int lo, int hi) { return pk2(lo + BIAS16, hi + BIAS16); }
+// the integer c_hi * 65536 + c_lo of a packed pair of signed 16-bit constants (what a v_add_u32 adds)
+__host__ __device__ __forceinline__ uint32_t pk_int(uint32_t packed) { return packed - ((packed & 0x8000u) << 1); }
+// biased cells + a constant pair given as pk_int: both halves in one 32-bit add
+__device__ __forceinline__ at_s2 padd32(at_s2 a, uint32_t c) { return __builtin_bit_cast(at_s2, __builtin_bit_cast(uint32_t, a) + c); }
 // per half clamp to [-1, 1] (the compiler would expand it into compares and selects)
 __device__ __forceinline__ at_s2 psign(at_s2 d) {
     uint32_t r;
@@ -88,12 +105,6 @@ __device__ __forceinline__ at_s2 psign(at_s2 d) {
 __device__ __forceinline__ at_s2 pclamp21(at_s2 d) {
     uint32_t r;
     asm("v_pk_max_i16 %0, %1, -2 op_sel_hi:[1,0]\n\tv_pk_min_i16 %0, %0, 1 op_sel_hi:[1,0]" : "=&v"(r) : "v"(as_u32(d)));
-    return as_s2(r);
-}
-// per half a + (low half of b) (b holds one 16-bit constant for both pairs)
-__device__ __forceinline__ at_s2 padd_lo(at_s2 a, uint32_t b) {
-    uint32_t r;
-    asm("v_pk_add_u16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(as_u32(a)), "v"(b));
     return as_s2(r);
 }
 // per half a * 4 + b
@@ -152,7 +163,7 @@ __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab
     const uint32_t w0 = a2_row_word(tab, n, 0, rows0, g, i0);
     const uint32_t w1 = a2_row_word(tab, n, 1, rows1, g, i1);
     // boundary in the fill's representation: odd F (2 Ix(i, 0) + 1), drift -i dz (see the cell)
-    return make_uint2(w0 | (w1 << 16), pk2(sc.eo + sc.ee * (i0 - 1) - i0 * dz + 1, sc.eo + sc.ee * (i1 - 1) - i1 * dz + 1));
+    return make_uint2(w0 | (w1 << 16), pk2b(sc.eo + sc.ee * (i0 - 1) - i0 * dz + 1, sc.eo + sc.ee * (i1 - 1) - i1 * dz + 1));
 }
 
 template <int K, int W, bool DEF, int OCC>
@@ -176,8 +187,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     __shared__ uint32_t fin_n[2];
     __shared__ AtChain chs[2];
     __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * RING];
-    __shared__ uint16_t colc[K][NT];            // Ix open (end-gap score on column nB)
-    __shared__ uint16_t colx[DEF ? 1 : K][NT];  // Ix extend (non-default scores)
+    __shared__ uint32_t colc[K][NT];            // Ix open (end-gap score on column nB), as pk_int
+    __shared__ uint32_t colx[DEF ? 1 : K][NT];  // Ix extend (non-default scores), as pk_int
     __shared__ uint32_t eqt[4][NT][KW];         // 16-bit substitution score fields by row base
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows[2];
@@ -473,8 +484,9 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                         const int s = ((j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi) - 2 * dz;
                         ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
                     }
-                    colc[k][tid] = (uint16_t)(((j == nB) ? sc.eo : sc.io) - dz);
-                    if (!DEF) colx[DEF ? 0 : k][tid] = (uint16_t)((j == nB) ? sc.ee : sc.ie);
+                    const int oc = ((j == nB) ? sc.eo : sc.io) - dz, ec = (j == nB) ? sc.ee : sc.ie;
+                    colc[k][tid] = pk_int(pk2(oc, oc));
+                    if (!DEF) colx[DEF ? 0 : k][tid] = pk_int(pk2(ec, ec));
                 }
     #pragma unroll
                 for (int r = 0; r < 4; ++r)
@@ -489,7 +501,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int g0 = sc.eo + sc.ee * (j0 + k - 1) - (j0 + k) * dz;
-                stG[k] = pk2(g0, g0);
+                stG[k] = pk2b(g0, g0);
                 stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
             }
             uint32_t payF = NEG16X2 | 0x00010001u, payY = NEG16X2;
@@ -535,12 +547,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     #pragma unroll
                                     for (int k = 0; k < K; ++k) {
                                         const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
-                                        stG[k] = (pk2(g0, g0) & m) | (stG[k] & ~m);
+                                        stG[k] = (pk2b(g0, g0) & m) | (stG[k] & ~m);
                                         stX[k] = ((NEG16X2 | 0x00010001u) & m) | (stX[k] & ~m);
                                     }
                                     // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
                                     const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1) - jb * dz) | 1;
-                                    carry = (pk2(c0, c0) & m) | (carry & ~m);
+                                    carry = (pk2b(c0, c0) & m) | (carry & ~m);
                                 }
                                 // substitution words of both rows
                                 uint32_t eq0[KW], eq1[KW];
@@ -583,6 +595,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
                                                         : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
                                                                  (at_s2){(short)sc.ie, (short)sc.ie});
+                                const uint32_t oy1i = pk_int(oy1), eyi = pk_int(ey);
                                 // Representation (doubled scores): G = max(M, Iy) tagged (M odd, Iy even);
                                 // Ix and F = max(M, Ix) kept ODD (2v + 1, no tag): then the diagonal
                                 // max(G, Ix) | 1 = max(G | 1, X1) needs no fix-up, Ix candidates built on G | 1
@@ -599,11 +612,13 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     const at_s2 nd1 = pmax(G1, X1);
                                     const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
                                     const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-                                    const at_s2 M = d1 + sM;
-                                    const at_s2 cg = padd_lo(G1, colc[k][tid]);
-                                    const at_s2 cx = DEF ? X1 : padd_lo(X1, colx[DEF ? 0 : k][tid]);  // drift: + ie - dz = 0
+                                    // default scores: both substitution halves are >= 0 (drift), so M is one
+                                    // 32-bit add too; other scores may subtract: per-half add
+                                    const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;
+                                    const at_s2 cg = padd32(G1, colc[k][tid]);
+                                    const at_s2 cx = DEF ? X1 : padd32(X1, colx[DEF ? 0 : k][tid]);  // drift: + ie - dz = 0
                                     const at_s2 Xn1 = pmax(cg, cx);
-                                    const at_s2 cf = F1 + as_s2(oy1), cy = DEF ? Y : Y + as_s2(ey);
+                                    const at_s2 cf = padd32(F1, oy1i), cy = DEF ? Y : padd32(Y, eyi);
                                     const at_s2 Yn = pmax(cf, cy);
                                     const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
                                     const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
@@ -655,9 +670,11 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     }
                                     const at_s2 e = pmax(as_s2(eG), as_s2(eX));
                                     if (rw & (A2_LAST | (A2_LAST << 16))) AT_DIAG(3, 1);
-                                    if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, AG_FIN)) fin[cur][2 * fin_n[0]++] = (int)e.x;
+                                    const uint32_t eu = as_u32(e);  // unbias the final cells
+                                    if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, AG_FIN))
+                                        fin[cur][2 * fin_n[0]++] = (int)(eu & 0xFFFFu) - BIAS16;
                                     if ((rw & (A2_LAST << 16)) && AT_OK(2 * fin_n[1] + 1 < AT2_CHUNK, AG_FIN))
-                                        fin[cur][2 * fin_n[1]++ + 1] = (int)e.y;
+                                        fin[cur][2 * fin_n[1]++ + 1] = (int)(eu >> 16) - BIAS16;
                                 }
                             }
                             carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1
