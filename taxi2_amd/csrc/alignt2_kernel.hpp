@@ -79,6 +79,7 @@ constexpr int NEG16 = -16384;
 // crosses between the halves.  v_add_u32 issues in 2.28 SIMD cycles, v_pk_add_u16 in 4.09
 // (profiles/r2/valu_peak.txt).
 constexpr int BIAS16 = 32768;
+constexpr int AT_ESC = AT_DONE + 1;  // walk state: stepped outside the stored trace band
 constexpr uint32_t NEG16X2 = 0x40004000u;  // -16384 + 32768 in both halves
 
 __device__ __forceinline__ at_s2 as_s2(uint32_t v) { return __builtin_bit_cast(at_s2, v); }
@@ -113,6 +114,12 @@ __device__ __forceinline__ at_s2 pmad4(at_s2 a, at_s2 b) {
     asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)));
     return as_s2(r);
 }
+// per half a * 16 + b
+__device__ __forceinline__ uint32_t pmad16(at_s2 a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, 16, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(as_u32(a)), "v"(b));
+    return r;
+}
 
 // Host: do all differences of the packed fill fit int16?
 __host__ __device__ inline bool at_fits16(const KScores& k, int max_len) {
@@ -133,16 +140,16 @@ __device__ __forceinline__ uint32_t a2_load_byte(const uint8_t* p) { return *(a2
 __device__ __forceinline__ uint32_t a2_load_trace(const uint8_t* p) { return *(const volatile a2_gbyte*)p; }
 
 // Row records.  One 8-byte LDS entry per step row g holds both streams: .x = two 16-bit row
-// words (stream 0 low, stream 1 high), .y = the packed column-0 boundary Ix(i, 0) = eo + ee (i-1)
-// of both rows (what wave 0's lane 0 receives from the left).  Row word bits: 0-7 the row byte,
-// 8 first row of its pair, 9 last row, 10 no row, 11-12 "ACGT" code of an exact A/C/G/T byte,
-// 13 any other byte (byte-compare substitution path).  The chain pairs of stream `st` are
-// tab[st], tab[st + 2], ...
+// words (stream 0 low, stream 1 high), .y = the trace band of the row (below).  Row word bits:
+// 0-7 the row byte, 8 first row of its pair, 9 last row, 10 no row, 11-12 "ACGT" code of an
+// exact A/C/G/T byte, 13 any other byte (byte-compare substitution path).  The chain pairs of
+// stream `st` are tab[st], tab[st + 2], ...
 constexpr uint32_t A2_FIRST = 1u << 8, A2_LAST = 1u << 9, A2_NONE = 1u << 10, A2_OTHER = 1u << 13;
 
 __device__ __forceinline__ uint32_t a2_row_word(const ChainPair* __restrict__ tab, int n, int st, int rows, int g,
-                                                int& irow) {
+                                                int& irow, int& nA) {
     irow = 0;
+    nA = 0;
     if (g >= rows) return A2_NONE;
     int k = st;
     for (int t = st + 2; t < n; t += 2)
@@ -155,22 +162,57 @@ __device__ __forceinline__ uint32_t a2_row_word(const ChainPair* __restrict__ ta
     if (i == 0) v |= A2_FIRST;
     if (i == cp.nA - 1) v |= A2_LAST;
     irow = i + 1;
+    nA = cp.nA;
     return v;
 }
+
+// Trace band.  The fill stores the trace bytes of row i (1-based) of a pair only for the column
+// blocks (K columns, one lane) that meet the diagonal strip
+//   j - i  in  [min(0, nB - nA) - band, max(0, nB - nA) + band]
+// (band <= 0: every block).  The strip holds both corners, so a first path that stays inside it
+// is walked from stored bytes alone; a walk that would step outside stops and its pair is queued
+// for a second launch with the full trace (k_alignt2's esc_* arguments), so results never depend
+// on the band.  Blocks [lo, hi] of row i; lo > hi: none.
+__host__ __device__ __forceinline__ void a2_band_blocks(int i, int nA, int nB, int band, int K, int& lo, int& hi) {
+    if (band <= 0) {
+        lo = 0;
+        hi = (nB - 1) / K;
+        return;
+    }
+    const int dl = min(0, nB - nA) - band, dh = max(0, nB - nA) + band;
+    lo = (max(1, i + dl) - 1) / K;
+    hi = (min(nB, i + dh) - 1) / K;
+}
+// .y of a row record: the union of both streams' block ranges as lo | (hi - lo) << 16, tested by a
+// fill lane with ONE 16-bit subtract and compare ((u16)(t - lo) <= hi - lo); no row: lo = 0x8000
 __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab, int n, int rows0, int rows1, int g,
-                                               const KScores& sc, int dz) {
-    int i0, i1;
-    const uint32_t w0 = a2_row_word(tab, n, 0, rows0, g, i0);
-    const uint32_t w1 = a2_row_word(tab, n, 1, rows1, g, i1);
-    // boundary in the fill's representation: odd F (2 Ix(i, 0) + 1), drift -i dz (see the cell)
-    return make_uint2(w0 | (w1 << 16), pk2b(sc.eo + sc.ee * (i0 - 1) - i0 * dz + 1, sc.eo + sc.ee * (i1 - 1) - i1 * dz + 1));
+                                               int nB, int band, int K) {
+    int i0, i1, a0, a1;
+    const uint32_t w0 = a2_row_word(tab, n, 0, rows0, g, i0, a0);
+    const uint32_t w1 = a2_row_word(tab, n, 1, rows1, g, i1, a1);
+    int lo = 0x7FFF, hi = -1;
+    if (i0 > 0) {
+        int l, h;
+        a2_band_blocks(i0, a0, nB, band, K, l, h);
+        lo = min(lo, l);
+        hi = max(hi, h);
+    }
+    if (i1 > 0) {
+        int l, h;
+        a2_band_blocks(i1, a1, nB, band, K, l, h);
+        lo = min(lo, l);
+        hi = max(hi, h);
+    }
+    const uint32_t y = hi < lo ? 0x8000u : (uint32_t)lo | ((uint32_t)(hi - lo) << 16);
+    return make_uint2(w0 | (w1 << 16), y);
 }
 
 template <int K, int W, bool DEF, int OCC>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
           double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
-          int cap_rows, int hops, unsigned long long* __restrict__ next) {
+          int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
+          unsigned long long* __restrict__ esc_n) {
     static_assert(K % 2 == 0 && K <= 16, "16-bit score fields: K / 2 words per stream and base");
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
@@ -194,6 +236,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     __shared__ int s_n, s_rows[2];
     __shared__ int s_fill;  // fill waves done with the current interval (cumulative per chain)
     __shared__ AtWalk wks[2 * AT2_CHUNK];
+    __shared__ int escf[2][AT2_CHUNK];  // pair already queued for the full-trace pass
 
 #ifdef TAXI2_GUARD
     at_poison_lds(xinfo, sizeof xinfo);
@@ -206,6 +249,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     at_poison_lds(colx, sizeof colx);
     at_poison_lds(eqt, sizeof eqt);
     at_poison_lds(wks, sizeof wks);
+    at_poison_lds(escf, sizeof escf);
     if (threadIdx.x == 0) s_n = s_rows[0] = s_rows[1] = s_fill = (int)AT_POISON_LDS;
     __syncthreads();
 #endif
@@ -214,7 +258,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring pointers etc. in SGPRs
     const bool walker = w == W;
     const int nm = ms.n;
-    const int64_t total = ps.count;
+    // second pass (ps.sel set): the pairs the band pass queued; *ps.dcount of them, pair p = sel[q]
+    const int64_t total = ps.dcount ? (int64_t)min((unsigned long long)ps.count, *ps.dcount) : ps.count;
     const int64_t chunk = chunk_req >= 1 ? min((int64_t)chunk_req, (int64_t)AT2_CHUNK)
                                          : max((int64_t)1, min((int64_t)AT2_CHUNK, total / ((int64_t)gridDim.x * 8)));
     uint8_t* const bufs = trace + (size_t)blockIdx.x * 2 * (size_t)buf_bytes;
@@ -233,6 +278,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         // indexes tab[] in walk_run; it must not be whatever an earlier kernel left in LDS)
         AtWalk& W_ = wks[lane];
         W_ = AtWalk{0, 0, AT_DONE, 0, 0, 0, 0u, 0u, 0u, 0, 0, 0, 0};
+        if (lane < AT2_CHUNK) escf[pb][lane] = 0;
         if (lane < nw) {
             const int pi = lane < n ? lane : lane - n;
             const ChainPair& cp = tab[pb][pi];
@@ -257,6 +303,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         const AtChain& ch = chs[pb];
         const int fx = cp.fx, lx = cp.lx, fy = ch.fy, ly = ch.ly, r0 = cp.r0, sm = cp.pad;
         const int prio = W_.prio;
+        // the stored strip (a2_band_blocks) holds every cell with nj - ni in [bdl, bdl + bwd]; a walk
+        // stepping onto any other cell stops (AT_ESC) and its pair is queued after the hop loop
+        const int bdl = min(0, ch.nB - cp.nA) - band;
+        const uint32_t bwd = (uint32_t)(abs(ch.nB - cp.nA) + 2 * band);
         const uint8_t* rs = cp.rseq;
         const uint8_t* cs = ch.cseq;
         const uint8_t* tr = bufs + (size_t)pb * (size_t)buf_bytes + sm;
@@ -264,9 +314,9 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
         uint32_t cb = W_.cb, xa = W_.xa, yb = W_.yb;
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
         for (int h = 0; budget < 0 || h < budget; ++h) {
-            if (!__any(st != AT_DONE)) break;
+            if (!__any(st < AT_DONE)) break;
             if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-            if (st == AT_DONE) continue;
+            if (st >= AT_DONE) continue;
             int ni, nj;
             if (st == AT_M) {
                 if (!first) {
@@ -296,7 +346,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 if (out_mode == OUT_BOTH) o = out + (p * 2 + ((prio ^ cp.swp) ? 1 : 0)) * nm;
                 else o = out + p * nm;
                 AT_DIAG(4, 1);
-                if (AT_OK(p >= 0 && p < total, AG_OUT))
+                if (AT_OK(p >= 0 && p < ps.count, AG_OUT))
                 for (int m = 0; m < nm; ++m)
                     o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
                 if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK && fin[pb][pi] != (int)AT_POISON_LDS, AG_FIN))  // undo the drift of cell (nA, nB)
@@ -305,14 +355,18 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 continue;
             }
             uint32_t nb = 0;
+            // stepping outside the stored strip: the byte read below is stale and the walk stops
+            // (no branch here: a divergent exit in the hop loop doubled its code)
+            bool esc = false;
             if (ni >= 1 && nj >= 1) {
+                esc = band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
                 const int t = (nj - 1) / K;
                 const int k = nj - 1 - t * K;
                 const int s = r0 + ni - 1 + (t & 63);
                 const size_t off = ((size_t)s * NT + t) * (2 * K) + 2 * k + sm;
                 if (AT_OK(off < (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace(tr - sm + off);
                 // guard build: the fill of this chain stored every byte the walk reads
-                (void)AT_OK((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87, AG_TRACE_POISON);
+                (void)AT_OK(esc || ((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87), AG_TRACE_POISON);
             }
             xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, AG_ROWSEQ)) ? a2_load_byte(rs + ni - 1) : 0u;
             yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, AG_COLSEQ)) ? a2_load_byte(cs + nj - 1) : 0u;
@@ -350,7 +404,11 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             cb = nb;
             i = ni;
             j = nj;
-            st = nst;
+            st = esc ? AT_ESC : nst;
+        }
+        if (st == AT_ESC) {  // queue the pair (once, whichever orientation stopped) for the full-trace pass
+            if (atomicOr(&escf[pb][pi], 1) == 0 && AT_OK(esc_list != nullptr, AG_OUT)) esc_list[atomicAdd(esc_n, 1ull)] = cp.p;
+            st = AT_DONE;
         }
         if (lane >= 2 * AT2_CHUNK) return;
         W_.i = i;
@@ -386,7 +444,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                     }
                     int64_t q = s_qc;
                     for (; q < s_qend; ++q) {
-                        const int64_t p = q;
+                        const int64_t p = ps.sel ? ps.sel[q] : q;
                         int64_t a, b;
                         decode_pair(ps, p, a, b);
                         const int4 ma = XS.meta[a];
@@ -495,8 +553,8 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
             }
             // rows 0..63, and "no row" for the ring slots read as rows -63..-1 by the lanes the
             // wavefront has not reached yet (overwritten only when row XR-64 is prefetched)
-            if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, sc, dz);
-            else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(A2_NONE | (A2_NONE << 16), 0u);
+            if (tid < 64) xinfo[tid] = a2_row_record(tab[cur], n, rows0, rows1, tid, nB, band, K);
+            else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(A2_NONE | (A2_NONE << 16), 0x8000u);
             uint32_t stG[K], stX[K];
     #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -505,6 +563,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
             }
             uint32_t payF = NEG16X2 | 0x00010001u, payY = NEG16X2;
+            // column-0 boundary of wave 0's lane 0 (row g = s): odd F = 2 Ix(i, 0) + 1 - i dz with
+            // Ix(i, 0) = eo + ee (i - 1); default scores (ee = dz) make it one constant
+            const uint32_t bnd1 = pk2b(sc.eo - dz + 1, sc.eo - dz + 1);
+            uint32_t bnd = bnd1;
             uint32_t carry = 0u;
             const uint2* ring_in = (w > 0 && !IS_W) ? ring + (size_t)(w - 1) * RING : nullptr;
             uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
@@ -520,12 +582,24 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             int ln;
                             asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
                             const int g = s - ln;
+                            // this lane's column block, from the lane id: threadIdx is not kept live
+                            // across the loop (it was spilled and reloaded in the first-row path)
+                            const int tq = w * 64 + ln;
                             const uint2 rec = xinfo[g & (XR - 1)];
+                            // trace band (a2_row_record): store iff (u16)(block - lo) <= hi - lo (covers
+                            // j0 <= nB).  The lane mask is formed here, a whole cell block ahead of the
+                            // store, so the exec-mask update there never waits on the compare.
+                            const bool in_band = (uint16_t)((uint16_t)tq - (uint16_t)rec.y) <= (uint16_t)(rec.y >> 16);
+                            asm volatile("" ::"s"(__builtin_amdgcn_ballot_w64(in_band)));
                             const uint32_t rw = rec.x;
                             (void)AT_OK(rw != AT_POISON_LDS, AG_ROW_POISON);
                             uint32_t inF, inY;
                             if constexpr (decltype(FW)::value) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
-                                inF = shr_old(payF, rec.y);
+                                if constexpr (!DEF) {  // one row on per step; a first row restarts its half
+                                    const uint32_t mf = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
+                                    bnd = (bnd1 & mf) | (as_u32(as_s2(bnd) + (at_s2){(short)sc.ee, (short)sc.ee}) & ~mf);
+                                }
+                                inF = shr_old(payF, bnd);
                                 inY = shr_old(payY, NEG16X2);
                             } else {
                                 const uint2 o = ring_in[(s + 1) & (RING - 1)];
@@ -539,10 +613,10 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                             // is reset by the next first row, and a skip branch cost phi copies of the
                             // whole column state on every step.
                             {
-                                if (tid == 0 && (rw & (A2_FIRST | (A2_FIRST << 16)))) AT_DIAG(5, 1);
+                                if (tq == 0 && (rw & (A2_FIRST | (A2_FIRST << 16)))) AT_DIAG(5, 1);
                                 if (rw & (A2_FIRST | (A2_FIRST << 16))) {  // a new pair starts in a stream
                                     uint32_t m = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
-                                    int jb = tid * K;
+                                    int jb = tq * K;
                                     asm volatile("" : "+v"(jb), "+v"(m));
     #pragma unroll
                                     for (int k = 0; k < K; ++k) {
@@ -559,7 +633,6 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 {
                                     // the per-thread table address is recomputed here (one op) rather
                                     // than kept live across the chain loop (it was spilled to scratch)
-                                    const int tq = w * 64 + ln;
                                     const uint32_t* t0 = eqt[(rw >> 11) & 3u][tq];
                                     const uint32_t* t1 = eqt[(rw >> 27) & 3u][tq];
     #pragma unroll
@@ -615,12 +688,15 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                     // default scores: both substitution halves are >= 0 (drift), so M is one
                                     // 32-bit add too; other scores may subtract: per-half add
                                     const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;
-                                    const at_s2 cg = padd32(G1, colc[k][tid]);
-                                    const at_s2 cx = DEF ? X1 : padd32(X1, colx[DEF ? 0 : k][tid]);  // drift: + ie - dz = 0
+                                    const at_s2 cg = padd32(G1, colc[k][tq]);
+                                    const at_s2 cx = DEF ? X1 : padd32(X1, colx[DEF ? 0 : k][tq]);  // drift: + ie - dz = 0
                                     const at_s2 Xn1 = pmax(cg, cx);
                                     const at_s2 cf = padd32(F1, oy1i), cy = DEF ? Y : padd32(Y, eyi);
                                     const at_s2 Yn = pmax(cf, cy);
                                     const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
+                                    // byte = 16 (4 sc + sb) + 4 sa + tags, built as two multiply-adds: the
+                                    // tags ride in the addend (tagG = bit 0 of Gn; default scores store no
+                                    // tagF, it is implied, see the walker)
                                     const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
                                     const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
                                     uint32_t code;
@@ -641,11 +717,12 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 const at_s2 F = F1;
                                 payF = as_u32(F);
                                 payY = as_u32(Y);
-                                if (j0 <= nB && AT_OK(((size_t)s * NT + tid + 1) * (2 * K) <= (size_t)buf_bytes, AG_STORE)) {
+                                if (in_band &&
+                                    AT_OK(((size_t)s * NT + tq + 1) * (2 * K) <= (size_t)buf_bytes, AG_STORE)) {
                                     // 32-bit offset from the uniform buffer base (one VGPR, saddr store; a
                                     // buffer is at most a few tens of MB)
-                                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tid) * (2u * K)));
-                                    if (tid == 0) AT_DIAG(2, 1);
+                                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tq) * (2u * K)));
+                                    if (tq == 0) AT_DIAG(2, 1);
                                     if constexpr (K == 16) {
                                         ((uint4*)dst)[0] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
                                         ((uint4*)dst)[1] = make_uint4(acc[4], acc[5], acc[6], acc[7]);
@@ -658,7 +735,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                                 }
                                 if constexpr (decltype(HO)::value)
                                     if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
-                                if ((rw & (A2_LAST | (A2_LAST << 16))) && tid == (nB - 1) / K) {  // owner of column nB
+                                if ((rw & (A2_LAST | (A2_LAST << 16))) && tq == (nB - 1) / K) {  // owner of column nB
                                     const int out_k = (nB - 1) % K;
                                     uint32_t eG = stG[0], eX = stX[0];
     #pragma unroll
@@ -702,7 +779,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                     }
                 }
                 const int gpre = (it + 1) * INTERVAL + tid;
-                if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, sc, dz);
+                if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = a2_row_record(tab[cur], n, rows0, rows1, gpre, nB, band, K);
                 if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
                 if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
                 __syncthreads();

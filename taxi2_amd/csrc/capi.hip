@@ -374,18 +374,25 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
 }
 
 // ---------------------------------------------------------------- trace-and-walk variants
+// trace band of the packed kernel (alignt2_kernel.hpp a2_band_blocks) and its escape queue
+struct BandArgs {
+    int band;
+    int64_t* esc_list;
+    unsigned long long* esc_n;
+};
+
 struct VariantT {
     int K, W, occ;
     bool def;
     const void* fn;
     void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int, int, double*,
-                   int32_t*, uint8_t*, int64_t, int, int, unsigned long long*);
+                   int32_t*, uint8_t*, int64_t, int, int, unsigned long long*, BandArgs);
 };
 
 template <int K, int W, bool DEF, int OCC>
 void launch_alignt(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                    int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
-                   unsigned long long* nx) {
+                   unsigned long long* nx, BandArgs) {
     hipLaunchKernelGGL((k_alignt<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
                        hops, nx);
 }
@@ -413,9 +420,9 @@ const VariantT* pick_variantt(const KScores& k, int max_len) {
 template <int K, int W, bool DEF, int OCC>
 void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                     int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
-                    unsigned long long* nx) {
+                    unsigned long long* nx, BandArgs ba) {
     hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
-                       hops, nx);
+                       hops, nx, ba.band, ba.esc_list, ba.esc_n);
 }
 
 const VariantT kAlignT2[] = {
@@ -463,12 +470,41 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
     int hops = 4096;  // per-interval cap; the packed kernel stops at the fill waves' signal
     if (const char* h = getenv("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
-    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 32)) return -1;
+    // Packed kernel: the fill stores only a diagonal strip of each pair's trace (band half-width in
+    // columns: TAXI2_AT_BAND, 0 = everything; default 3 sqrt(max_len), at least 32: wider than the
+    // first paths of synthetic families measured at 200-2 000 bp); walks that leave
+    // it queue their pair and a second launch redoes exactly those pairs with the full trace.
+    int band = 0;
+    if (packed) {
+        band = std::max(32, (int)std::ceil(3.0 * std::sqrt((double)std::max(1, max_len))));
+        if (4 * band >= max_len) band = 0;  // the strip would be most of the row
+        if (const char* e = getenv("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
+    }
+    // d_work: [u64 pad] [u64 pass-1 cursor] [u64 pass-2 cursor] [u64 queue count] [pad] [i64 queue...]
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 64 + (band > 0 ? (size_t)ps.count * 8 : 0))) return -1;
     unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 32, st));
+    unsigned long long* next2 = (unsigned long long*)((char*)ctx->d_work + 16);
+    unsigned long long* esc_n = (unsigned long long*)((char*)ctx->d_work + 24);
+    int64_t* esc_list = (int64_t*)((char*)ctx->d_work + 64);
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 64, st));
     v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), ps, k, ms, chunk, out_mode, d_out,
-             d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next);
+             d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next, BandArgs{band, esc_list, esc_n});
     HIP_TRY(ctx, hipGetLastError());
+    if (band > 0) {  // the queued pairs (usually none: the workgroups exit at once), full trace
+        PairSrc p2 = ps;
+        p2.sel = esc_list;
+        p2.dcount = esc_n;
+        v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), p2, k, ms, chunk, out_mode, d_out,
+                 d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next2, BandArgs{0, nullptr, nullptr});
+        HIP_TRY(ctx, hipGetLastError());
+        if (getenv("TAXI2_AT_BAND_STATS")) {  // diagnostics: queued pairs of this call on stderr
+            unsigned long long q = 0;
+            HIP_TRY(ctx, hipMemcpyAsync(&q, esc_n, sizeof q, hipMemcpyDeviceToHost, st));
+            HIP_TRY(ctx, hipStreamSynchronize(st));
+            fprintf(stderr, "taxi2 band: k_alignt2<%d,%d,%d> band %d: %llu of %lld pairs took the full-trace pass\n",
+                    v.K, v.W, (int)v.def, band, q, (long long)ps.count);
+        }
+    }
     if (shared_release(ctx, st)) return -1;
 #ifdef TAXI2_GUARD
     if (packed) {  // debug build: report (and clear) out-of-range accesses the guards skipped

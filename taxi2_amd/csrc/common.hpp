@@ -35,6 +35,10 @@ struct PairSrc {
     int64_t R;  // RECT: reference count (g = q * R + r)
     const int64_t* la;  // LIST
     const int64_t* lb;
+    // k_alignt2's second pass only: the launch covers the queued pairs sel[0 .. *dcount) (indices
+    // into this source's own pairs, outputs at those indices)
+    const int64_t* sel = nullptr;
+    const unsigned long long* dcount = nullptr;
 };
 
 struct KScores {
