@@ -207,12 +207,12 @@ __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab
     return make_uint2(w0 | (w1 << 16), y);
 }
 
-template <int K, int W, bool DEF, int OCC>
-__global__ void __launch_bounds__(64 * (W + 1), OCC)
-k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
-          double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
-          int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
-          unsigned long long* __restrict__ esc_n) {
+template <int K, int W, bool DEF>
+__device__ __forceinline__ void
+alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
+             double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
+             int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
+             unsigned long long* __restrict__ esc_n) {
     static_assert(K % 2 == 0 && K <= 16, "16-bit score fields: K / 2 words per stream and base");
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
@@ -791,6 +791,27 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
     };
     if (walker) chain_loop(std::true_type{});
     else chain_loop(std::false_type{});
+}
+
+// The band pass (every pair of the launch, trace strip of half-width `band`; 0 = full trace) ...
+template <int K, int W, bool DEF, int OCC>
+__global__ void __launch_bounds__(64 * (W + 1), OCC)
+k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
+          double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
+          int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
+          unsigned long long* __restrict__ esc_n) {
+    alignt2_body<K, W, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows, hops,
+                            next, band, esc_list, esc_n);
+}
+// ... and the full-trace pass over the pairs it queued (ps.sel / ps.dcount): a kernel of its own
+// name, so a profile shows the second pass (normally empty) apart from the first
+template <int K, int W, bool DEF, int OCC>
+__global__ void __launch_bounds__(64 * (W + 1), OCC)
+k_alignt2_queued(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
+                 double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
+                 int cap_rows, int hops, unsigned long long* __restrict__ next) {
+    alignt2_body<K, W, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows, hops,
+                            next, 0, nullptr, nullptr);
 }
 
 }  // namespace taxi2

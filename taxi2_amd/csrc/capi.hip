@@ -421,8 +421,12 @@ template <int K, int W, bool DEF, int OCC>
 void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                     int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
                     unsigned long long* nx, BandArgs ba) {
-    hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
-                       hops, nx, ba.band, ba.esc_list, ba.esc_n);
+    if (ps.sel)  // the queued pairs of a band pass, full trace
+        hipLaunchKernelGGL((k_alignt2_queued<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr,
+                           bb, cap, hops, nx);
+    else
+        hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
+                           hops, nx, ba.band, ba.esc_list, ba.esc_n);
 }
 
 const VariantT kAlignT2[] = {

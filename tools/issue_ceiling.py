@@ -14,6 +14,10 @@ Method.
   into basic blocks and a block is HOT when it is reached on the straight path of the step (no
   s_cbranch_execz / s_cbranch_vccz jumps over it): the cold blocks (a pair's first row, a row byte
   other than A/C/G/T, the owner of column nB on a pair's last row) run once per pair or never.
+* The trace block (byte packing + the 16-byte store, behind the band's lane mask) runs only on
+  the steps where some lane of the wave meets the stored strip: it is priced with weight
+  band_store_fraction() (the fraction of (fill wave, step) pairs of a config-3 chain with a lane
+  in the strip; 1.0 with --band 0).
 * Each VALU opcode (suffixes _e32 / _e64 / _dpp / _sdwa stripped) gets the SIMD cycles per wave64
   instruction measured at 8 waves per SIMD in valu_peak.txt; an opcode the microbenchmark does
   not list gets the cost of its class (v_pk_* and 3-source VOP3 4.09, v_cmp / v_cndmask, other
@@ -97,14 +101,17 @@ def step_loops(lines: list[str]) -> list[tuple[int, int]]:
     return [lp for lp in loops if not any(o != lp and lp[0] <= o[0] and o[1] <= lp[1] for o in loops)]
 
 
-def hot_instructions(body: list[str]) -> list[str]:
+def hot_instructions(body: list[str]) -> tuple[list[str], list[str]]:
     """Instructions of the blocks on the straight path: a forward s_cbranch_exec/vcc z jump marks
-    everything up to its target label as a conditional (cold) block."""
-    out, skip_to = [], None
+    everything up to its target label as a conditional (cold) block -- except the block holding
+    the trace store, returned separately (second list)."""
+    out, store, skip_to, block = [], [], None, []
     for l in body:
         lab = re.match(r"^(\.LBB\w+):", l)
         if lab and skip_to == lab.group(1):
-            skip_to = None
+            if any(op.startswith("global_store_dwordx4") for op in block):
+                store.extend(block)
+            skip_to, block = None, []
             continue
         t = l.strip().split()
         if not t or t[0].startswith((".", ";")) or t[0].endswith(":"):
@@ -115,7 +122,33 @@ def hot_instructions(body: list[str]) -> list[str]:
             continue
         if skip_to is None:
             out.append(t[0])
-    return out
+        else:
+            block.append(t[0])
+    return out, store
+
+
+def band_store_fraction(L: int, K: int, W: int, band: int, pairs: int) -> float:
+    """Fraction of (fill wave, step) pairs of one chain (`pairs` pairs of L x L per stream, both
+    streams alike) in which some lane's column block meets the stored strip of its row
+    (alignt2_kernel.hpp a2_band_blocks with nA = nB = L)."""
+    import numpy as np
+
+    if band <= 0:
+        return 1.0
+    rows = pairs * L
+    steps = rows + 63
+    lanes = np.arange(64)
+    hit = 0
+    for w in range(W):
+        t = 64 * w + lanes
+        for st in range(steps):
+            g = st - lanes
+            ok = (g >= 0) & (g < rows)
+            i = g % L + 1
+            lo = (np.maximum(1, i - band) - 1) // K
+            hi = (np.minimum(L, i + band) - 1) // K
+            hit += bool(np.any(ok & (t >= lo) & (t <= hi)))
+    return hit / (W * steps)
 
 
 def pmc(path: Path, kernel_pat: str) -> dict[str, float]:
@@ -138,6 +171,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=524288)
     ap.add_argument("--cells", type=float, default=1e6, help="useful DP cells per pair")
     ap.add_argument("--out", default=str(ROOT / "profiles/compute_ceiling.json"))
+    ap.add_argument("--band", type=int, default=95, help="trace band of the run (capi.hip default at 1 000 bp)")
+    ap.add_argument("--shape", default="1000,8,2,4", help="L,K,W,pairs per stream of the profiled chains")
     args = ap.parse_args()
 
     costs = valu_costs(Path(args.costs))
@@ -148,13 +183,22 @@ def main() -> None:
     unlisted: Counter = Counter()
     loops = []
     hot_all: Counter = Counter()
+    L, K, W, P = (int(x) for x in args.shape.split(","))
+    f = band_store_fraction(L, K, W, args.band, P)
     for a, b in step_loops(body):
-        hot = [op for op in hot_instructions(body[a:b + 1]) if op.startswith("v_")]
+        hot, store = hot_instructions(body[a:b + 1])
+        hot = [op for op in hot if op.startswith("v_")]
+        store = [op for op in store if op.startswith("v_")]
         hist = Counter(base_op(op) for op in hot)
-        cyc = sum(price(op, costs, unlisted) for op in hot)
-        loops.append({"lines": [start + a + 1, start + b + 1], "hot_valu": len(hot), "cycles": cyc,
-                      "mean_cyc": cyc / max(1, len(hot)), "histogram": dict(hist.most_common())})
+        shist = Counter(base_op(op) for op in store)
+        cyc = sum(price(op, costs, unlisted) for op in hot) + f * sum(price(op, costs, unlisted) for op in store)
+        n = len(hot) + f * len(store)
+        loops.append({"lines": [start + a + 1, start + b + 1], "hot_valu": len(hot), "trace_block_valu": len(store),
+                      "trace_block_weight": f, "cycles": cyc, "mean_cyc": cyc / max(1e-9, n),
+                      "histogram": dict(hist.most_common()), "trace_block_histogram": dict(shist.most_common())})
         hot_all.update(hist)
+        for op, c in shist.items():
+            hot_all[op] += f * c
     n_all = sum(hot_all.values())
     cyc_all = sum(price(op, costs, Counter()) * c for op, c in hot_all.items())
     mean_cyc = cyc_all / n_all
@@ -174,6 +218,8 @@ def main() -> None:
         "ceiling_instr_per_simd_clk": 1.0 / mean_cyc,
         "pmc_frac_of_ceiling": achieved * mean_cyc,
         "full_rate_share": sum(c for op, c in hot_all.items() if price(op, costs, Counter()) < 3.0) / n_all,
+        "trace_band": args.band,
+        "trace_block_weight": f,
         "step_loops": loops,
         "priced_by_class": dict(unlisted),
         "source": f"{Path(args.pmc_csv).relative_to(ROOT) if Path(args.pmc_csv).is_absolute() else args.pmc_csv} "
