@@ -79,6 +79,31 @@ class _OrganismFasta:
         self.fh.close()
 
 
+def group_minima(qids: list[str], res: np.ndarray, scale: float, R: int) -> list[tuple[int, int, float | None]]:
+    """Per group of consecutive equal query ids (``groupby(distance.x.id)``, decontaminate.py:255-259):
+    ``min(distances, key=d or inf)`` (:261-268) -- the first minimum as (query, reference, scaled
+    value), or (the group's first query, reference 0, None) when no distance is defined.  ``res`` rows
+    are closest_rows output (closest index, unscaled value); nothing when there are no references
+    (the reference's groupby then yields no group and zip stops)."""
+    idx = res[:, 0].astype(np.int64)
+    dmin = res[:, 1]
+    minima: list[tuple[int, int, float | None]] = []
+    Q = len(qids)
+    if R:
+        g0 = 0
+        for k in range(1, Q + 1):
+            if k == Q or qids[k] != qids[g0]:
+                best = None
+                for q in range(g0, k):
+                    v = dmin[q] * scale if idx[q] >= 0 else inf
+                    if best is None or v < best[0]:
+                        best = (v, q)
+                v, q = best
+                minima.append((q, int(idx[q]), v) if v != inf else (g0, 0, None))
+                g0 = k
+    return minima
+
+
 class Decontaminate:
     def __init__(self):
         self.work_dir: Path = None
@@ -180,24 +205,7 @@ class Decontaminate:
         finally:
             qs.free()
             rs.free()
-        idx = res[:, 0].astype(np.int64)
-        dmin = res[:, 1]
-
-        # group minima: min(distances of the group, key=d or inf) -- first minimum; all None ->
-        # the group's first distance (its first query against outgroup[0])
-        minima: list[tuple[int, int, float | None]] = []
-        if R:
-            g0 = 0
-            for k in range(1, Q + 1):
-                if k == Q or dn[k].id != dn[g0].id:
-                    best = None
-                    for q in range(g0, k):
-                        v = dmin[q] * scale if idx[q] >= 0 else inf
-                        if best is None or v < best[0]:
-                            best = (v, q)
-                    v, q = best
-                    minima.append((q, int(idx[q]), v) if v != inf else (g0, 0, None))
-                    g0 = k
+        minima = group_minima([s.id for s in dn], res, scale, R)
         threshold = self.params.thresholds.similarity
         verdicts, lines = [], []
         for sequence, (q, r, d) in zip(data, minima):

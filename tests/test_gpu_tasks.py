@@ -312,3 +312,96 @@ def test_decontaminate(tmp_path, engine, oracle_c, pct):
                 v = A[q, r]
                 fh.write(Distance(DistanceMetric.Uncorrected(), dn[q], on[r], float(v) if np.isfinite(v) else None))
     assert (tmp_path / "out/distances/p.linear.tsv").read_text() == lin.read_text()
+
+
+@pytest.mark.parametrize("pct", [False, True])
+def test_decontaminate2(tmp_path, engine, oracle_c, pct):
+    """decontaminate2.py:390-434: outgroup AND ingroup minima per group of consecutive query ids,
+    x100 on the outgroup side only, side weights, contaminant = out defined and (in undefined or
+    out < in); summary, sequence files and all four distance files against the oracle."""
+    from taxi2_amd.distances import Distance, DistanceHandler, DistanceMetric
+    from taxi2_amd.handlers import FileHandler
+    from taxi2_amd.sequences import Sequence, SequenceHandler, Sequences
+    from taxi2_amd.tasks import Decontaminate2
+
+    allseqs = read_tab("Taxi2test1_120.tab")
+    data = allseqs[:12]
+    data = data[:4] + [Sequence(data[3].id, data[8].seq, data[8].extras)] + data[4:]
+    data.append(Sequence("allN", "NNNNNNNNNN", dict(data[0].extras)))
+    outgroup = allseqs[40:48] + [Sequence("twin", data[1].seq, dict(data[1].extras))]
+    ingroup = allseqs[60:70] + [Sequence("inN", "NNNN", dict(data[0].extras))]
+    task = Decontaminate2()
+    task.engine = engine
+    task.progress_handler = None
+    task.work_dir = tmp_path / "out"
+    task.input = Sequences(data)
+    task.outgroup = Sequences(outgroup)
+    task.ingroup = Sequences(ingroup)
+    task.params.pairs.write = False
+    task.params.weights.outgroup = 1.0
+    task.params.weights.ingroup = 100.0 if pct else 1.5
+    task.params.format.percentage_multiply = pct
+    task.start()
+
+    dn = [s.normalize() for s in data]
+    Q = len(dn)
+
+    def side(refs, scale):
+        rn = [s.normalize() for s in refs]
+        R = len(rn)
+        seqs = [s.seq for s in dn] + [s.seq for s in rn]
+        pa = np.repeat(np.arange(Q), R)
+        pb = np.tile(np.arange(R), Q) + Q
+        out, _ = oracle_c.batch(seqs, pa, pb, align=True, scores=(1, -1, -8, -1, -1, -1), metrics=("p",))
+        A = out[:, 0, 0].reshape(Q, R) * scale
+        minima, g0 = [], 0
+        for k in range(1, Q + 1):
+            if k == Q or dn[k].id != dn[g0].id:
+                best = None
+                for q in range(g0, k):
+                    for r in range(R):
+                        v = A[q, r] if np.isfinite(A[q, r]) else np.inf
+                        if best is None or v < best[0]:
+                            best = (v, r)
+                minima.append((rn[best[1]].id, None if best[0] == np.inf else float(best[0])))
+                g0 = k
+        return rn, A, minima
+
+    on, AO, omin = side(outgroup, 100.0 if pct else 1.0)
+    inn, AI, imin = side(ingroup, 1.0)
+    rows = []
+    for s, (oid, od), (iid, idd) in zip(data, omin, imin):
+        od = None if od is None else od * task.params.weights.outgroup
+        idd = None if idd is None else idd * task.params.weights.ingroup
+        c = False if od is None else True if idd is None else od < idd
+        rows.append((s, oid, od, iid, idd, c))
+    assert any(r[5] for r in rows) and not all(r[5] for r in rows)
+    exp_sum = tmp_path / "exp_summary.tsv"
+    cols = ("query_id", "outgroup_id", "outgroup_distance", "ingroup_id", "ingroup_distance", "contaminant")
+    with FileHandler.Tabfile(exp_sum, "w", columns=cols) as fh:
+        for s, oid, od, iid, idd, c in rows:
+            fh.write((s.id, oid, "NA" if od is None else "{:.4f}".format(od), iid,
+                      "NA" if idd is None else "{:.4f}".format(idd), "Yes" if c else "No"))
+    assert (tmp_path / "out/summary.tsv").read_text() == exp_sum.read_text()
+    for name, want in (("decontaminated.tsv", False), ("contaminants.tsv", True)):
+        exp = tmp_path / f"exp_{name}"
+        with SequenceHandler.Tabfile(exp, "w", idHeader="seqid", seqHeader="sequence") as fh:
+            for r in rows:
+                if r[5] == want:
+                    fh.write(r[0])
+        assert (tmp_path / "out" / name).read_text() == exp.read_text(), name
+    for label, refs, A in (("outgroup", on, AO), ("ingroup", inn, AI)):
+        lin = tmp_path / f"exp_{label}_lin.tsv"
+        with DistanceHandler.Linear.WithExtras(lin, "w", missing="NA", formatter="{:.4f}") as fh:
+            for q in range(Q):
+                for r in range(len(refs)):
+                    v = A[q, r]
+                    fh.write(Distance(DistanceMetric.Uncorrected(), dn[q], refs[r], float(v) if np.isfinite(v) else None))
+        assert (tmp_path / f"out/distances/{label}.p.linear.tsv").read_text() == lin.read_text(), label
+        mat = tmp_path / f"exp_{label}_mat.tsv"
+        with DistanceHandler.Matrix(mat, "w", missing="NA", formatter="{:.4f}") as fh:
+            for q in range(Q):
+                for r in range(len(refs)):
+                    v = A[q, r]
+                    fh.write(Distance(DistanceMetric.Uncorrected(), dn[q], refs[r], float(v) if np.isfinite(v) else None))
+        assert (tmp_path / f"out/distances/{label}.p.matricial.tsv").read_text() == mat.read_text(), label
