@@ -159,6 +159,18 @@ __device__ __forceinline__ void dp_step1c(int s, int lane, S1Col<NW> (&st)[K], S
     carry = s1_best_left<B, TRACK>(in);
 }
 
+// Orientation of a pair cut into a chain (true: columns = X[a], rows = Y[b]).  A pair that
+// contains the chain's column sequence keeps it on the columns, so the chain goes on.  A chain
+// starts with X[a] on the columns (the sequence consecutive pairs share: a triangle row, a
+// query against its references) unless Y[b] is more than 1/8 longer (then the shorter rows
+// save more steps than the chain would).  Equal lengths: X[a] always.
+__device__ __forceinline__ bool at_swap(const uint8_t* xa, const uint8_t* yb, int la, int lb, const uint8_t* ccol,
+                                        int n) {
+    if (n > 0 && xa == ccol) return true;
+    if (n > 0 && yb == ccol) return false;
+    return 8 * lb <= 9 * la;
+}
+
 // Pass 1 (B = false) over ps / pass 2 (B = true) over wlist[0, *wcount), as k_align1.
 template <int K, int W, bool DEF, int OCC, bool B, int NW>
 __global__ void __launch_bounds__(64 * W, OCC)
@@ -204,7 +216,9 @@ k_align1c(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 int64_t q = qc;
                 const uint8_t* ccol = nullptr;
                 for (; q < qend; ++q) {
-                    const int64_t p = B ? (int64_t)wlist[q] : q;
+                    // pass 2 entries carry pass 1's orientation in bit 31 (pair index < 2^31, host-checked)
+                    const uint32_t wq = B ? wlist[q] : 0u;
+                    const int64_t p = B ? (int64_t)(wq & 0x7FFFFFFFu) : q;
                     int64_t a, b;
                     decode_pair(ps, p, a, b);
                     const int4 ma = XS.meta[a];
@@ -225,7 +239,14 @@ k_align1c(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                         }
                         continue;
                     }
-                    const bool swp = mb.x <= ma.x;  // rows = b, columns = a
+                    // orientation (swp: rows = b, columns = a): the chain rule at_swap (keep
+                    // the shared sequence on the columns; rows may then be up to 1/8 longer than
+                    // columns, within the variant's capacity, which covers both sets).  It depends on
+                    // the chain being cut, so pass 2 -- which cuts its own chains -- must not re-decide
+                    // it: it reuses pass 1's choice from the worklist entry (a re-decided orientation
+                    // wrote the unwritten orientation's slot: a null slot in single-orientation mode)
+                    const bool swp = B ? (wq >> 31) != 0u
+                                       : at_swap(XS.bytes + XS.offs[a], YS.bytes + YS.offs[b], ma.x, mb.x, ccol, n);
                     const uint8_t* cseq = swp ? XS.bytes + XS.offs[a] : YS.bytes + YS.offs[b];
                     if (n > 0 && cseq != ccol) break;
                     const int4 rm = swp ? mb : ma;
@@ -344,13 +365,13 @@ k_align1c(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
                 double* slot_a = cp.swp ? o_ba : o_ab;  // orientation A = (rows, cols)
                 double* slot_b = cp.swp ? o_ab : o_ba;
                 if (B) {
-                    a1_write(slot_b, ms, c);
+                    if (slot_b) a1_write(slot_b, ms, c);
                 } else {
                     const bool diverges = (c.w[1] & 0x3FFFu) != 0u;
                     if (slot_a) a1_write(slot_a, ms, c);
                     if (slot_b) {
                         if (!diverges) a1_write(slot_b, ms, c);
-                        else wlist[atomicAdd(wcount, 1u)] = (uint32_t)p;
+                        else wlist[atomicAdd(wcount, 1u)] = (uint32_t)p | ((uint32_t)cp.swp << 31);
                     }
                     if (sout) sout[p] = (int)f.x >> 1;
                 }

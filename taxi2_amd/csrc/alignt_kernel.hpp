@@ -80,18 +80,6 @@ struct AtWalk {  // one walk: position, state, its cell's trace byte, bytes of t
     int valid, ts, tv, gap;
 };
 
-// Orientation of a pair cut into a chain (true: columns = X[a], rows = Y[b]).  A pair that
-// contains the chain's column sequence keeps it on the columns, so the chain goes on.  A chain
-// starts with X[a] on the columns (the sequence consecutive pairs share: a triangle row, a
-// query against its references) unless Y[b] is more than 1/8 longer (then the shorter rows
-// save more steps than the chain would).  Equal lengths: X[a] always.
-__device__ __forceinline__ bool at_swap(const uint8_t* xa, const uint8_t* yb, int la, int lb, const uint8_t* ccol,
-                                        int n) {
-    if (n > 0 && xa == ccol) return true;
-    if (n > 0 && yb == ccol) return false;
-    return 8 * lb <= 9 * la;
-}
-
 template <int K, int W, bool DEF, int OCC>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,

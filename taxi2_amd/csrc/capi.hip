@@ -332,6 +332,8 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
     // chained kernel (consecutive pairs sharing their column sequence stream through the lanes);
     // TAXI2_A1_NOCHAIN=1 selects the one-pair-at-a-time kernel
     const bool chain = !getenv("TAXI2_A1_NOCHAIN");
+    if (chain && ps.count >= ((int64_t)1 << 31))  // worklist entries: pair index | orientation << 31
+        return fail(ctx, "single-orientation aligner: %lld pairs in one call (limit 2^31 - 1)", (long long)ps.count);
     const size_t lds = chain ? a1c_lds_bytes(v.K, v.W, v.def) : a1_lds_bytes(xcap, v.K, v.W, v.def);
     const void* const* fns = chain ? v.fnc : v.fn;
     auto launch = chain ? v.launchc : v.launch;

@@ -88,20 +88,23 @@ def test_alignt_triangle(engine, oracle_c, env):
     st.free()
 
 
+@pytest.mark.parametrize("scores", ["default", "generic"])
 @pytest.mark.parametrize("env", [{}, {"TAXI2_AT_CHUNK": "5"}, {"TAXI2_NO_PACKED": "1"}])
-def test_alignt_rectangle(engine, oracle_c, env):
+def test_alignt_rectangle(engine, oracle_c, env, scores):
     """One ordered orientation per pair (versusReference): the walk of the (query, ref) slot,
-    with queries longer and shorter than the references (rows / columns swapped)."""
+    with queries longer and shorter than the references (rows / columns swapped; under generic
+    scores the swapped walk reads the stored tagF)."""
     seqs = _tie_heavy(14, 700, 0x62)
     qseq = seqs[:6]
     rseq = [s[:350] if k % 2 else s for k, s in enumerate(seqs[6:])]
     qs = engine.upload(qseq, align=True)
     rs = engine.upload(rseq, align=True)
-    got = _with_env(env, lambda: engine.rect_pairs(qs, rs, 0, len(qseq), METRICS, SCORE_SETS["default"]))
+    sc = SCORE_SETS[scores]
+    got = _with_env(env, lambda: engine.rect_pairs(qs, rs, 0, len(qseq), METRICS, sc))
     allseq = qseq + rseq
     pa = np.repeat(np.arange(len(qseq)), len(rseq))
     pb = np.tile(np.arange(len(rseq)), len(qseq)) + len(qseq)
-    exp, _ = oracle_c.batch(allseq, pa, pb, align=True, scores=SCORE_SETS["default"])
+    exp, _ = oracle_c.batch(allseq, pa, pb, align=True, scores=sc)
     assert_metrics_equal(got, exp[:, 0, :])
     qs.free()
     rs.free()

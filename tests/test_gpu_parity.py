@@ -372,22 +372,26 @@ def test_chained_pairs(engine, oracle_c, chunk):
         s.free()
 
 
+@pytest.mark.parametrize("scores", ["default", "generic"])
 @pytest.mark.parametrize("chunk", [16, 5])
-def test_chained_long_ragged_rect(engine, oracle_c, chunk):
+def test_chained_long_ragged_rect(engine, oracle_c, chunk, scores):
     """2 100-2 600 bp (past the packed kernel's 2 048 columns, so k_align1c with three-word
     counters) query x reference with forced chains: references both shorter and longer than each
-    query, so chains start, break and restart in both orientations.  This is the shape on which a
-    changed chain-orientation rule faulted; every result against the oracle."""
+    query, so chains start, break and restart in both orientations, and the chain rule (at_swap)
+    puts rows up to 1/8 longer than columns.  Round 1's version of that rule faulted here: pass 2
+    re-decided the orientation and wrote the other orientation's (null) slot; pass 2 now reuses
+    pass 1's choice.  Every result against the oracle."""
     rng = np.random.default_rng(0x2100 + chunk)
     fam = family_sequences(12, 2600, 0x54 + chunk, ancestors=2, max_sub=0.05, indel_rate=0.02)
     seqs = [s[: 2100 + int(rng.integers(0, 500))] for s in fam]
     q, r = seqs[:4], seqs[4:]
     qs = engine.upload(q, align=True)
     rs = engine.upload(r, align=True)
-    got = _with_env("TAXI2_A1_CHUNK", str(chunk), lambda: engine.rect_pairs(qs, rs, 0, len(q), METRICS, None))
+    sc = SCORE_SETS[scores]
+    got = _with_env("TAXI2_A1_CHUNK", str(chunk), lambda: engine.rect_pairs(qs, rs, 0, len(q), METRICS, sc))
     pa = np.repeat(np.arange(len(q)), len(r))
     pb = np.tile(np.arange(len(r)), len(q)) + len(q)
-    exp, _ = oracle_c.batch(seqs, pa, pb, align=True, scores=SCORE_SETS["default"])
+    exp, _ = oracle_c.batch(seqs, pa, pb, align=True, scores=sc)
     assert_metrics_equal(got, exp[:, 0, :])
     for s in (qs, rs):
         s.free()
