@@ -799,7 +799,7 @@ struct Tracer {
     }
 };
 
-int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out);
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n);
 
 // Raw-mode NCD with C(x) computed once per set member (when the pairs outnumber the sequences).
 int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
@@ -830,7 +830,7 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
         hipLaunchKernelGGL(k_seq_streams, dim3((unsigned)((S.n + 255) / 256)), dim3(256), 0, ctx->stream, view(S), S.n,
                            d_sst);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_sst, S.n, singles[k])) return -1;
+        if (launch_zlen(ctx, d_sst, S.n, singles[k], S.max_len)) return -1;
     }
     for (int64_t c0 = 0; c0 < count; c0 += chunk) {
         const int64_t n = std::min(chunk, count - c0);
@@ -840,7 +840,7 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
         hipLaunchKernelGGL(k_ncd_concat_streams, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, view(X),
                            view(Y), d_idx, d_idx + chunk, n, both, d_cst);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_cst, m, d_c)) return -1;
+        if (launch_zlen(ctx, d_cst, m, d_c, X.max_len + Y.max_len)) return -1;
         hipLaunchKernelGGL(k_ncd_finish_cached, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, d_c, d_cx,
                            d_cy, d_idx, d_idx + chunk, n, both, d_v);
         HIP_TRY(ctx, hipGetLastError());
@@ -850,11 +850,29 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
     return 0;
 }
 
-// Compressed lengths of `n` device stream descriptors (persistent threads, per-thread scratch
-// slabs kept in the context; the head tables are zeroed once at allocation).
-int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out) {
+// Compressed lengths of `n` device stream descriptors, every stream at most max_n bytes.  Streams
+// up to zlw::NMAX bytes: one wave per stream with its state in LDS (k_zlen_wave, zlen_wave.hpp);
+// longer ones (or TAXI2_ZLEN_SERIAL=1): one thread per stream with per-thread HBM scratch slabs
+// kept in the context (the head tables are zeroed once at allocation).
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n) {
     if (n <= 0) return 0;
-    const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 128);  // 2 waves / SIMD
+    if (max_n <= zlw::NMAX && !getenv("TAXI2_ZLEN_SERIAL")) {
+        const int nmax = std::max(max_n, 4);
+        const size_t lds = zlw::lds_bytes(nmax);
+        if (lds > 64 * 1024)
+            HIP_TRY(ctx, hipFuncSetAttribute((const void*)k_zlen_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int per_cu = 0;
+        HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave, 64, lds));
+        const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
+        hipLaunchKernelGGL(k_zlen_wave, dim3((unsigned)grid), dim3(64), lds, ctx->stream, d_st, n, nmax, d_out);
+        HIP_TRY(ctx, hipGetLastError());
+        return 0;
+    }
+    // waves per SIMD of the one-thread-per-stream parse (TAXI2_ZLEN_WAVES, 1..4: VGPRs cap it at 4);
+    // each thread owns 113 KB of HBM scratch
+    int wps = 2;
+    if (const char* e = getenv("TAXI2_ZLEN_WAVES")) wps = std::max(1, std::min(4, atoi(e)));
+    const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 4 * 64 * wps);
     const int64_t threads = (want + 63) / 64 * 64;
     if (ctx->z_threads < threads) {
         if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
@@ -1275,7 +1293,7 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
                            aligned ? tr.d_out + tr.chunk * 2 * tr.cap : nullptr, aligned ? tr.d_len : nullptr,
                            aligned ? tr.cap : 0, d_st);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_st, m * 3, d_c)) return -1;
+        if (launch_zlen(ctx, d_st, m * 3, d_c, aligned ? 2 * tr.cap : X->max_len + Y->max_len)) return -1;
         hipLaunchKernelGGL(k_ncd_finish, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, d_c, m, d_v);
         HIP_TRY(ctx, hipGetLastError());
         HIP_TRY(ctx, hipMemcpyAsync(out + c0 * no, d_v, (size_t)m * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1312,7 +1330,7 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
         hipLaunchKernelGGL(k_zlen_streams, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, view(*X),
                            view(*Y), di, ys ? di + chunk : nullptr, n, d_st);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_st, n, d_c)) return -1;
+        if (launch_zlen(ctx, d_st, n, d_c, X->max_len + (ys ? Y->max_len : 0))) return -1;
         HIP_TRY(ctx, hipMemcpyAsync(out + c0, d_c, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }

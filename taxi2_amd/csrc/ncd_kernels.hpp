@@ -10,6 +10,7 @@
 #pragma once
 #include "common.hpp"
 #include "deflate_len.hpp"
+#include "zlen_wave.hpp"
 
 namespace taxi2 {
 
@@ -37,6 +38,21 @@ k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, 
     for (int64_t s = tid; s < n; s += nthreads) {
         const ZStream d = st[s];
         out[s] = zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t);
+    }
+}
+
+// One wave per stream, all state in LDS (zlen_wave.hpp): for launches whose streams are at most
+// `nmax` bytes (dynamic LDS sized for nmax).  Persistent: each workgroup (one wave) takes streams
+// blockIdx.x, + gridDim.x, ...
+__global__ void __launch_bounds__(64)
+k_zlen_wave(const ZStream* __restrict__ st, int64_t n, int nmax, int32_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t zsm[];
+    const int lane = (int)threadIdx.x;
+    for (int64_t s = blockIdx.x; s < n; s += gridDim.x) {
+        const ZStream d = st[s];
+        const int r = d.na + d.nb <= nmax ? zlw::compressed_len_wave(d.a, d.na, d.b, d.nb, zsm, nmax, lane) : -1;
+        if (lane == 0) out[s] = r;  // -1: longer than the launch promised (the host checks)
+        __syncthreads();
     }
 }
 

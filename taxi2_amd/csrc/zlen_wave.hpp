@@ -1,0 +1,216 @@
+// Compressed length of zlib.compress(s) with ONE WAVE per stream, everything in LDS.
+//
+// Same result as deflate_len.hpp's compressed_len (zlib 1.2.11, level 6) -- the parse, tallies
+// and block flushes are that code's -- but the two latency-bound parts are restructured:
+//
+// * Hash chains without head / prev tables.  deflate_slow inserts every position p <= n - 3 in
+//   order, so zlib's chain from p is exactly "the earlier positions with the same 15-bit hash
+//   ((b0 << 10) ^ (b1 << 5) ^ b2, masked), newest first", and hash_head = the newest of them.
+//   The wave sorts the keys (hash << 16 | position) once per stream (bitonic, in LDS); candidate
+//   k of a query at p is then sorted[idx(p) - 1 - k] while the hash matches: one LDS read, no
+//   pointer chase.  (Inputs stay below 32 768 bytes on this path, so zlib's prev[p & WMASK]
+//   aliasing never applies.)
+// * longest_match evaluated for 64 candidates at once, one per lane, then reduced to what zlib's
+//   sequential loop returns: the chain is cut at the first candidate <= limit (the first one, the
+//   hash head, only needs to be a real position: its distance was checked by the caller); the
+//   loop stops at the first candidate whose length reaches nice_match AND beats prev_length (it is
+//   the first improvement to reach nice); among the candidates up to there the longest wins, the
+//   earliest on ties, and only if it beats prev_length (zlib's strict `len > best_len`).  zlib's
+//   quick rejects (bytes best_len - 1 / best_len, 0, 1) only skip candidates that cannot improve,
+//   so comparing full lengths gives the same answer.  A second round covers candidates 64-127.
+//
+// Everything else is uniform across the wave (every lane runs the same parse on the same values);
+// lane 0 alone owns the Huffman statistics (Trees, in LDS) and the block flushes.
+#pragma once
+#include "deflate_len.hpp"
+
+namespace taxi2 {
+namespace zlw {
+
+constexpr int NMAX = 16384;  // longest stream on this path (LDS: ~7 B per byte + the trees)
+
+__host__ __device__ inline int pow2_at_least(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+__host__ __device__ inline size_t al16(size_t b) { return (b + 15) / 16 * 16; }
+// LDS layout for streams of at most nmax bytes: [window nmax + 264][keys P2 x u32][idx nmax x u16][Trees]
+__host__ __device__ inline size_t off_keys(int nmax) { return al16((size_t)nmax + zl::MAX_MATCH + 16); }
+__host__ __device__ inline size_t off_idx(int nmax) { return off_keys(nmax) + (size_t)pow2_at_least(nmax) * 4; }
+__host__ __device__ inline size_t off_trees(int nmax) { return al16(off_idx(nmax) + (size_t)nmax * 2); }
+__host__ __device__ inline size_t lds_bytes(int nmax) { return al16(off_trees(nmax) + sizeof(zl::Trees)); }
+
+__device__ __forceinline__ uint32_t hash3(const uint8_t* w, int p) {
+    return (((uint32_t)w[p] << 10) ^ ((uint32_t)w[p + 1] << 5) ^ (uint32_t)w[p + 2]) & (uint32_t)zl::HASH_MASK;
+}
+
+// bytes w[p .. p + 3] (little-endian) from two aligned LDS words: one v_alignbyte
+__device__ __forceinline__ uint32_t load4(const uint8_t* w, int p) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(w) + (p >> 2);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(p & 3));
+}
+
+// zlib's longest_match for the query at `strstart` (see the header comment); uniform in, uniform out
+__device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint32_t* keys, int i0, int strstart,
+                                                  int lookahead, int prev_length, int& match_start, int lane) {
+    const int chain_length = prev_length >= zl::GOOD ? zl::CHAIN >> 2 : zl::CHAIN;
+    const int nice = zl::NICE < lookahead ? zl::NICE : lookahead;
+    const int limit = strstart > zl::MAX_DIST ? strstart - zl::MAX_DIST : 0;
+    const uint32_t h = keys[i0] >> 16;
+    int best = prev_length, best_pos = -1;
+    for (int base = 0; base < chain_length; base += 64) {
+        const int k = base + lane;
+        const int idx = i0 - 1 - k;
+        bool ok = k < chain_length && idx >= 0;
+        int cand = 0;
+        if (ok) {
+            const uint32_t kk = keys[idx];
+            cand = (int)(kk & 0xFFFFu);
+            ok = (kk >> 16) == h && (k == 0 ? cand > 0 : cand > limit);
+        }
+        int len = 0;
+        if (ok) {
+            // common prefix, four bytes per step (the window is zero-padded past the input, as
+            // zlib's; lengths are capped at MAX_MATCH as its scan loop is).  zlib examines a
+            // candidate only when bytes 0 and 1 match (byte 2 then matches by the hash): a shorter
+            // prefix is no candidate.
+            for (;;) {
+                const uint32_t x = load4(win, strstart + len) ^ load4(win, cand + len);
+                if (x) {
+                    len += __builtin_ctz(x) >> 3;
+                    break;
+                }
+                len += 4;
+                if (len >= zl::MAX_MATCH) break;
+            }
+            len = len < zl::MAX_MATCH ? len : zl::MAX_MATCH;
+            if (len < zl::MIN_MATCH) len = 0;
+        }
+        const uint64_t stop = __ballot(len >= nice && len > prev_length);
+        // lanes up to the stop, then the longest (earliest on ties) by bisection on ballots: no
+        // cross-lane data movement but one readlane
+        const uint64_t upto = stop ? (stop ^ (stop - 1)) : ~0ull;
+        const int lv = (upto >> lane) & 1ull ? len : 0;
+        int rlen = 0;
+#pragma unroll
+        for (int bit = 8; bit >= 0; --bit) {
+            const int t = rlen | (1 << bit);
+            if (__ballot(lv >= t)) rlen = t;
+        }
+        if (rlen > best) {
+            best = rlen;
+            best_pos = __builtin_amdgcn_readlane(cand, __builtin_ctzll(__ballot(lv == rlen)));
+        }
+        // the chain ends inside this round, or the loop stopped: no further rounds
+        if (stop || __ballot(ok) != ~0ull) break;
+    }
+    if (best_pos >= 0) match_start = best_pos;
+    return best <= lookahead ? best : lookahead;
+}
+
+// len(zlib.compress(upper(a) + upper(b))); n = na + nb <= nmax (the caller's LDS layout).
+__device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_t* b, int nb, uint8_t* lds, int nmax,
+                                          int lane) {
+    using namespace zl;
+    const int n = na + nb;
+    uint8_t* win = lds;
+    uint32_t* keys = reinterpret_cast<uint32_t*>(lds + off_keys(nmax));
+    uint16_t* idx_of = reinterpret_cast<uint16_t*>(lds + off_idx(nmax));
+    Trees& t = *reinterpret_cast<Trees*>(lds + off_trees(nmax));
+
+    for (int i = lane; i < n + MAX_MATCH + 12; i += 64) {
+        uint8_t c = 0;
+        if (i < na) c = a[i];
+        else if (i < n) c = b[i - na];
+        win[i] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+    }
+    __syncthreads();
+    // sorted (hash, position) keys of the inserted positions 0 .. n - 3
+    const int npos = n >= MIN_MATCH ? n - (MIN_MATCH - 1) : 0;
+    const int P2 = pow2_at_least(npos > 1 ? npos : 2);
+    for (int i = lane; i < P2; i += 64) keys[i] = i < npos ? (hash3(win, i) << 16) | (uint32_t)i : 0xFFFFFFFFu;
+    __syncthreads();
+    for (int size = 2; size <= P2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = lane; i < P2 / 2; i += 64) {
+                const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));  // stride is a power of 2
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint32_t x = keys[lo], y = keys[hi];
+                if ((x > y) == up) {
+                    keys[lo] = y;
+                    keys[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = lane; i < npos; i += 64) idx_of[keys[i] & 0xFFFFu] = (uint16_t)i;
+    if (lane == 0) init_block(t);
+    __syncthreads();
+
+    int64_t bits = 0;
+    int block_start = 0, last_lit = 0;
+    int strstart = 0, lookahead = n;
+    int match_length = MIN_MATCH - 1, prev_length, match_start = 0, prev_match;
+    bool match_available = false;
+    auto flush = [&](bool last) {  // FLUSH_BLOCK_ONLY, lane 0; bits broadcast
+        __syncthreads();
+        if (lane == 0) {
+            flush_block(t, strstart - block_start, last, bits);
+            init_block(t);
+        }
+        bits = __shfl(bits, 0);
+        block_start = strstart;
+        last_lit = 0;
+        __syncthreads();
+    };
+    while (lookahead != 0) {
+        int hash_head = 0, i0 = 0;
+        if (lookahead >= MIN_MATCH) {  // insert(strstart): hash_head = the newest earlier same-hash position
+            i0 = idx_of[strstart];
+            if (i0 > 0) {
+                const uint32_t kp = keys[i0 - 1];
+                if ((kp >> 16) == (keys[i0] >> 16)) hash_head = (int)(kp & 0xFFFFu);
+            }
+        }
+        prev_length = match_length;
+        prev_match = match_start;
+        match_length = MIN_MATCH - 1;
+        if (hash_head != 0 && prev_length < LAZY && strstart - hash_head <= MAX_DIST) {
+            match_length = coop_longest_match(win, keys, i0, strstart, lookahead, prev_length, match_start, lane);
+            if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > TOO_FAR)
+                match_length = MIN_MATCH - 1;
+        }
+        if (prev_length >= MIN_MATCH && match_length <= prev_length) {
+            if (lane == 0) {  // _tr_tally_dist
+                t.lfc[length_code(prev_length - MIN_MATCH) + LITERALS + 1]++;
+                t.dfc[dist_code(strstart - 1 - prev_match - 1)]++;
+            }
+            const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
+            lookahead -= prev_length - 1;
+            strstart += prev_length - 2;  // the match's other positions (inserted by the sort)
+            match_available = false;
+            match_length = MIN_MATCH - 1;
+            strstart++;
+            if (bflush) flush(false);
+        } else if (match_available) {
+            if (lane == 0) t.lfc[win[strstart - 1]]++;
+            const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
+            if (bflush) flush(false);
+            strstart++;
+            lookahead--;
+        } else {
+            match_available = true;
+            strstart++;
+            lookahead--;
+        }
+    }
+    if (match_available && lane == 0) t.lfc[win[strstart - 1]]++;
+    flush(true);
+    return 2 + (int)(bits >> 3) + 4;
+}
+
+}  // namespace zlw
+}  // namespace taxi2

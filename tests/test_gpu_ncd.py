@@ -203,3 +203,42 @@ def test_ncd_aligned_long_sequences(engine):
         assert got[k, 0] == R.ncd(ax, ay)
         assert got[k, 1] == R.ncd(by, bx)
     st.free()
+
+
+def test_zlib_lengths_wave_path_edges(engine):
+    """The one-wave-per-stream path (k_zlen_wave, streams <= 16 384 bytes): high-entropy inputs
+    near its 16 384-byte limit (mostly literals: up to the 16 383-symbol block flush), DNA
+    families with long repeats (matches reaching nice_match / MAX_MATCH, second candidate round),
+    tiny inputs; against Python's zlib and against the one-thread-per-stream path."""
+    import os
+
+    rng = random.Random(29)
+    wide = "".join(chr(c) for c in list(range(33, 97)) + list(range(123, 127)))
+
+    def no_repeat(L: int) -> str:  # no 3-gram twice: every byte a literal, 16 383 of them flush a block
+        out, seen = ["!", "#"], set()
+        while len(out) < L:
+            c = rng.choice(wide)
+            g = out[-2] + out[-1] + c
+            if g not in seen:
+                seen.add(g)
+                out.append(c)
+        return "".join(out)
+
+    seqs = [no_repeat(16384), no_repeat(16383), "".join(rng.choice(wide) for _ in range(16200))]
+    fam = family_sequences(4, 2500, 0x29, ancestors=1, max_sub=0.01, indel_rate=0.002)
+    seqs += fam + ["ACGT" * 600, "A" * 3000, "", "AC", "ACG", "ACGTACGT"]
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    exp1 = [len(zlib.compress(s.upper().encode())) for s in seqs]
+    assert engine.zlib_lengths(st, np.arange(n)).tolist() == exp1
+    xs = np.array([3, 4, 5, 6, 7, 8, 9, 3, 10])
+    ys = np.array([4, 3, 6, 5, 8, 7, 3, 9, 10])
+    exp2 = [len(zlib.compress((seqs[a] + seqs[b]).upper().encode())) for a, b in zip(xs, ys)]
+    assert engine.zlib_lengths(st, xs, st, ys).tolist() == exp2
+    os.environ["TAXI2_ZLEN_SERIAL"] = "1"
+    try:
+        assert engine.zlib_lengths(st, xs, st, ys).tolist() == exp2
+    finally:
+        os.environ.pop("TAXI2_ZLEN_SERIAL")
+    st.free()
