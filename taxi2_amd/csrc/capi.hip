@@ -574,13 +574,16 @@ int launch_alignlong_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, con
     const size_t bb = ((size_t)ntile * (size_t)(rows + 63) * (size_t)TC + 255) / 256 * 256;
     int per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v->fn, 64 * (v->W + 1), 0));
-    double budget_gb = 40.0;
+    // trace budget: 40 GB, grown up to 96 GB (a third of the HBM) when that keeps every resident
+    // workgroup busy (pairs past ~6 500 bp need > 80 MB of trace each); TAXI2_AT_TRACE_GB fixes it
+    const int64_t resident = (int64_t)ctx->num_cus * std::max(1, per_cu);
+    double budget_gb = std::max(40.0, std::min(96.0, (double)std::min<int64_t>(ps.count, resident) * 2.0 * (double)bb / 1e9));
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     const int64_t fit = (int64_t)(budget_gb * 1e9 / (2.0 * (double)bb));
     if (2.0 * (double)bb > 200e9)
         return fail(ctx, "pair trace of %lld x %lld bp needs %.1f GB (limit 200 GB)", (long long)rows,
                     (long long)cols, 2.0 * (double)bb / 1e9);
-    const int64_t grid = std::max<int64_t>(1, std::min({ps.count, (int64_t)ctx->num_cus * std::max(1, per_cu), fit}));
+    const int64_t grid = std::max<int64_t>(1, std::min({ps.count, resident, fit}));
     if (shared_acquire(ctx, st)) return -1;
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
     const int64_t brows = rows + 64;
