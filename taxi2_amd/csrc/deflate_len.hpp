@@ -27,9 +27,11 @@
 #define __device__
 #define __forceinline__ inline
 #endif
-// The Huffman bookkeeping runs once per stream; keeping it out of line leaves the per-byte parse
-// loop its own small register set (higher occupancy for this latency-bound scalar code).
-#define ZL_COLD __attribute__((noinline))
+// The Huffman bookkeeping runs once per block.  The one-thread parse calls it out of line
+// (flush_block: its own small register set, higher occupancy for that latency-bound scalar code);
+// the one-wave parse (zlen_wave.hpp) inlines it (flush_block_inl), so the trees it keeps in LDS are
+// addressed with LDS instructions rather than flat ones.
+#define ZL_COLD __attribute__((always_inline))
 
 namespace taxi2 {
 namespace zl {
@@ -239,7 +241,7 @@ __host__ __device__ ZL_COLD inline void scan_tree(Trees& t, uint16_t* dl, int ma
 // _tr_flush_block for one block of `stored_len` input bytes: adds its bits to `bits` (the
 // stream's bit count so far; a stored block pads to a byte first) and, for the last block, the
 // final bi_windup.  Leaves the block statistics for init_block to reset.
-__host__ __device__ ZL_COLD inline void flush_block(Trees& t, int stored_len, bool last, int64_t& bits) {
+__host__ __device__ __forceinline__ void flush_block_inl(Trees& t, int stored_len, bool last, int64_t& bits) {
     const int lmax = build_tree(t, T_LIT);
     const int dmax = build_tree(t, T_DIST);
     scan_tree(t, t.ldl, lmax);
@@ -261,6 +263,9 @@ __host__ __device__ ZL_COLD inline void flush_block(Trees& t, int stored_len, bo
         bits += 3 + t.opt_len;
     }
     if (last) bits = (bits + 7) & ~(int64_t)7;
+}
+__host__ __device__ __attribute__((noinline)) inline void flush_block(Trees& t, int stored_len, bool last, int64_t& bits) {
+    flush_block_inl(t, stored_len, last, bits);
 }
 
 // init_block: empty statistics, END_BLOCK counted once.

@@ -29,6 +29,15 @@ namespace zlw {
 
 constexpr int NMAX = 16384;  // longest stream on this path (LDS: ~7 B per byte + the trees)
 
+#ifdef ZLW_PROF  // tools/zlw_phases.hip: s_memtime ticks per phase (window, sort, parse, flush) + counts
+__device__ unsigned long long zlw_prof[8];
+#define ZLW_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define ZLW_ADD(k, x) do { if (lane == 0) atomicAdd(&zlw_prof[k], (unsigned long long)(x)); } while (0)
+#else
+#define ZLW_T(v) (void)0
+#define ZLW_ADD(k, x) (void)0
+#endif
+
 __host__ __device__ inline int pow2_at_least(int v) {
     int p = 1;
     while (p < v) p <<= 1;
@@ -52,12 +61,12 @@ __device__ __forceinline__ uint32_t load4(const uint8_t* w, int p) {
 }
 
 // zlib's longest_match for the query at `strstart` (see the header comment); uniform in, uniform out
-__device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint32_t* keys, int i0, int strstart,
-                                                  int lookahead, int prev_length, int& match_start, int lane) {
+__device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint32_t* keys, int i0, uint32_t h,
+                                                  int strstart, int lookahead, int prev_length, int& match_start,
+                                                  int lane) {
     const int chain_length = prev_length >= zl::GOOD ? zl::CHAIN >> 2 : zl::CHAIN;
     const int nice = zl::NICE < lookahead ? zl::NICE : lookahead;
     const int limit = strstart > zl::MAX_DIST ? strstart - zl::MAX_DIST : 0;
-    const uint32_t h = keys[i0] >> 16;
     int best = prev_length, best_pos = -1;
     for (int base = 0; base < chain_length; base += 64) {
         const int k = base + lane;
@@ -75,13 +84,18 @@ __device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint
             // zlib's; lengths are capped at MAX_MATCH as its scan loop is).  zlib examines a
             // candidate only when bytes 0 and 1 match (byte 2 then matches by the hash): a shorter
             // prefix is no candidate.
-            for (;;) {
-                const uint32_t x = load4(win, strstart + len) ^ load4(win, cand + len);
-                if (x) {
-                    len += __builtin_ctz(x) >> 3;
+            for (;;) {  // eight bytes per step: the four word reads of a step go out together
+                const uint32_t x0 = load4(win, strstart + len) ^ load4(win, cand + len);
+                const uint32_t x1 = load4(win, strstart + len + 4) ^ load4(win, cand + len + 4);
+                if (x0) {
+                    len += __builtin_ctz(x0) >> 3;
                     break;
                 }
-                len += 4;
+                if (x1) {
+                    len += 4 + (__builtin_ctz(x1) >> 3);
+                    break;
+                }
+                len += 8;
                 if (len >= zl::MAX_MATCH) break;
             }
             len = len < zl::MAX_MATCH ? len : zl::MAX_MATCH;
@@ -118,7 +132,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     uint32_t* keys = reinterpret_cast<uint32_t*>(lds + off_keys(nmax));
     uint16_t* idx_of = reinterpret_cast<uint16_t*>(lds + off_idx(nmax));
     Trees& t = *reinterpret_cast<Trees*>(lds + off_trees(nmax));
-
+    ZLW_T(tw0);
     for (int i = lane; i < n + MAX_MATCH + 12; i += 64) {
         uint8_t c = 0;
         if (i < na) c = a[i];
@@ -126,6 +140,8 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
         win[i] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
     }
     __syncthreads();
+    ZLW_T(tw1);
+    ZLW_ADD(0, tw1 - tw0);
     // sorted (hash, position) keys of the inserted positions 0 .. n - 3
     const int npos = n >= MIN_MATCH ? n - (MIN_MATCH - 1) : 0;
     const int P2 = pow2_at_least(npos > 1 ? npos : 2);
@@ -149,6 +165,8 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     for (int i = lane; i < npos; i += 64) idx_of[keys[i] & 0xFFFFu] = (uint16_t)i;
     if (lane == 0) init_block(t);
     __syncthreads();
+    ZLW_T(tw2);
+    ZLW_ADD(1, tw2 - tw1);
 
     int64_t bits = 0;
     int block_start = 0, last_lit = 0;
@@ -158,7 +176,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     auto flush = [&](bool last) {  // FLUSH_BLOCK_ONLY, lane 0; bits broadcast
         __syncthreads();
         if (lane == 0) {
-            flush_block(t, strstart - block_start, last, bits);
+            flush_block_inl(t, strstart - block_start, last, bits);
             init_block(t);
         }
         bits = __shfl(bits, 0);
@@ -166,28 +184,55 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
         last_lit = 0;
         __syncthreads();
     };
-    while (lookahead != 0) {
-        int hash_head = 0, i0 = 0;
-        if (lookahead >= MIN_MATCH) {  // insert(strstart): hash_head = the newest earlier same-hash position
-            i0 = idx_of[strstart];
-            if (i0 > 0) {
-                const uint32_t kp = keys[i0 - 1];
-                if ((kp >> 16) == (keys[i0] >> 16)) hash_head = (int)(kp & 0xFFFFu);
+    // The parse's per-position LDS reads, 64 positions at a time into lane registers: lane l holds
+    // for position pb + l its sorted index | hash head << 16 (pinf), its hash, and the byte before
+    // it (the literal a step there tallies); the serial parse then reads them with v_readlane.
+    int pb = -64;
+    uint32_t pinf = 0, phash = 0, pbyte = 0;
+    auto prefetch = [&](int s0) {
+        pb = s0;
+        const int p = s0 + lane;
+        uint32_t v = 0, hq = 0;
+        if (p < npos) {
+            const int ii = idx_of[p];
+            hq = keys[ii] >> 16;
+            uint32_t hh = 0;
+            if (ii > 0) {
+                const uint32_t kp = keys[ii - 1];
+                if ((kp >> 16) == hq) hh = kp & 0xFFFFu;
             }
+            v = (uint32_t)ii | (hh << 16);
+        }
+        pinf = v;
+        phash = hq;
+        pbyte = (p >= 1 && p <= n) ? win[p - 1] : 0u;
+    };
+    // tallies: no-return LDS atomics on the u16 frequency pairs (lane 0), nothing waits on them
+    auto tally = [&](uint16_t* f, int c) {
+        if (lane == 0) atomicAdd(reinterpret_cast<uint32_t*>(f + (c & ~1)), 1u << (16 * (c & 1)));
+    };
+    while (lookahead != 0) {
+        if (strstart - pb >= 64) prefetch(strstart);
+        const int sl = strstart - pb;
+        int hash_head = 0, i0 = 0;
+        uint32_t hq = 0;
+        if (lookahead >= MIN_MATCH) {  // insert(strstart): hash_head = the newest earlier same-hash position
+            const uint32_t inf = __builtin_amdgcn_readlane(pinf, sl);
+            i0 = (int)(inf & 0xFFFFu);
+            hash_head = (int)(inf >> 16);
+            hq = __builtin_amdgcn_readlane(phash, sl);
         }
         prev_length = match_length;
         prev_match = match_start;
         match_length = MIN_MATCH - 1;
         if (hash_head != 0 && prev_length < LAZY && strstart - hash_head <= MAX_DIST) {
-            match_length = coop_longest_match(win, keys, i0, strstart, lookahead, prev_length, match_start, lane);
+            match_length = coop_longest_match(win, keys, i0, hq, strstart, lookahead, prev_length, match_start, lane);
             if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > TOO_FAR)
                 match_length = MIN_MATCH - 1;
         }
         if (prev_length >= MIN_MATCH && match_length <= prev_length) {
-            if (lane == 0) {  // _tr_tally_dist
-                t.lfc[length_code(prev_length - MIN_MATCH) + LITERALS + 1]++;
-                t.dfc[dist_code(strstart - 1 - prev_match - 1)]++;
-            }
+            tally(t.lfc, length_code(prev_length - MIN_MATCH) + LITERALS + 1);  // _tr_tally_dist
+            tally(t.dfc, dist_code(strstart - 1 - prev_match - 1));
             const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
             lookahead -= prev_length - 1;
             strstart += prev_length - 2;  // the match's other positions (inserted by the sort)
@@ -196,7 +241,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
             strstart++;
             if (bflush) flush(false);
         } else if (match_available) {
-            if (lane == 0) t.lfc[win[strstart - 1]]++;
+            tally(t.lfc, (int)__builtin_amdgcn_readlane(pbyte, sl));
             const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
             if (bflush) flush(false);
             strstart++;
@@ -207,8 +252,12 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
             lookahead--;
         }
     }
-    if (match_available && lane == 0) t.lfc[win[strstart - 1]]++;
+    if (match_available) tally(t.lfc, win[strstart - 1]);
+    ZLW_T(tw3);
+    ZLW_ADD(2, tw3 - tw2);
     flush(true);
+    ZLW_T(tw4);
+    ZLW_ADD(3, tw4 - tw3);
     return 2 + (int)(bits >> 3) + 4;
 }
 
