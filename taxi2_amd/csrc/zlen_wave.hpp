@@ -44,14 +44,20 @@ __host__ __device__ inline int pow2_at_least(int v) {
     return p;
 }
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) / 16 * 16; }
-// LDS layout for streams of at most nmax bytes: [window nmax + 264][keys P2 x u32][idx nmax x u16][Trees]
+// LDS layout for streams of at most nmax bytes: [window nmax + 274][key region: P2 x u32][Trees].
+// The key region holds the (hash << 16 | position) sort keys; after the sort it is reused as the
+// sorted positions (u16, first half) and each position's sorted index (u16, second half).
 __host__ __device__ inline size_t off_keys(int nmax) { return al16((size_t)nmax + zl::MAX_MATCH + 16); }
-__host__ __device__ inline size_t off_idx(int nmax) { return off_keys(nmax) + (size_t)pow2_at_least(nmax) * 4; }
-__host__ __device__ inline size_t off_trees(int nmax) { return al16(off_idx(nmax) + (size_t)nmax * 2); }
+__host__ __device__ inline size_t off_idx(int nmax) { return off_keys(nmax) + (size_t)pow2_at_least(nmax) * 2; }
+__host__ __device__ inline size_t off_trees(int nmax) { return al16(off_keys(nmax) + (size_t)pow2_at_least(nmax) * 4); }
 __host__ __device__ inline size_t lds_bytes(int nmax) { return al16(off_trees(nmax) + sizeof(zl::Trees)); }
 
 __device__ __forceinline__ uint32_t hash3(const uint8_t* w, int p) {
     return (((uint32_t)w[p] << 10) ^ ((uint32_t)w[p + 1] << 5) ^ (uint32_t)w[p + 2]) & (uint32_t)zl::HASH_MASK;
+}
+// the same hash from the low three bytes of a little-endian word
+__device__ __forceinline__ uint32_t hash_w(uint32_t w) {
+    return (((w & 0xFFu) << 10) ^ (((w >> 8) & 0xFFu) << 5) ^ ((w >> 16) & 0xFFu)) & (uint32_t)zl::HASH_MASK;
 }
 
 // bytes w[p .. p + 3] (little-endian) from two aligned LDS words: one v_alignbyte
@@ -61,7 +67,7 @@ __device__ __forceinline__ uint32_t load4(const uint8_t* w, int p) {
 }
 
 // zlib's longest_match for the query at `strstart` (see the header comment); uniform in, uniform out
-__device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint32_t* keys, int i0, uint32_t h,
+__device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint16_t* spos, int i0, uint32_t h,
                                                   int strstart, int lookahead, int prev_length, int& match_start,
                                                   int lane) {
     const int chain_length = prev_length >= zl::GOOD ? zl::CHAIN >> 2 : zl::CHAIN;
@@ -73,10 +79,11 @@ __device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint
         const int idx = i0 - 1 - k;
         bool ok = k < chain_length && idx >= 0;
         int cand = 0;
-        if (ok) {
-            const uint32_t kk = keys[idx];
-            cand = (int)(kk & 0xFFFFu);
-            ok = (kk >> 16) == h && (k == 0 ? cand > 0 : cand > limit);
+        uint32_t w0 = 0;
+        if (ok) {  // the chain: earlier sorted positions while the hash (from the candidate's bytes) holds
+            cand = spos[idx];
+            w0 = load4(win, cand);
+            ok = hash_w(w0) == h && (k == 0 ? cand > 0 : cand > limit);
         }
         int len = 0;
         if (ok) {
@@ -85,7 +92,7 @@ __device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint
             // candidate only when bytes 0 and 1 match (byte 2 then matches by the hash): a shorter
             // prefix is no candidate.
             for (;;) {  // eight bytes per step: the four word reads of a step go out together
-                const uint32_t x0 = load4(win, strstart + len) ^ load4(win, cand + len);
+                const uint32_t x0 = load4(win, strstart + len) ^ (len ? load4(win, cand + len) : w0);
                 const uint32_t x1 = load4(win, strstart + len + 4) ^ load4(win, cand + len + 4);
                 if (x0) {
                     len += __builtin_ctz(x0) >> 3;
@@ -130,6 +137,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     const int n = na + nb;
     uint8_t* win = lds;
     uint32_t* keys = reinterpret_cast<uint32_t*>(lds + off_keys(nmax));
+    uint16_t* spos = reinterpret_cast<uint16_t*>(lds + off_keys(nmax));  // after the sort
     uint16_t* idx_of = reinterpret_cast<uint16_t*>(lds + off_idx(nmax));
     Trees& t = *reinterpret_cast<Trees*>(lds + off_trees(nmax));
     ZLW_T(tw0);
@@ -162,7 +170,16 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
             __syncthreads();
         }
     }
-    for (int i = lane; i < npos; i += 64) idx_of[keys[i] & 0xFFFFu] = (uint16_t)i;
+    // compact the sorted keys to positions in place: chunk c writes bytes [128 c, 128 c + 128),
+    // i.e. keys [32 c, 32 c + 32), all read by chunk c / 2 <= c (read, barrier, write)
+    for (int base = 0; base < npos; base += 64) {
+        const uint32_t kv = base + lane < npos ? keys[base + lane] : 0u;
+        __syncthreads();
+        if (base + lane < npos) spos[base + lane] = (uint16_t)(kv & 0xFFFFu);
+        __syncthreads();
+    }
+    // the second half of the region is free now: sorted index of every position
+    for (int i = lane; i < npos; i += 64) idx_of[spos[i]] = (uint16_t)i;
     if (lane == 0) init_block(t);
     __syncthreads();
     ZLW_T(tw2);
@@ -195,11 +212,11 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
         uint32_t v = 0, hq = 0;
         if (p < npos) {
             const int ii = idx_of[p];
-            hq = keys[ii] >> 16;
+            hq = hash3(win, p);
             uint32_t hh = 0;
             if (ii > 0) {
-                const uint32_t kp = keys[ii - 1];
-                if ((kp >> 16) == hq) hh = kp & 0xFFFFu;
+                const uint32_t q = spos[ii - 1];
+                if (hash3(win, (int)q) == hq) hh = q;
             }
             v = (uint32_t)ii | (hh << 16);
         }
@@ -226,7 +243,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
         prev_match = match_start;
         match_length = MIN_MATCH - 1;
         if (hash_head != 0 && prev_length < LAZY && strstart - hash_head <= MAX_DIST) {
-            match_length = coop_longest_match(win, keys, i0, hq, strstart, lookahead, prev_length, match_start, lane);
+            match_length = coop_longest_match(win, spos, i0, hq, strstart, lookahead, prev_length, match_start, lane);
             if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > TOO_FAR)
                 match_length = MIN_MATCH - 1;
         }
