@@ -1,4 +1,5 @@
-// Column-tiled trace-and-walk aligner for sequences of any length (Gotoh; the reference's
+// Column-tiled trace-and-walk aligner for sequences of any length (Gotoh, and with LIN the
+// Needleman-Wunsch fill Biopython uses when open == extend everywhere; the reference's
 // PairwiseAligner.Biopython.align has no length limit: src/itaxotools/taxi2/align.py:151-157).
 //
 // The other aligners hold a whole row of the DP in one workgroup's registers: 64 K W columns
@@ -32,11 +33,17 @@ struct LongPair {
     int nA, fx, lx, nB, fy, ly, ntile, fin;
 };
 
+// LIN (linear scores, oracle/restatement.py _nw): one DP value per cell, S(i, j) = max(D, V, H) with
+// D = S(i-1, j-1) + s, V = S(i-1, j) + (ee on the last column, else ie), H = S(i, j-1) + (ee on the
+// last row, else ie); the trace byte is the tie set D=1 | V=2 | H=4 of the cell, and each walk is
+// stateless: from (nA, nB), the first set move in H > V > D (orientation (x, y)) or V > H > D
+// (the (y, x) alignment), row 0 / column 0 forcing H / V -- align_kernel.hpp's NW priorities.
+//
 // Optional aligned strings (taxi2_align_strings for long pairs): when sx != nullptr every walk also
 // writes its alignment right-aligned into slot [p][prio] of sx / sy (cap bytes each: bytes
 // [nA + nB - len, nA + nB)) and len into slen[p][prio] -- prio 1 is the (y, x) alignment written
 // in (x, y) column order, as k_traceback does.  out == nullptr: no metrics.
-template <int K, int W, int OCC>
+template <int K, int W, int OCC, bool LIN>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int out_mode, double* __restrict__ out,
             int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes, uint2* __restrict__ bnd_all,
@@ -86,10 +93,10 @@ k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int
         wpos[lane] = lp[pb].nA + lp[pb].nB - 1;
         if (!have_prev || (lane == 1 && out_mode != OUT_BOTH)) return;
         W_.prio = lane;
-        W_.i = lp[pb].nA + 1;
-        W_.j = lp[pb].nB + 1;
+        W_.i = lp[pb].nA + (LIN ? 0 : 1);
+        W_.j = lp[pb].nB + (LIN ? 0 : 1);
         W_.st = AT_M;
-        W_.first = 1;
+        W_.first = LIN ? 0 : 1;
     };
     auto walk_run = [&](int pb, int target) {
         AtWalk& W_ = wks[lane < 2 ? lane : 0];
@@ -110,6 +117,58 @@ k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int
             if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target)
                 break;
             if (st == AT_DONE) continue;
+            if constexpr (LIN) {  // stateless NW walk: the move at (i, j) from its own tie set
+                uint32_t tb = 0;
+                if (i >= 1 && j >= 1) {
+                    const int t = (j - 1) / TC;
+                    const int jj = j - 1 - t * TC;
+                    const int l = jj / K;
+                    const int k = jj - l * K;
+                    const size_t s = (size_t)t * (size_t)(nA + 63) + (size_t)(i - 1 + (l & 63));
+                    tb = *(const volatile uint8_t*)(tr + (s * NT + l) * K + k);
+                }
+                // 0 = D, 1 = V (x against a gap), 2 = H (y against a gap)
+                const int mv = i == 0 ? 2
+                             : j == 0 ? 1
+                             : prio ? ((tb & 2u) ? 1 : (tb & 4u) ? 2 : 0)
+                                    : ((tb & 4u) ? 2 : (tb & 2u) ? 1 : 0);
+                xa = i >= 1 ? q.rseq[i - 1] : 0u;
+                yb = j >= 1 ? q.cseq[j - 1] : 0u;
+                if (ox) {
+                    ox[pos] = mv == 2 ? (uint8_t)'-' : (uint8_t)xa;
+                    oy[pos] = mv == 1 ? (uint8_t)'-' : (uint8_t)yb;
+                    --pos;
+                }
+                if (mv == 0) {
+                    const int bx = base_code(xa), by = base_code(yb);
+                    if (bx < 4 && by < 4) {
+                        ++valid;
+                        const int dd = bx ^ by;
+                        ts += dd == 2;
+                        tv += (dd != 0) & (dd != 2);
+                    }
+                    --i;
+                    --j;
+                } else if (mv == 1) {
+                    if (base_code(xa) < 4 && j - 1 >= fy && j <= ly) ++gap;
+                    --i;
+                } else {
+                    if (base_code(yb) < 4 && i - 1 >= fx && i <= lx) ++gap;
+                    --j;
+                }
+                if (i == 0 && j == 0) {
+                    const int64_t p = q.p;
+                    if (out) {
+                        double* o = out_mode == OUT_BOTH ? out + (p * 2 + prio) * nm : out + p * nm;
+                        for (int m = 0; m < nm; ++m)
+                            o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
+                    }
+                    if (slen) slen[p * 2 + prio] = q.nA + q.nB - 1 - pos;
+                    if (sout && !prio) sout[p] = q.fin >> 1;
+                    st = AT_DONE;
+                }
+                continue;
+            }
             int ni, nj;
             if (ox && !first) {  // this column of the alignment, written right to left
                 ox[pos] = st == AT_IY ? (uint8_t)'-' : (uint8_t)xa;
@@ -333,7 +392,7 @@ k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int
                                         stG[k] = sc.eo + sc.ee * (jb + k);
                                         stX[k] = NEG_INF;
                                     }
-                                    carry = jb == 0 ? 1 : sc.eo + sc.ee * (jb - 1);
+                                    carry = jb == 0 ? (LIN ? 0 : 1) : sc.eo + sc.ee * (jb - 1);
                                 }
                                 const uint32_t ec = (xi >> 11) & 7u;
                                 const uint32_t eqlo = (ec & 1u) ? eqp1 : eqp0;
@@ -352,6 +411,23 @@ k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int
                                 int d = carry;
                                 int F = inF, Y = inY;
                                 uint32_t acc[K / 4];
+                                if constexpr (LIN) {  // NW: S only (stG), F = S(i, j - 1)
+#pragma unroll
+                                    for (int k = 0; k < K; ++k) {
+                                        const int U = stG[k];
+                                        const uint32_t e = (eq >> (3 * k)) & 7u;
+                                        const int Dv = d + (e ? sc.ma : sc.mi);
+                                        const int Vv = U + colc[k][tid].y;
+                                        const int Hv = F + ey;
+                                        const int S = max(Dv, max(Vv, Hv));
+                                        const uint32_t tset = (Dv == S ? 1u : 0u) | (Vv == S ? 2u : 0u) | (Hv == S ? 4u : 0u);
+                                        uint32_t a = k % 4 == 0 ? 0u : acc[k / 4];
+                                        acc[k / 4] = push_bits<8>(a, (int)tset);
+                                        stG[k] = S;
+                                        F = S;
+                                        d = U;
+                                    }
+                                } else
 #pragma unroll
                                 for (int k = 0; k < K; ++k) {
                                     const int G = stG[k], X = stX[k];
@@ -395,14 +471,14 @@ k_alignlong(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int
                                         eG = (int)(((uint32_t)stG[k] & m) | ((uint32_t)eG & ~m));
                                         eX = (int)(((uint32_t)stX[k] & m) | ((uint32_t)eX & ~m));
                                     }
-                                    lp[cur].fin = max(eG, eX);
+                                    lp[cur].fin = LIN ? eG : max(eG, eX);
                                 }
                             }
                             if (W > 1 && ring_out != nullptr && lane == 63)
                                 ring_out[(g + 1) & (RING - 1)] = make_uint2((uint32_t)payF, (uint32_t)payY);
                             if (w == W - 1 && lane == 63 && g >= 0 && g < nA && tile + 1 < q.ntile)
                                 bnd[g] = make_uint2((uint32_t)payF, (uint32_t)payY);  // hand-off to tile + 1
-                            carry = max(inF, inY);
+                            carry = LIN ? inF : max(inF, inY);
                         }
                     }
                 }

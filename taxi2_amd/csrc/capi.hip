@@ -539,34 +539,39 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
 // ---------------------------------------------------------------- column-tiled (any length)
 struct VariantL {
     int K, W, occ;
+    bool lin;
     const void* fn;
     void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int, double*, int32_t*,
                    uint8_t*, int64_t, uint2*, int64_t, unsigned long long*, uint8_t*, uint8_t*, int32_t*, int);
 };
 
-template <int K, int W, int OCC>
+template <int K, int W, int OCC, bool LIN>
 void launch_alignlong(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                       int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, uint2* bnd, int64_t brows,
                       unsigned long long* nx, uint8_t* sx, uint8_t* sy, int32_t* slen, int cap) {
-    hipLaunchKernelGGL((k_alignlong<K, W, OCC>), g, b, 0, st, x, y, ps, sc, ms, om, out, so, tr, bb, bnd, brows, nx,
+    hipLaunchKernelGGL((k_alignlong<K, W, OCC, LIN>), g, b, 0, st, x, y, ps, sc, ms, om, out, so, tr, bb, bnd, brows, nx,
                        sx, sy, slen, cap);
 }
 
-#define T2_VARIANTL(K, W, OCC) VariantL{K, W, OCC, (const void*)&k_alignlong<K, W, OCC>, &launch_alignlong<K, W, OCC>}
+#define T2_VARIANTL(K, W, OCC, LIN) \
+    VariantL{K, W, OCC, LIN, (const void*)&k_alignlong<K, W, OCC, LIN>, &launch_alignlong<K, W, OCC, LIN>}
 // tile widths 64 K W: 2 048 (production), 1 024 and 256 (TAXI2_LONG_TILE: tests cover many tiles
-// with short sequences)
-const VariantL kAlignLong[] = {T2_VARIANTL(8, 4, 2), T2_VARIANTL(8, 2, 2), T2_VARIANTL(4, 1, 2)};
+// with short sequences); Gotoh and linear (NW) scores
+const VariantL kAlignLong[] = {T2_VARIANTL(8, 4, 2, false), T2_VARIANTL(8, 2, 2, false), T2_VARIANTL(4, 1, 2, false),
+                               T2_VARIANTL(8, 4, 2, true),  T2_VARIANTL(8, 2, 2, true),  T2_VARIANTL(4, 1, 2, true)};
 
-// Gotoh pairs of any length (alignlong_kernel.hpp): rows = X sequences, columns = Y sequences.
+// Pairs of any length (alignlong_kernel.hpp): rows = X sequences, columns = Y sequences; Gotoh, or
+// Biopython's NW fill and traceback order when the scores are linear (open == extend).
 int launch_alignlong_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps, const KScores& k,
                            const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores, hipStream_t st,
                            uint8_t* sx = nullptr, uint8_t* sy = nullptr, int32_t* slen = nullptr, int cap = 0) {
     if (ps.count <= 0) return 0;
-    const VariantL* v = &kAlignLong[0];
+    const bool lin = is_linear(k);
+    const VariantL* v = lin ? &kAlignLong[3] : &kAlignLong[0];
     if (const char* t = getenv("TAXI2_LONG_TILE")) {
         const int tc = atoi(t);
         for (const auto& c : kAlignLong)
-            if (64 * c.K * c.W == tc) v = &c;
+            if (64 * c.K * c.W == tc && c.lin == lin) v = &c;
     }
     const int64_t TC = 64 * v->K * v->W;
     const int64_t rows = std::max(1, X.max_len), cols = std::max(1, Y.max_len);
@@ -611,11 +616,8 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
             return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     }
     // past every register-resident shape (and on request, TAXI2_LONG=1): the column-tiled aligner
-    if (max_len > 4095 || getenv("TAXI2_LONG")) {
-        if (is_linear(k))
-            return fail(ctx, "sequence length %d: linear (open == extend) scores are aligned up to 4095 bp", max_len);
+    if (max_len > 4095 || getenv("TAXI2_LONG"))
         return launch_alignlong_pairs(ctx, X, Y, ps, k, ms, out_mode, d_out, d_scores, st);
-    }
     const Variant* v = pick_variant(k, max_len);
     if (!v) return fail(ctx, "sequence length %d exceeds the aligner's column capacity", max_len);
     // int DP range check: every finite (doubled, tie-tagged) score stays far above NEG_INF
@@ -732,7 +734,6 @@ struct Tracer {
         cap = cap_;
         longp = max_len > 4095 || getenv("TAXI2_LONG");
         if (longp) {  // strings from k_alignlong's walkers: only the index and output staging
-            if (lin) return fail(ctx, "aligned strings past 4095 bp need Gotoh (open != extend) scores");
             chunk = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 30) / (4 * (int64_t)std::max(cap, 1))));
             HIP_TRY(ctx, hipMalloc(&d_idx, (size_t)chunk * 2 * sizeof(int64_t)));
             HIP_TRY(ctx, hipMalloc(&d_out, (size_t)chunk * 2 * cap * 2));

@@ -40,7 +40,7 @@ def _env(env: dict, fn):
 LONG256 = {"TAXI2_LONG": "1", "TAXI2_LONG_TILE": "256"}
 
 
-@pytest.mark.parametrize("scores", ["default", "generic"])
+@pytest.mark.parametrize("scores", ["default", "generic", "linear"])
 @pytest.mark.parametrize("tile", ["256", "1024", "2048"])
 def test_tiled_triangle_small(engine, oracle_c, scores, tile):
     from taxi2_amd._native import tri_pairs
@@ -80,16 +80,17 @@ def test_tiled_rectangle_and_list(engine, oracle_c):
     rs.free()
 
 
-@pytest.mark.parametrize("length", [5000, 10000])
-def test_long_sequences(engine, oracle_c, length):
+@pytest.mark.parametrize("length,scores", [(5000, "default"), (10000, "default"), (5000, "linear")])
+def test_long_sequences(engine, oracle_c, length, scores):
     from taxi2_amd._native import tri_pairs
 
     fam = family_sequences(4, length, 0x51 + length, ancestors=2, max_sub=0.1, indel_rate=0.01)
     seqs = [fam[0], fam[1][: length - 300], fam[2], fam[3][: length // 2]]
     st = engine.upload(seqs, align=True)
     a, b = tri_pairs(len(seqs))
-    got, gsc = engine.all_pairs(st, 0, len(a), METRICS, None, with_scores=True)
-    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=SCORE_SETS["default"])
+    sc = SCORE_SETS[scores]
+    got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
     assert np.array_equal(gsc, esc)
     assert_metrics_equal(got, exp)
     st.free()
@@ -101,21 +102,23 @@ def test_tiled_aligned_strings_equal_traceback(engine):
     st = engine.upload(seqs, align=True)
     xs = np.array([0, 1, 2, 3, 4, 5, 10, 11, 0])
     ys = np.array([5, 6, 7, 8, 9, 0, 1, 10, 0])
-    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"]):
+    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"], SCORE_SETS["linear"]):
         ref = engine.align_strings(st, st, xs, ys, sc, both=True)
         got = _env(LONG256, lambda: engine.align_strings(st, st, xs, ys, sc, both=True))
         assert got == ref
     st.free()
 
 
-def test_long_aligned_strings_match_counters(engine, oracle_c):
+@pytest.mark.parametrize("scores", ["default", "linear"])
+def test_long_aligned_strings_match_counters(engine, oracle_c, scores):
     """Past 4 095 bp: the strings the walkers write have the columns the walks counted."""
     fam = family_sequences(3, 6000, 0x54, ancestors=1, max_sub=0.08, indel_rate=0.01)
     seqs = [fam[0], fam[1][:5500], fam[2]]
     st = engine.upload(seqs, align=True)
     xs, ys = np.array([0, 1, 0]), np.array([1, 2, 2])
-    strings = engine.align_strings(st, st, xs, ys, None, both=True)
-    aligned = engine.list_pairs(st, st, xs, ys, METRICS, None)
+    sc = SCORE_SETS[scores]
+    strings = engine.align_strings(st, st, xs, ys, sc, both=True)
+    aligned = engine.list_pairs(st, st, xs, ys, METRICS, sc)
     for k, pair in enumerate(strings):
         for o, (ax, ay) in enumerate(pair):
             assert ax.replace("-", "") == seqs[xs[k]] and ay.replace("-", "") == seqs[ys[k]]
