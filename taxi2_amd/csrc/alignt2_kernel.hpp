@@ -67,6 +67,11 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
     for (size_t k = threadIdx.x; k < bytes / 4; k += blockDim.x) w[k] = AT_POISON_LDS;
 }
 
+// 1: a step whose wave has no lane inside the trace band skips the trace-code arithmetic
+// (bit-identical; 0 builds the always-encode variant for A/B runs)
+#ifndef A2_SKIP_OUT_OF_BAND
+#define A2_SKIP_OUT_OF_BAND 1
+#endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
 #endif
@@ -590,7 +595,8 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                             // j0 <= nB).  The lane mask is formed here, a whole cell block ahead of the
                             // store, so the exec-mask update there never waits on the compare.
                             const bool in_band = (uint16_t)((uint16_t)tq - (uint16_t)rec.y) <= (uint16_t)(rec.y >> 16);
-                            asm volatile("" ::"s"(__builtin_amdgcn_ballot_w64(in_band)));
+                            const uint64_t bmask = __builtin_amdgcn_ballot_w64(in_band);
+                            asm volatile("" ::"s"(bmask));
                             const uint32_t rw = rec.x;
                             (void)AT_OK(rw != AT_POISON_LDS, AG_ROW_POISON);
                             uint32_t inF, inY;
@@ -678,6 +684,10 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 at_s2 d1 = as_s2(carry);
                                 at_s2 F1 = as_s2(inF), Y = as_s2(inY);
                                 uint32_t acc[KW];
+                                // TR = false: no lane of the wave stores this step's trace (every block is
+                                // outside both streams' bands), so the trace codes are not formed at all --
+                                // the same cells, ~13 fewer VALU instructions per cell pair
+                                auto cells = [&](auto TR) {
     #pragma unroll
                                 for (int k = 0; k < K; ++k) {
                                     const at_s2 G = as_s2(stG[k]), X1 = as_s2(stX[k]);
@@ -694,6 +704,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     const at_s2 cf = padd32(F1, oy1i), cy = DEF ? Y : padd32(Y, eyi);
                                     const at_s2 Yn = pmax(cf, cy);
                                     const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
+                                    if constexpr (decltype(TR)::value) {
                                     // byte = 16 (4 sc + sb) + 4 sa + tags, built as two multiply-adds: the
                                     // tags ride in the addend (tagG = bit 0 of Gn; default scores store no
                                     // tagF, it is implied, see the walker)
@@ -708,15 +719,18 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     }
                                     if (k % 2 == 0) acc[k / 2] = code;
                                     else acc[k / 2] = __builtin_amdgcn_perm(code, acc[k / 2], 0x06040200u);
+                                    }
                                     stG[k] = as_u32(Gn);
                                     stX[k] = as_u32(Xn1);
                                     F1 = Fn1;
                                     Y = Yn;
                                     d1 = nd1;
                                 }
-                                const at_s2 F = F1;
-                                payF = as_u32(F);
-                                payY = as_u32(Y);
+                                };
+                                if (A2_SKIP_OUT_OF_BAND && !bmask) {
+                                    cells(std::false_type{});
+                                } else {
+                                cells(std::true_type{});
                                 if (in_band &&
                                     AT_OK(((size_t)s * NT + tq + 1) * (2 * K) <= (size_t)buf_bytes, AG_STORE)) {
                                     // 32-bit offset from the uniform buffer base (one VGPR, saddr store; a
@@ -733,6 +747,10 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         for (int q = 0; q < KW; ++q) dst[q] = acc[q];
                                     }
                                 }
+                                }
+                                const at_s2 F = F1;
+                                payF = as_u32(F);
+                                payY = as_u32(Y);
                                 if constexpr (decltype(HO)::value)
                                     if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
                                 if ((rw & (A2_LAST | (A2_LAST << 16))) && tq == (nB - 1) / K) {  // owner of column nB

@@ -16,7 +16,8 @@ Method.
   other than A/C/G/T, the owner of column nB on a pair's last row) run once per pair or never.
 * The trace block (byte packing + the 16-byte store, behind the band's lane mask) runs only on
   the steps where some lane of the wave meets the stored strip: it is priced with weight
-  band_store_fraction() (the fraction of (fill wave, step) pairs of a config-3 chain with a lane
+  band_store_fraction(); with the out-of-band skip (split_skip) the whole trace-forming cell
+  block has that weight and the no-trace cell block the rest (the fraction of (fill wave, step) pairs of a config-3 chain with a lane
   in the strip; 1.0 with --band 0).
 * Each VALU opcode (suffixes _e32 / _e64 / _dpp / _sdwa stripped) gets the SIMD cycles per wave64
   instruction measured at 8 waves per SIMD in valu_peak.txt; an opcode the microbenchmark does
@@ -127,6 +128,43 @@ def hot_instructions(body: list[str]) -> tuple[list[str], list[str]]:
     return out, store
 
 
+def split_skip(body: list[str], kernel: list[str], a: int):
+    """The out-of-band skip (alignt2_kernel.hpp A2_SKIP_OUT_OF_BAND): a wave-uniform
+    `s_cbranch_scc0/scc1 L` to an out-of-line stub (outside the loop) that `s_branch`es back to the
+    in-line no-trace cells; the fall-through is the trace-forming cells + store, which end with
+    `s_cbranch_execnz J` over the no-trace cells to the common tail at J.  Returns
+    (prefix, trace_variant, no_trace_variant, tail) instruction-line lists, or None without it."""
+    labels = {}
+    for i, l in enumerate(kernel):
+        m = re.match(r"^(\.LBB\w+):", l)
+        if m:
+            labels[m.group(1)] = i
+    for i, l in enumerate(body):
+        m = re.match(r"^\s+s_cbranch_scc[01]\s+(\.LBB\w+)", l)
+        if not m or m.group(1) not in labels:
+            continue
+        out = labels[m.group(1)]
+        if a <= out < a + len(body):
+            continue
+        stub = []
+        for l2 in kernel[out + 1:]:
+            mb = re.match(r"^\s+s_branch\s+(\.LBB\w+)", l2)
+            if mb:
+                back = mb.group(1)
+                break
+            stub.append(l2)
+        else:
+            return None
+        b = next(k for k, x in enumerate(body) if x.startswith(back + ":"))
+        mj = next((re.match(r"^\s+s_cbranch_execnz\s+(\.LBB\w+)", x) for x in reversed(body[i:b])
+                   if re.match(r"^\s+s_cbranch_execnz", x)), None)
+        if mj is None:
+            return None
+        j = next(k for k, x in enumerate(body) if x.startswith(mj.group(1) + ":"))
+        return body[:i], body[i + 1:b], stub + body[b:j], body[j:]
+    return None
+
+
 def band_store_fraction(L: int, K: int, W: int, band: int, pairs: int) -> float:
     """Fraction of (fill wave, step) pairs of one chain (`pairs` pairs of L x L per stream, both
     streams alike) in which some lane's column block meets the stored strip of its row
@@ -186,19 +224,34 @@ def main() -> None:
     L, K, W, P = (int(x) for x in args.shape.split(","))
     f = band_store_fraction(L, K, W, args.band, P)
     for a, b in step_loops(body):
-        hot, store = hot_instructions(body[a:b + 1])
-        hot = [op for op in hot if op.startswith("v_")]
-        store = [op for op in store if op.startswith("v_")]
-        hist = Counter(base_op(op) for op in hot)
-        shist = Counter(base_op(op) for op in store)
-        cyc = sum(price(op, costs, unlisted) for op in hot) + f * sum(price(op, costs, unlisted) for op in store)
-        n = len(hot) + f * len(store)
-        loops.append({"lines": [start + a + 1, start + b + 1], "hot_valu": len(hot), "trace_block_valu": len(store),
-                      "trace_block_weight": f, "cycles": cyc, "mean_cyc": cyc / max(1e-9, n),
+        sk = split_skip(body[a:b + 1], body, a)
+        if sk is None:  # one variant: hot blocks weight 1, the trace store block weight f
+            hot, store = hot_instructions(body[a:b + 1])
+            segs = [(hot, 1.0), (store, f)]
+            skip_valu = 0
+        else:  # prefix + tail weight 1; trace cells + store weight f; no-trace cells weight 1 - f
+            pre, tr, nt, tail = sk
+            h_pre, s_pre = hot_instructions(pre)
+            h_tr, s_tr = hot_instructions(tr)
+            h_nt, _ = hot_instructions(nt)
+            h_tl, s_tl = hot_instructions(tail)
+            hot = h_pre + h_tl
+            store = s_pre + h_tr + s_tr + s_tl
+            segs = [(hot, 1.0), (store, f), (h_nt, 1.0 - f)]
+            skip_valu = sum(1 for op in h_nt if op.startswith("v_"))
+        segs = [([op for op in ops if op.startswith("v_")], wgt) for ops, wgt in segs]
+        hist = Counter(base_op(op) for op in segs[0][0])
+        shist = Counter(base_op(op) for op in segs[1][0])
+        cyc = sum(wgt * sum(price(op, costs, unlisted) for op in ops) for ops, wgt in segs)
+        n = sum(wgt * len(ops) for ops, wgt in segs)
+        loops.append({"lines": [start + a + 1, start + b + 1], "hot_valu": len(segs[0][0]),
+                      "trace_block_valu": len(segs[1][0]), "trace_block_weight": f,
+                      "no_trace_block_valu": skip_valu, "no_trace_block_weight": (1.0 - f) if skip_valu else 0.0,
+                      "cycles": cyc, "mean_cyc": cyc / max(1e-9, n),
                       "histogram": dict(hist.most_common()), "trace_block_histogram": dict(shist.most_common())})
-        hot_all.update(hist)
-        for op, c in shist.items():
-            hot_all[op] += f * c
+        for ops, wgt in segs:
+            for op in ops:
+                hot_all[base_op(op)] += wgt
     n_all = sum(hot_all.values())
     cyc_all = sum(price(op, costs, Counter()) * c for op, c in hot_all.items())
     mean_cyc = cyc_all / n_all
