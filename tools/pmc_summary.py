@@ -34,6 +34,7 @@ def main() -> None:
     ap.add_argument("dst")
     ap.add_argument("--tag", required=True)
     ap.add_argument("--batch", type=int, default=524288)
+    ap.add_argument("--band", type=int, default=95, help="trace band of the profiled run")
     args = ap.parse_args()
     src, dst = Path(args.src), Path(args.dst)
     dst.mkdir(parents=True, exist_ok=True)
@@ -46,18 +47,19 @@ def main() -> None:
     kernels = sorted(set(fetch) | set(write))
     per = {k: {"fetch_kb": fetch.get(k, {}).get("FETCH_SIZE", 0.0), "write_kb": write.get(k, {}).get("WRITE_SIZE", 0.0)}
            for k in kernels}
-    total_kb = sum(v["fetch_kb"] + v["write_kb"] for v in per.values())
+    # gfx950: FETCH_SIZE tallies each 128-B request as 64 B (MI355X_MICROARCH.md HBM section): x 2
+    total_kb = sum(2.0 * v["fetch_kb"] + v["write_kb"] for v in per.values())
     rec = {
         "workload": "config3",
         "batch": args.batch,
         "kernels": per,
         "hbm_bytes_per_launch": total_kb * 1024.0,
         "source": f"profiles/{dst.name}/pmc_fetch_{args.tag}.csv, pmc_write_{args.tag}.csv",
-        "note": "FETCH_SIZE + WRITE_SIZE (KB) x 1024 from separate rocprofv3 --pmc passes over one launch of the "
-                "bench command (--steps 1 --warmup 0), summed over the path's kernels.  k_alignt writes one trace "
-                "byte per DP cell (~1.06 MB per 1 000 bp pair, 8-byte coalesced stores per lane and step; "
-                "WRITE_SIZE is exact for such streams) and its walker reads ~2 x 1 100 single bytes per pair "
-                "(64-B line fetches, uncalibrated width: FETCH_SIZE reported uncorrected).",
+        "note": "WRITE_SIZE (KB) x 1024: exact for the 16-B-per-lane trace stores (MI355X_MICROARCH.md HBM "
+                "section). FETCH_SIZE (KB) x 1024 x 2: gfx950 tallies each 128-B request as 64 B (same section); "
+                "the walker's reads are single-byte gathers whose lines this counts once each.  Separate "
+                "rocprofv3 --pmc passes over one launch of bench.py --steps 1 --warmup 0.",
+        "trace_band": args.band,
     }
     (ROOT / "profiles/pmc_traffic.json").write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec, indent=1))
