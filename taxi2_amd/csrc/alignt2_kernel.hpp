@@ -42,8 +42,9 @@ typedef short at_s2 __attribute__((ext_vector_type(2)));
 // on the first launch of a process instead of depending on what earlier kernels left behind:
 // every LDS array at kernel start and the row ring / wave ring at every chain start (0xA5 bytes;
 // a row record, ring entry or walk state still holding the pattern when read sets a code), and
-// the chain's trace buffer before its fill (0x7F bytes: outside the valid trace-byte range
-// [-88, 87], so the walker flags any byte the fill of ITS chain did not store).
+// the chain's trace buffer before its fill (0x64 bytes: outside the valid trace-byte ranges --
+// [-88, 87] for the tagF layout, [-22, 21] or that + 128 for the default-score layout -- so the
+// walker flags any byte the fill of ITS chain did not store).
 #ifdef TAXI2_GUARD
 __device__ unsigned int at_guard_err;
 #define AT_OK(cond, code) ((cond) ? true : (atomicOr(&at_guard_err, (unsigned)(code)), false))
@@ -118,6 +119,21 @@ __device__ __forceinline__ at_s2 pmad4(at_s2 a, at_s2 b) {
     uint32_t r;
     asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)));
     return as_s2(r);
+}
+// per half a * 8 + b
+__device__ __forceinline__ at_s2 pmad8(at_s2 a, at_s2 b) {
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, 8, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(as_u32(a)), "v"(as_u32(b)));
+    return as_s2(r);
+}
+// Default-score trace byte: (128 tagG + 16 sc + 4 sb + sa) mod 256, digits in [-2, 1] (sc, sb in
+// [-1, 1]), built by three multiply-adds from Gn (whose bit 0 is tagG: 128 Gn mod 256 = 128 tagG).
+// Code t = 16 sc + 4 sb + sa lies in [-22, 21], so tag 0 bytes are t (as int8) and tag 1 bytes are
+// t + 128: an int8 outside [-22, 21] means tag 1 and t = (int8)(byte ^ 0x80).
+__device__ __forceinline__ int at_dec_def(uint32_t b, bool& tag) {
+    const int x = (int)(int8_t)(uint8_t)b;
+    tag = x < -22 || x > 21;
+    return tag ? (int)(int8_t)(uint8_t)(b ^ 0x80u) : x;
 }
 // per half a * 16 + b
 __device__ __forceinline__ uint32_t pmad16(at_s2 a, uint32_t b) {
@@ -371,18 +387,24 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 const size_t off = ((size_t)s * NT + t) * (2 * K) + 2 * k + sm;
                 if (AT_OK(off < (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace(tr - sm + off);
                 // guard build: the fill of this chain stored every byte the walk reads
-                (void)AT_OK(esc || ((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87), AG_TRACE_POISON);
+                (void)AT_OK(esc || (DEF ? ((int)(int8_t)(uint8_t)nb >= -22 && (int)(int8_t)(uint8_t)nb <= 21) ||
+                                              ((int)(int8_t)(uint8_t)(nb ^ 0x80u) >= -22 && (int)(int8_t)(uint8_t)(nb ^ 0x80u) <= 21)
+                                        : ((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87)),
+                            AG_TRACE_POISON);
             }
             xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, AG_ROWSEQ)) ? a2_load_byte(rs + ni - 1) : 0u;
             yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, AG_COLSEQ)) ? a2_load_byte(cs + nj - 1) : 0u;
             // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa, digits sa in [-2, 1],
             // sb, sc in [-1, 1] (balanced base 4: u = code + 22 has digits sa + 2, sb + 1, sc + 1)
-            const int nu = ((int)(int8_t)(uint8_t)nb >> 2) + 22;
-            const int cu = ((int)(int8_t)(uint8_t)cb >> 2) + 22;
+            // (default scores: the byte is the code itself with tagG as its 128 bit, at_dec_def)
+            bool tagG, ctag;
+            const int nu = (DEF ? at_dec_def(nb, tagG) : ((int)(int8_t)(uint8_t)nb >> 2)) + 22;
+            const int cu = (DEF ? at_dec_def(cb, ctag) : ((int)(int8_t)(uint8_t)cb >> 2)) + 22;
+            (void)ctag;
+            if (!DEF) tagG = nb & 1u;
             // class of (ni, nj) from sa = clamp(G - X1, -2, 1) and tagG (X1 = 2 Ix + 1, G tagged):
             // 1 -> M if tagG else Iy; 0 -> M (M = Ix); -1 -> Ix = Iy tie; -2 -> Ix
             const int sa = (nu & 3) - 2;
-            const bool tagG = nb & 1u;
             const bool clsM = sa == 0 || (sa == 1 && tagG);
             int nst;
             if (ni == 0) {
@@ -520,7 +542,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 if constexpr (!IS_W) {
                     uint4* tb = (uint4*)(bufs + (size_t)cur * (size_t)buf_bytes);
                     const size_t nv = ((size_t)(max(rows0, rows1) + 63) * NT * (2 * K) + 15) / 16;
-                    const uint4 pz = make_uint4(0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu);
+                    const uint4 pz = make_uint4(0x64646464u, 0x64646464u, 0x64646464u, 0x64646464u);
                     for (size_t v = tid; v < nv && AT_OK(v * 16 + 16 <= (size_t)buf_bytes, AG_STORE); v += NT) tb[v] = pz;
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -705,15 +727,14 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     const at_s2 Yn = pmax(cf, cy);
                                     const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
                                     if constexpr (decltype(TR)::value) {
-                                    // byte = 16 (4 sc + sb) + 4 sa + tags, built as two multiply-adds: the
-                                    // tags ride in the addend (tagG = bit 0 of Gn; default scores store no
-                                    // tagF, it is implied, see the walker)
-                                    const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
-                                    const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
                                     uint32_t code;
-                                    if constexpr (DEF) {  // tagF is implied (see the walker): one v_bfi
-                                        code = (as_u32(Gn) & 0x00010001u) | (t4 & ~0x00010001u);
-                                    } else {  // tagF = M >= Ix  <=>  M - X1 >= 0 (both odd)
+                                    if constexpr (DEF) {
+                                        // tagF is implied (see the walker); byte = 128 tagG + 16 sc + 4 sb + sa:
+                                        // three multiply-adds starting from Gn (at_dec_def)
+                                        code = as_u32(pmad4(pmad4(pmad8(Gn, psign(cf - cy)), psign(cg - cx)), pclamp21(Gn - Xn1)));
+                                    } else {  // byte = 4 (16 sc + 4 sb + sa) + tags; tagF = M >= Ix  <=>  M - X1 >= 0 (both odd)
+                                        const at_s2 t2 = pmad4(pmad4(psign(cf - cy), psign(cg - cx)), pclamp21(Gn - Xn1));
+                                        const uint32_t t4 = as_u32(t2 << (at_s2){2, 2});
                                         const uint32_t ge = ~as_u32(M - Xn1) >> 14;  // bit 15 / 31 -> bit 1 / 17
                                         code = t4 | (as_u32(Gn) & 0x00010001u) | (ge & 0x00020002u);
                                     }
