@@ -48,6 +48,19 @@ constexpr int UNROLL = 32;  // asm blocks per loop iteration (256 measured instr
                  : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3])                                                \
                  : "v"(cq))
 
+// SDWA form (the packed aligner's substitution add: one 16-bit word added into the high half)
+#define CH8_S(INS)                                                                                               \
+    asm volatile(INS " %0, %0, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+                 INS " %1, %1, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+                 INS " %2, %2, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+                 INS " %3, %3, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+                 INS " %4, %4, %8 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t" \
+                 INS " %5, %5, %8 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t" \
+                 INS " %6, %6, %8 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t" \
+                 INS " %7, %7, %8 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1"      \
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]) \
+                 : "v"(c))
+
 // instruction table: name, form (2 = dst,src0,src1; 3 = three sources; 1 = mov; v = with vcc; 6 = 64-bit pair)
 #define VALU_LIST(X)                                                                                             \
     X(0, "v_add_f32", 2) X(1, "v_add_u32", 2) X(2, "v_sub_u32", 2) X(3, "v_max_i32", 2) X(4, "v_min_u32", 2)     \
@@ -59,12 +72,14 @@ constexpr int UNROLL = 32;  // asm blocks per loop iteration (256 measured instr
     X(26, "v_add3_u32", 3) X(27, "v_perm_b32", 3) X(28, "v_bfi_b32", 3) X(29, "v_alignbit_b32", 3)              \
     X(30, "v_bfe_u32", 3) X(31, "v_lshl_add_u32", 3) X(32, "v_and_or_b32", 3) X(33, "v_pk_mad_u16", 3)          \
     X(34, "v_pk_fma_f16", 3) X(35, "v_mad_u32_u24", 3) X(36, "v_pk_add_f32", 6) X(37, "v_pk_mul_f32", 6)       \
-    X(38, "v_max_u16", 2) X(39, "v_add_u16", 2) X(40, "v_max_f16", 2) X(41, "v_cvt_f32_i32", 1)
+    X(38, "v_max_u16", 2) X(39, "v_add_u16", 2) X(40, "v_max_f16", 2) X(41, "v_cvt_f32_i32", 1)               \
+    X(42, "v_add_u32_sdwa", s)
 #define FORM_2(INS) CH8(INS)
 #define FORM_3(INS) CH8_3(INS)
 #define FORM_1(INS) CH8_1(INS)
 #define FORM_v(INS) CH8_V(INS)
 #define FORM_6(INS) CH4_64(INS)
+#define FORM_s(INS) CH8_S(INS)
 
 template <int MODE>
 __global__ void __launch_bounds__(256) k_valu(unsigned* out, unsigned long long* cyc, int iters, unsigned seed) {
