@@ -4,6 +4,9 @@
   config2: versusAll, pre-aligned p / jc / k2p.  samples/Taxi2test1_ca9000.tab is missing from the
            reference; stand-in = 9 000 synthetic pre-aligned 600-column rows
            (lowercase acgt, 2 % '-' runs, 0.5 % 'n'), the full 4.05e7-pair space.
+  config5: versusAll pre-aligned p / jc / k2p at FULL size on one GPU: N = 200 000 synthetic
+           1 000-column rows (seed 0x7A14), all 2.0e10 unordered pairs in 2^26-pair blocks whose
+           outputs are overwritten in HBM (the multi-GPU task streams such blocks to rank 0, §6).
   config4: versusReference, align + p (closest reference per query, extras p-gaps / jc / k2p for
            the argmin pair), Q x R with R = 10 000 references of 650 bp (seed 0x7A13 generator);
            a Q slice is timed and pairs/s = Q_slice x R / time (the full 1e6 x 1e4 job scales
@@ -11,7 +14,7 @@
 
 Prints one JSON line per workload.  Inputs are uploaded before timing; outputs stay on the GPU
 (config2) or come back as the closest-pair vectors (config4, what the task consumes).
-usage: python tools/bench_configs.py [--config2] [--config4] [--q-slice 1024]
+usage: python tools/bench_configs.py [--config2] [--config4] [--config5] [--q-slice 1024]
 """
 
 from __future__ import annotations
@@ -68,6 +71,33 @@ def config2(eng, steps: int) -> dict:
             "algorithmic_GBps": total * bp / dt / 1e9, "hbm_frac": total * bp / dt / 8e12}
 
 
+def config5(eng) -> dict:
+    import torch
+
+    n, L = 200_000, 1000
+    buf, offs = prealigned_rows(n, L, 0x7A14)
+    st = eng.upload_packed(buf, offs, align=False)
+    del buf
+    total = n * (n - 1) // 2
+    metrics = ("p", "jc", "k2p")
+    B = 1 << 26
+    out = torch.empty((B, len(metrics)), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.Stream()
+    eng.all_pairs_dev(st, 0, B, metrics, out.data_ptr(), None, None, stream.cuda_stream)
+    stream.synchronize()
+    t0 = time.perf_counter()
+    for k0 in range(0, total, B):
+        c = min(B, total - k0)
+        eng.all_pairs_dev(st, k0, c, metrics, out.data_ptr(), None, None, stream.cuda_stream)
+    stream.synchronize()
+    dt = time.perf_counter() - t0
+    bp = 2 * ((L + 3) // 4) + 8 * len(metrics)
+    return {"workload": "config5 pre-aligned at full size: versusAll 200 000 x 1 000 pre-aligned, p/jc/k2p, "
+                        "all unordered pairs on ONE GPU (outputs overwritten per 2^26-pair block)",
+            "pairs": total, "seconds": dt, "pairs_per_s": total / dt,
+            "algorithmic_GBps": total * bp / dt / 1e9, "hbm_frac": total * bp / dt / 8e12}
+
+
 def config4(eng, q_slice: int, steps: int) -> dict:
     from taxi2_amd.synth import family_sequences
 
@@ -92,10 +122,11 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config2", action="store_true")
     ap.add_argument("--config4", action="store_true")
+    ap.add_argument("--config5", action="store_true")
     ap.add_argument("--q-slice", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=2)
     args = ap.parse_args()
-    if not (args.config2 or args.config4):
+    if not (args.config2 or args.config4 or args.config5):
         args.config2 = args.config4 = True
     import torch  # noqa: F401  -- before the engine: torch's bundled HIP runtime must load first
 
@@ -106,6 +137,8 @@ def main() -> None:
         print(json.dumps(config2(eng, args.steps)), flush=True)
     if args.config4:
         print(json.dumps(config4(eng, args.q_slice, args.steps)), flush=True)
+    if args.config5:
+        print(json.dumps(config5(eng)), flush=True)
 
 
 if __name__ == "__main__":
