@@ -14,8 +14,8 @@
 //
 // Per cell and pair the byte is (int8) (16 sc + 4 sb + sa) << 2 | tagF << 1 | tagG with the
 // signs sa = sign(G - X), sb = sign(cg - cx), sc = sign(cf - cy) of alignt_kernel.hpp (default
-// scores: no tagF, it follows from sa and tagG because opens <= extends; the packing is then one
-// v_bfi).  Bytes
+// scores: no tagF, it follows from sa and tagG because opens <= extends, and the byte is
+// (128 tagG + 16 sc + 4 sb + sa) mod 256, three multiply-adds from Gn: at_dec_def).  Bytes
 // are stored per lane and step as [k][stream] (2K bytes, one 16-byte store for K = 8).
 //
 // Substitution scores come from an LDS table eqt[base][thread][K/2] of 16-bit fields (the
