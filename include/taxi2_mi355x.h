@@ -123,6 +123,14 @@ int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q
                      const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* out,
                      int32_t* scores_out);
 
+/* Same with device-resident outputs on `stream` (NULL: the context's own), asynchronous.  The
+ * streamed versusAll feeds its x-major row blocks [x0, x1) x [0, N) from it in PREALIGNED mode
+ * (versus_all.py:732-773 drain order; set_q == set_r), where recomputing the block is cheaper
+ * than storing the triangle. */
+int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1,
+                         const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* d_out,
+                         int32_t* d_scores, void* stream);
+
 /* ---- explicit pair list (align.py:50-51 align_pairs, distances.py:297 calculate) ------- *
  * Pairs (xs[k] of set_x, ys[k] of set_y): out[count][2][nmetrics] in ALIGN mode
  * ([k][0] = (x, y), [k][1] = (y, x)), out[count][nmetrics] in PREALIGNED mode. */

@@ -38,6 +38,7 @@ EXPORTS = (
     "taxi2_all_pairs_dev",
     "taxi2_counts_metrics_dev",
     "taxi2_rect_pairs",
+    "taxi2_rect_pairs_dev",
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
@@ -95,6 +96,7 @@ _SIGNATURES = {
     "taxi2_all_pairs_dev": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
     "taxi2_counts_metrics_dev": (_INT, [_P, _P, _I64, _P, _INT, ctypes.c_double, _P, _P]),
     "taxi2_rect_pairs": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
+    "taxi2_rect_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
@@ -386,6 +388,21 @@ class Engine:
                 "taxi2_rect_pairs",
             )
         return (out, sc_out) if with_scores else out
+
+    def rect_pairs_dev(self, q: SeqSet, r: SeqSet, q0: int, q1: int, metrics, out_ptr: int, scores=None,
+                       scores_ptr: int | None = None, stream: int | None = None) -> None:
+        """Asynchronous device-output rectangle: out[(q - q0) * R + r][M] (orientation (q, r))."""
+        codes = metric_codes(metrics)
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_rect_pairs_dev(
+                    self._ctx, q.id, r.id, int(q0), int(q1), ctypes.byref(cs), codes.ctypes.data, len(codes),
+                    ctypes.c_void_p(out_ptr), ctypes.c_void_p(scores_ptr) if scores_ptr else None,
+                    ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_rect_pairs_dev",
+            )
 
     def list_pairs(self, x: SeqSet, y: SeqSet, xs, ys, metrics, scores=None, *, with_scores=False):
         """Explicit pairs.  ALIGN: (count, 2, M) [(x,y), (y,x)]; else (count, M)."""

@@ -157,8 +157,38 @@ __host__ __device__ inline bool at_fits16(const KScores& k, int max_len) {
 // come from LDS structs, so the compiler cannot infer their space).  Trace bytes bypass the
 // vector L1 (the buffer was rewritten two chains ago).
 typedef const __attribute__((address_space(1))) uint8_t a2_gbyte;
+typedef const __attribute__((address_space(1))) uint32_t a2_gword;
 __device__ __forceinline__ uint32_t a2_load_byte(const uint8_t* p) { return *(a2_gbyte*)p; }
 __device__ __forceinline__ uint32_t a2_load_trace(const uint8_t* p) { return *(const volatile a2_gbyte*)p; }
+__device__ __forceinline__ uint32_t a2_load_trace32(const uint8_t* p) { return *(const volatile a2_gword*)p; }
+
+// Raw-difference trace (default scores, the band pass).  Instead of forming sign digits per cell
+// (3 subtracts, 3 clamps and 3 multiply-adds per column pair: ~45 % of the fill's issue cycles),
+// the fill stores two exact differences of the cell's own states per pair,
+//   D = Gn - Xn1   (G = max(M, Iy) tagged, Ix odd)   and   E = Fn1 - Yn   (F = max(M, Ix) odd),
+// as int8: one 32-bit subtract each over both halves and one v_perm per column gather the four
+// bytes (D lo, D hi, E lo, E hi).  Between the states of one cell these differences are bounded by
+// the scores (default scores: D in [-18, 34], E in [-17, 35] over every cell of the CPU model,
+// tools/proto_rawdiff.c), so the int8 is exact.  The high half's bytes carry the low half's borrow
+// (the subtract is 32-bit): the walker adds back (lo byte < 0).
+// What the walker derives from the NEXT cell's (D, E):
+//   tag      = D even  (Gn odd iff M won; Xn1 odd)          -- parity survives any wrap
+//   class    = clamp(D, -2, 1) with tag, as the sign-digit code's sa
+//   Ix(i, j) formed from (i-1, j):  sign(cg - cx) = sign(D + (1 - tag) + colc_j)
+//   Iy(i, j) formed from (i, j-1):  sign(cf - cy) = sign(E + oy1_i)
+// (colc_j = ox_j - dz, oy1_i = oy_i - dz - 1 as in the fill).  The walker also sums the score of
+// its moves; a walk whose sum differs from the fill's optimum (impossible while the differences
+// fit int8: any wrong decision leaves the optimal path strictly) queues its pair for the
+// sign-digit full-trace pass, like a walk that leaves the band.
+__device__ __forceinline__ void a2_raw_de(uint32_t w, int sm, int& d, int& e) {
+    if (sm == 0) {
+        d = (int)(int8_t)(uint8_t)w;
+        e = (int)(int8_t)(uint8_t)(w >> 16);
+    } else {
+        d = (int)(int8_t)(uint8_t)((w >> 8) + ((w >> 7) & 1u));
+        e = (int)(int8_t)(uint8_t)((w >> 24) + ((w >> 23) & 1u));
+    }
+}
 
 // Row records.  One 8-byte LDS entry per step row g holds both streams: .x = two 16-bit row
 // words (stream 0 low, stream 1 high), .y = the trace band of the row (below).  Row word bits:
@@ -228,13 +258,17 @@ __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab
     return make_uint2(w0 | (w1 << 16), y);
 }
 
-template <int K, int W, bool DEF>
+// RAW: the raw-difference trace (default scores; 4 K bytes per lane and step, [step][lane][k] words),
+// else the sign-digit code (2 K bytes per lane and step, [step][lane][k][stream] bytes)
+template <int K, int W, bool DEF, bool RAW>
 __device__ __forceinline__ void
 alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
              double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
              int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
              unsigned long long* __restrict__ esc_n) {
     static_assert(K % 2 == 0 && K <= 16, "16-bit score fields: K / 2 words per stream and base");
+    static_assert(!RAW || DEF, "the raw-difference bounds are those of the default scores");
+    constexpr int TB = RAW ? 4 * K : 2 * K;  // trace bytes per lane and step
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
     constexpr int KW = K / 2;
@@ -334,6 +368,8 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         int i = W_.i, j = W_.j, first = W_.first;
         uint32_t cb = W_.cb, xa = W_.xa, yb = W_.yb;
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
+        int sc2 = W_.sc2;
+        const int nA_ = cp.nA, nB_ = ch.nB;
         for (int h = 0; budget < 0 || h < budget; ++h) {
             if (!__any(st < AT_DONE)) break;
             if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
@@ -348,6 +384,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                         ts += dd == 2;
                         tv += (dd != 0) & (dd != 2);
                     }
+                    if constexpr (RAW) sc2 += xa == yb ? sc.ma : sc.mi;
                 }
                 ni = i - 1;
                 nj = j - 1;
@@ -361,6 +398,16 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 nj = j - 1;
             }
             first = 0;
+            if constexpr (RAW) {
+                if (ni == 0 && nj == 0) {  // the gap run (if any) opened at the start: end-gap open
+                    if (st != AT_M) sc2 += sc.eo;
+                    // the walked score must be the fill's optimum, else a decision was wrong
+                    if (sc2 != ((fin[pb][pi] + (nA_ + nB_) * dz) & ~1)) {
+                        st = AT_ESC;
+                        continue;
+                    }
+                }
+            }
             if (ni == 0 && nj == 0) {
                 const int64_t p = cp.p;
                 double* o;
@@ -384,16 +431,59 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 const int t = (nj - 1) / K;
                 const int k = nj - 1 - t * K;
                 const int s = r0 + ni - 1 + (t & 63);
-                const size_t off = ((size_t)s * NT + t) * (2 * K) + 2 * k + sm;
-                if (AT_OK(off < (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace(tr - sm + off);
-                // guard build: the fill of this chain stored every byte the walk reads
-                (void)AT_OK(esc || (DEF ? ((int)(int8_t)(uint8_t)nb >= -22 && (int)(int8_t)(uint8_t)nb <= 21) ||
-                                              ((int)(int8_t)(uint8_t)(nb ^ 0x80u) >= -22 && (int)(int8_t)(uint8_t)(nb ^ 0x80u) <= 21)
-                                        : ((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87)),
-                            AG_TRACE_POISON);
+                if constexpr (RAW) {
+                    const size_t off = ((size_t)s * NT + t) * TB + 4 * k;
+                    if (AT_OK(off + 4 <= (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace32(tr - sm + off);
+                    int dv_, ev_;
+                    a2_raw_de(nb, sm, dv_, ev_);
+                    // guard build: the poison (0x64 = 100) lies far outside the differences' range
+                    (void)AT_OK(esc || (dv_ >= -64 && dv_ <= 63 && ev_ >= -64 && ev_ <= 63), AG_TRACE_POISON);
+                } else {
+                    const size_t off = ((size_t)s * NT + t) * TB + 2 * k + sm;
+                    if (AT_OK(off < (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace(tr - sm + off);
+                    // guard build: the fill of this chain stored every byte the walk reads
+                    (void)AT_OK(esc || (DEF ? ((int)(int8_t)(uint8_t)nb >= -22 && (int)(int8_t)(uint8_t)nb <= 21) ||
+                                                  ((int)(int8_t)(uint8_t)(nb ^ 0x80u) >= -22 && (int)(int8_t)(uint8_t)(nb ^ 0x80u) <= 21)
+                                            : ((int)(int8_t)(uint8_t)nb >= -88 && (int)(int8_t)(uint8_t)nb <= 87)),
+                                AG_TRACE_POISON);
+                }
             }
             xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, AG_ROWSEQ)) ? a2_load_byte(rs + ni - 1) : 0u;
             yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, AG_COLSEQ)) ? a2_load_byte(cs + nj - 1) : 0u;
+            if constexpr (RAW) {
+                int dv, ev;
+                a2_raw_de(nb, sm, dv, ev);
+                const bool tg = !(dv & 1);  // Gn odd iff M won, Xn1 odd
+                const int sa = dv < -2 ? -2 : dv > 1 ? 1 : dv;
+                const bool clsM = sa == 0 || (sa == 1 && tg);
+                int nst;
+                if (ni == 0) {
+                    nst = AT_IY;
+                } else if (nj == 0) {
+                    nst = AT_IX;
+                } else if (st == AT_M) {  // best state of (ni, nj)
+                    nst = clsM ? AT_M : sa == 1 ? AT_IY : sa == -1 ? (prio ? AT_IY : AT_IX) : AT_IX;
+                } else if (st == AT_IX) {  // Ix(i, j) from (i-1, j): sign of (G | 1) + ox_j - X1 there
+                    const int sb = dv + (tg ? 0 : 1) + (j == nB_ ? sc.eo : sc.io) - dz;
+                    const bool gp = sb > 0 || (sb == 0 && (tg || prio));
+                    nst = gp ? (tg ? AT_M : AT_IY) : AT_IX;
+                } else {  // Iy(i, j) from (i, j-1): sign of F1 + oy1_i - Y there (tagF = class M, see below)
+                    const int scv = ev + (i == nA_ ? sc.eo : sc.io) - dz - 1;
+                    const bool fp = scv > 0 || (scv == 0 && (clsM || !prio));
+                    nst = fp ? (clsM ? AT_M : AT_IX) : AT_IY;
+                }
+                if (st == AT_IX) {  // gap moves: extend when the run continues, end scores on the edges
+                    const bool en = j == nB_ || j == 0;
+                    sc2 += nst == AT_IX ? (en ? sc.ee : sc.ie) : (en ? sc.eo : sc.io);
+                } else if (st == AT_IY) {
+                    const bool en = i == nA_ || i == 0;
+                    sc2 += nst == AT_IY ? (en ? sc.ee : sc.ie) : (en ? sc.eo : sc.io);
+                }
+                i = ni;
+                j = nj;
+                st = esc ? AT_ESC : nst;
+                continue;
+            }
             // byte: (int8) code << 2 | tags, code = 16 sc + 4 sb + sa, digits sa in [-2, 1],
             // sb, sc in [-1, 1] (balanced base 4: u = code + 22 has digits sa + 2, sb + 1, sc + 1)
             // (default scores: the byte is the code itself with tagG as its 128 bit, at_dec_def)
@@ -449,6 +539,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         W_.ts = ts;
         W_.tv = tv;
         W_.gap = gap;
+        W_.sc2 = sc2;
     };
 
     // The fill waves and the walker wave run separate copies of the chain loop (same barrier
@@ -541,7 +632,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 at_poison_lds(ring, sizeof ring);
                 if constexpr (!IS_W) {
                     uint4* tb = (uint4*)(bufs + (size_t)cur * (size_t)buf_bytes);
-                    const size_t nv = ((size_t)(max(rows0, rows1) + 63) * NT * (2 * K) + 15) / 16;
+                    const size_t nv = ((size_t)(max(rows0, rows1) + 63) * NT * TB + 15) / 16;
                     const uint4 pz = make_uint4(0x64646464u, 0x64646464u, 0x64646464u, 0x64646464u);
                     for (size_t v = tid; v < nv && AT_OK(v * 16 + 16 <= (size_t)buf_bytes, AG_STORE); v += NT) tb[v] = pz;
                 }
@@ -705,7 +796,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 // walker breaks them with the neighbour's tag (it reads that byte anyway).
                                 at_s2 d1 = as_s2(carry);
                                 at_s2 F1 = as_s2(inF), Y = as_s2(inY);
-                                uint32_t acc[KW];
+                                uint32_t acc[RAW ? K : KW];
                                 // TR = false: no lane of the wave stores this step's trace (every block is
                                 // outside both streams' bands), so the trace codes are not formed at all --
                                 // the same cells, ~13 fewer VALU instructions per cell pair
@@ -726,7 +817,13 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     const at_s2 cf = padd32(F1, oy1i), cy = DEF ? Y : padd32(Y, eyi);
                                     const at_s2 Yn = pmax(cf, cy);
                                     const at_s2 Gn = pmax(M, Yn), Fn1 = pmax(M, Xn1);
-                                    if constexpr (decltype(TR)::value) {
+                                    if constexpr (decltype(TR)::value && RAW) {
+                                        // D = Gn - Xn1, E = Fn1 - Yn over both halves with 32-bit subtracts
+                                        // (2.28 cycles, vs 4.09 for v_pk_sub); bytes D lo, D hi, E lo, E hi
+                                        const uint32_t dD = as_u32(Gn) - as_u32(Xn1);
+                                        const uint32_t dE = as_u32(Fn1) - as_u32(Yn);
+                                        acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
+                                    } else if constexpr (decltype(TR)::value) {
                                     uint32_t code;
                                     if constexpr (DEF) {
                                         // tagF is implied (see the walker); byte = 128 tagG + 16 sc + 4 sb + sa:
@@ -753,12 +850,19 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 } else {
                                 cells(std::true_type{});
                                 if (in_band &&
-                                    AT_OK(((size_t)s * NT + tq + 1) * (2 * K) <= (size_t)buf_bytes, AG_STORE)) {
+                                    AT_OK(((size_t)s * NT + tq + 1) * TB <= (size_t)buf_bytes, AG_STORE)) {
                                     // 32-bit offset from the uniform buffer base (one VGPR, saddr store; a
                                     // buffer is at most a few tens of MB)
-                                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tq) * (2u * K)));
+                                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tq) * (uint32_t)TB));
                                     if (tq == 0) AT_DIAG(2, 1);
-                                    if constexpr (K == 16) {
+                                    if constexpr (RAW && K % 4 == 0) {
+    #pragma unroll
+                                        for (int q = 0; q < K / 4; ++q)
+                                            ((uint4*)dst)[q] = make_uint4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                                    } else if constexpr (RAW) {
+    #pragma unroll
+                                        for (int q = 0; q < K / 2; ++q) ((uint2*)dst)[q] = make_uint2(acc[2 * q], acc[2 * q + 1]);
+                                    } else if constexpr (K == 16) {
                                         ((uint4*)dst)[0] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
                                         ((uint4*)dst)[1] = make_uint4(acc[4], acc[5], acc[6], acc[7]);
                                     } else if constexpr (K == 8) {
@@ -839,18 +943,20 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
           double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
           int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
           unsigned long long* __restrict__ esc_n) {
-    alignt2_body<K, W, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows, hops,
-                            next, band, esc_list, esc_n);
+    alignt2_body<K, W, DEF, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
+                                 hops, next, band, esc_list, esc_n);
 }
 // ... and the full-trace pass over the pairs it queued (ps.sel / ps.dcount): a kernel of its own
-// name, so a profile shows the second pass (normally empty) apart from the first
+// name, so a profile shows the second pass (normally empty) apart from the first.  It stores the
+// sign-digit code, which is exact for any scores, so a pair queued by a raw walk's score check
+// cannot fail again.
 template <int K, int W, bool DEF, int OCC>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2_queued(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
                  double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
                  int cap_rows, int hops, unsigned long long* __restrict__ next) {
-    alignt2_body<K, W, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows, hops,
-                            next, 0, nullptr, nullptr);
+    alignt2_body<K, W, DEF, false>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
+                                   hops, next, 0, nullptr, nullptr);
 }
 
 }  // namespace taxi2

@@ -26,6 +26,7 @@
 #include "common.hpp"
 #include "pack_kernels.hpp"
 #include "prealigned_kernel.hpp"
+#include "subset_kernels.hpp"
 #include "trace_kernel.hpp"
 
 using namespace taxi2;
@@ -66,6 +67,8 @@ struct taxi2_ctx {
     size_t d_bnd_bytes = 0;
     void* d_fmt = nullptr;  // text formatter staging
     size_t d_fmt_bytes = 0;
+    void* d_sub = nullptr;  // subset aggregation scratch (row partials, groups, worklist)
+    size_t d_sub_bytes = 0;
     void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
     void* d_zslabs = nullptr;
     int64_t z_threads = 0;
@@ -461,12 +464,14 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(cmax, atoi(c)));
     int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(cmax, ps.count / (grid * 8)));
     // two trace buffers per resident workgroup: shrink the chunk (hence the chain rows) until they
-    // fit the budget (TAXI2_AT_TRACE_GB, default 40 GB of the 288 GB HBM)
-    double budget_gb = 40.0;
+    // fit the budget (TAXI2_AT_TRACE_GB, default 40 GB of the 288 GB HBM; 80 GB for the packed
+    // default-score kernel, whose raw-difference trace takes 4 bytes per lane-column and step)
+    const bool raw = packed && v.def;  // alignt2_kernel.hpp: raw-difference trace in the band pass
+    double budget_gb = raw ? 80.0 : 40.0;
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     auto buf_bytes = [&](int64_t e) {
         const int64_t per_stream = packed ? (e + 1) / 2 : e;  // a stream takes every other pair of a chain
-        return at_buf_bytes((int)per_stream * std::max(1, max_len), packed ? 2 * v.K : v.K, v.W);
+        return at_buf_bytes((int)per_stream * std::max(1, max_len), packed ? (raw ? 4 : 2) * v.K : v.K, v.W);
     };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
     if (shared_acquire(ctx, st)) return -1;
@@ -487,16 +492,20 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
         if (const char* e = getenv("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
     }
     // d_work: [u64 pad] [u64 pass-1 cursor] [u64 pass-2 cursor] [u64 queue count] [pad] [i64 queue...]
-    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 64 + (band > 0 ? (size_t)ps.count * 8 : 0))) return -1;
+    // (the queue also takes raw-difference walks whose score check failed, so it exists whenever
+    // the band pass can queue anything)
+    const bool queue = band > 0 || raw;
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 64 + (queue ? (size_t)ps.count * 8 : 0))) return -1;
     unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
     unsigned long long* next2 = (unsigned long long*)((char*)ctx->d_work + 16);
     unsigned long long* esc_n = (unsigned long long*)((char*)ctx->d_work + 24);
     int64_t* esc_list = (int64_t*)((char*)ctx->d_work + 64);
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 64, st));
     v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), ps, k, ms, chunk, out_mode, d_out,
-             d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next, BandArgs{band, esc_list, esc_n});
+             d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next,
+             BandArgs{band, queue ? esc_list : nullptr, esc_n});
     HIP_TRY(ctx, hipGetLastError());
-    if (band > 0) {  // the queued pairs (usually none: the workgroups exit at once), full trace
+    if (queue) {  // the queued pairs (usually none: the workgroups exit at once), full trace
         PairSrc p2 = ps;
         p2.sel = esc_list;
         p2.dcount = esc_n;
@@ -652,9 +661,49 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     return 0;
 }
 
+// host copy of the triangle row of linear pair index g (common.hpp decode_pair)
+static int64_t tri_row_host(int64_t g, int64_t N) {
+    auto start = [N](int64_t a) { return a * (2 * N - a - 1) / 2; };
+    const double n2 = 2.0 * (double)N - 1.0;
+    const double disc = n2 * n2 - 8.0 * (double)g;
+    int64_t r = (int64_t)((n2 - std::sqrt(disc > 0.0 ? disc : 0.0)) * 0.5);
+    r = std::max<int64_t>(0, std::min<int64_t>(r, N - 2));
+    while (r > 0 && start(r) > g) --r;
+    while (r + 1 <= N - 2 && start(r + 1) <= g) ++r;
+    return r;
+}
+
 int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                       const MetricSpec& ms, double* d_out, hipStream_t st) {
     if (ps.count <= 0) return 0;
+    // triangle / rectangle blocks: PT x PT pair tiles with LDS-staged planes (prealigned_kernel.hpp);
+    // TAXI2_PRE_NOTILE=1 keeps the one-thread-per-pair kernel (A/B and parity tests)
+    if (ps.mode != PAIRS_LIST && ps.count >= 4096 && !getenv("TAXI2_PRE_NOTILE")) {
+        int64_t x0, nx, y0, ny;
+        if (ps.mode == PAIRS_TRI) {
+            const int64_t a0 = tri_row_host(ps.k0, ps.N), a1 = tri_row_host(ps.k0 + ps.count - 1, ps.N);
+            x0 = a0;
+            nx = a1 - a0 + 1;
+            y0 = a0 + 1;
+            ny = ps.N - y0;
+        } else {
+            x0 = ps.k0 / ps.R;
+            nx = (ps.k0 + ps.count - 1) / ps.R + 1 - x0;
+            y0 = 0;
+            ny = ps.R;
+        }
+        const int64_t tiles_x = (nx + PT - 1) / PT, tiles_y = (ny + PT - 1) / PT;
+        if (tiles_x * tiles_y > ((int64_t)1 << 31) - 1) return fail(ctx, "pre-aligned tile grid too large");
+        const int nwords = (std::max(X.max_len, Y.max_len) + 31) / 32;
+        if (ps.mode == PAIRS_TRI)
+            hipLaunchKernelGGL(k_prealigned_tile<PAIRS_TRI>, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0, st,
+                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out);
+        else
+            hipLaunchKernelGGL(k_prealigned_tile<PAIRS_RECT>, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0, st,
+                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out);
+        HIP_TRY(ctx, hipGetLastError());
+        return 0;
+    }
     const int64_t blocks = std::min<int64_t>((ps.count + 255) / 256, (int64_t)ctx->num_cus * 64);
     hipLaunchKernelGGL(k_prealigned, dim3((unsigned)blocks), dim3(256), 0, st, view(X), view(Y), ps,
                        ms, d_out);
@@ -944,6 +993,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_bnd) (void)hipFree(ctx->d_bnd);
     if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
+    if (ctx->d_sub) (void)hipFree(ctx->d_sub);
     if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
     if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
     if (ctx->shared_ev) (void)hipEventDestroy(ctx->shared_ev);
@@ -1100,6 +1150,28 @@ int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     PairSrc ps{PAIRS_RECT, q0 * R->n, (q1 - q0) * R->n, 0, R->n, nullptr, nullptr};
     return run_pairs(ctx, *Q, *R, ps, sc, ms, OUT_AB, out, scores_out);
+}
+
+int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
+                         const int32_t* metrics, int nmetrics, double* d_out, int32_t* d_scores, void* stream) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (Q->mode != R->mode) return fail(ctx, "query and reference sets differ in mode");
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, std::max(Q->max_len, R->max_len))) return -1;
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if (Q->mode == TAXI2_MODE_PREALIGNED && d_scores) return fail(ctx, "no scores in PREALIGNED mode");
+    if ((q1 - q0) * R->n > 0 && !d_out) return fail(ctx, "null output");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairSrc ps{PAIRS_RECT, q0 * R->n, (q1 - q0) * R->n, 0, R->n, nullptr, nullptr};
+    if (Q->mode == TAXI2_MODE_ALIGN) {
+        if (!sc) return fail(ctx, "scores required in ALIGN mode");
+        return launch_align_pairs(ctx, *Q, *R, ps, sc, ms, OUT_AB, d_out, d_scores, st);
+    }
+    return launch_prealigned(ctx, *Q, *R, ps, ms, d_out, st);
 }
 
 int taxi2_list_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
@@ -1540,9 +1612,51 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
         return fail(ctx, "null pointer passed to taxi2_subset_aggregate_dev");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    hipLaunchKernelGGL(k_subset_aggregate_rows, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, st, d_vals, nrows,
-                       ncols, m, d_row_code, d_col_start, d_col_idx, ns, init ? 1 : 0, d_sum, d_min, d_max, d_count);
-    HIP_TRY(ctx, hipGetLastError());
+    if (init) {
+        const int64_t blocks = std::min<int64_t>((nk + 255) / 256, (int64_t)ctx->num_cus * 32);
+        hipLaunchKernelGGL(k_subset_init, dim3((unsigned)blocks), dim3(256), 0, st, nk, d_sum, d_min, d_max, d_count);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (nrows == 0) return 0;
+    // exact parallel summation (subset_kernels.hpp), rows in sub-blocks whose row partials fit
+    // ~256 MB of scratch (and the groups' LDS sort), in ascending order on one stream
+    const int64_t per_row = (int64_t)ns * m;
+    const int64_t rows_per = std::max<int64_t>(1, std::min<int64_t>(SUB_MAX_ROWS, ((int64_t)256 << 20) /
+                                                                    (per_row * (int64_t)(sizeof(SubPart) + sizeof(SubWork)))));
+    const int64_t rsub = std::min(rows_per, nrows);
+    auto al = [](size_t v) { return (v + 255) / 256 * 256; };
+    const size_t o_part = 0, o_work = al((size_t)rsub * per_row * sizeof(SubPart));
+    const size_t o_rows = o_work + al((size_t)rsub * per_row * sizeof(SubWork));
+    const size_t o_code = o_rows + al((size_t)rsub * 4), o_start = o_code + al((size_t)rsub * 4);
+    const size_t o_n = o_start + al((size_t)(rsub + 1) * 4), total = o_n + 256;
+    if (ensure(ctx, &ctx->d_sub, &ctx->d_sub_bytes, total)) return -1;
+    char* base = (char*)ctx->d_sub;
+    SubPart* part = (SubPart*)(base + o_part);
+    SubWork* work = (SubWork*)(base + o_work);
+    int32_t* grows = (int32_t*)(base + o_rows);
+    int32_t* gcode = (int32_t*)(base + o_code);
+    int32_t* gstart = (int32_t*)(base + o_start);
+    int32_t* ngrp = (int32_t*)(base + o_n);
+    unsigned int* wcount = (unsigned int*)(base + o_n + 64);
+    for (int64_t r0 = 0; r0 < nrows; r0 += rsub) {
+        const int64_t nr = std::min(rsub, nrows - r0);
+        const double* v = d_vals + r0 * ncols * m;
+        const int32_t* rc = d_row_code + r0;
+        hipLaunchKernelGGL(k_subset_groups, dim3(1), dim3(1024), 0, st, rc, (int)nr, grows, gcode, gstart, ngrp);
+        HIP_TRY(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * ns + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m, rc,
+                           d_col_start, d_col_idx, (int)ns, (const double*)d_sum, part);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipMemsetAsync(wcount, 0, 4, st));
+        hipLaunchKernelGGL(k_subset_combine, dim3((unsigned)((nr * per_row + 255) / 256)), dim3(256), 0, st, nr,
+                           (int)ns, m, (const int32_t*)ngrp, (const int32_t*)gcode, (const int32_t*)gstart,
+                           (const int32_t*)grows, (const SubPart*)part, d_sum, d_min, d_max, d_count, work, wcount);
+        HIP_TRY(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_subset_fixup, dim3((unsigned)(ctx->num_cus * 8)), dim3(256), 0, st, v, ncols, m, (int)ns,
+                           d_col_start, d_col_idx, (const int32_t*)gstart, (const int32_t*)grows,
+                           (const SubWork*)work, (const unsigned int*)wcount, d_sum);
+        HIP_TRY(ctx, hipGetLastError());
+    }
     return 0;
 }
 

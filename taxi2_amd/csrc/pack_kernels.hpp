@@ -28,7 +28,10 @@ k_meta(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offs, cons
     if (lane == 0) meta[s] = make_int4(len, first, last, woffs ? (int)woffs[s] : 0);
 }
 
-// One workgroup per sequence, one thread per 32-column word.
+// One workgroup per sequence, one thread per 32-column word.  The '-' plane keeps only the gaps
+// inside the sequence's own [first, last ACGT] (k_meta runs first): a gap column counts only
+// inside the pair's common range, and with both sides' gap bits pre-restricted (and valid bits
+// inside their range by definition) the tiled kernel needs no per-pair mask.
 __global__ void __launch_bounds__(256)
 k_planes(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offs,
          const int4* __restrict__ meta, int64_t n, uint4* __restrict__ planes) {
@@ -50,7 +53,7 @@ k_planes(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offs,
                 nv |= 1u << t;
                 lo |= (uint32_t)(bc & 1) << t;
                 hi |= (uint32_t)(bc >> 1) << t;
-            } else if (ch == '-') {
+            } else if (ch == '-' && c >= m.y && c <= m.z) {
                 gp |= 1u << t;
             }
         }
@@ -100,48 +103,6 @@ __global__ void __launch_bounds__(256) k_counts_metrics(const uint64_t* __restri
             out[k * ms.n + m] = scale == 1.0 ? v : v * scale;
         }
     }
-}
-
-// DistanceAggregator (versus_all.py:57-96, fed x-major by _aggregate_distances :617-640) over a
-// block of rows [nrows][ncols][m] of adjusted values, accumulated into per-(subset x, subset y,
-// metric) state: one thread per key and metric, which visits the block's rows of subset a in
-// ascending x and, per row, the columns of subset b in ascending y (col_idx[col_start[b] ..
-// col_start[b+1]) sorted ascending) -- the reference's own order for that key, so feeding the row
-// blocks in ascending order gives the sums bit for bit.  SimpleAggregator.add: sum += v,
-// min from +inf (first of equal values kept), max from 0.0, count; None (non-finite) skipped.
-__global__ void __launch_bounds__(256) k_subset_aggregate_rows(const double* __restrict__ vals, int64_t nrows,
-                                                             int64_t ncols, int m, const int32_t* __restrict__ row_code,
-                                                             const int64_t* __restrict__ col_start,
-                                                             const int32_t* __restrict__ col_idx, int ns, int init,
-                                                             double* __restrict__ sum, double* __restrict__ mn,
-                                                             double* __restrict__ mx, int64_t* __restrict__ count) {
-    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t nk = (int64_t)ns * ns * m;
-    if (t >= nk) return;
-    const int a = (int)(t / ((int64_t)ns * m));
-    const int b = (int)((t / m) % ns);
-    const int k = (int)(t % m);
-    double s = init ? 0.0 : sum[t];
-    double lo = init ? __builtin_inf() : mn[t];
-    double hi = init ? 0.0 : mx[t];
-    int64_t c = init ? 0 : count[t];
-    const int64_t j0 = col_start[b], j1 = col_start[b + 1];
-    for (int64_t x = 0; x < nrows; ++x) {
-        if (row_code[x] != a) continue;
-        const double* row = vals + x * ncols * m + k;
-        for (int64_t j = j0; j < j1; ++j) {
-            const double v = row[(int64_t)col_idx[j] * m];
-            if (!isfinite(v)) continue;
-            s += v;
-            if (v < lo) lo = v;
-            if (v > hi) hi = v;
-            ++c;
-        }
-    }
-    sum[t] = s;
-    mn[t] = lo;
-    mx[t] = hi;
-    count[t] = c;
 }
 
 }  // namespace taxi2

@@ -11,10 +11,9 @@
 // and the four counters are popcounts.  The counters are symmetric, so one value per
 // unordered pair serves both ordered rows of versusAll.
 //
-// One thread per pair; the planes of a whole set are small (N x L/8 bytes: 2 000 x 600 bp is
-// 150 KB) and stay resident in L2 / the Infinity Cache, so operands are read straight from
-// there.  Work per pair is ~6 VALU ops per 32 columns, so the kernel is bounded by its f64
-// output stream (HBM write).
+// k_prealigned: one thread per pair, operands straight from L2 (pair lists, small launches).
+// k_prealigned_tile: the triangle and the rectangle, PT x PT pair tiles with both sides' planes
+// staged in LDS (below).
 #pragma once
 #include "common.hpp"
 
@@ -42,7 +41,8 @@ __device__ __forceinline__ void count_words(const uint4* __restrict__ px, const 
     }
 }
 
-// Generic pair-list form (TRI / RECT / LIST); one thread per pair, operands from L2.
+// Generic pair-list form (LIST; TRI / RECT too small for a tile); one thread per pair, operands
+// from L2.
 __global__ void __launch_bounds__(256)
 k_prealigned(SetView XS, SetView YS, PairSrc ps, MetricSpec ms, double* __restrict__ out) {
     const int nm = ms.n;
@@ -57,6 +57,109 @@ k_prealigned(SetView XS, SetView YS, PairSrc ps, MetricSpec ms, double* __restri
         uint32_t v, ts, tv, g;
         count_words(XS.planes + ma.w, YS.planes + mb.w, lo, hi, v, ts, tv, g);
         for (int m = 0; m < nm; ++m) out[p * nm + m] = metric_value(ms.code[m], v, ts, tv, g);
+    }
+}
+
+// Tiled form for the versusAll triangle and the rectangle (round 3).  The one-thread-per-pair
+// kernel gathers 2 x ceil(L/32) words of planes per pair from L2 (1 KB per 1 000 bp pair): at
+// config 5 (N = 200 000, a 100 MB plane set that does not stay in L2) the operand gathers, not
+// the arithmetic, bound it.  Here a workgroup takes a tile of PT x-sequences x PT y-sequences,
+// stages both sides' planes in LDS PWC words at a time (coalesced 16-byte loads, zero beyond a
+// sequence's end) and each thread accumulates a 4 x 4 block of pairs from registers: per word
+// 8 LDS reads feed 16 pair updates, so every plane word fetched from memory serves PT pairs.
+//
+// No per-pair range mask: a valid bit lies inside its own sequence's [first, last ACGT] by
+// definition, and k_planes keeps gap bits only inside that range, so
+//   both = vx & vy,   gap = (gx & vy) | (gy & vx)
+// are already restricted to the pair's common range [max(first), min(last)] (count_words masks it
+// explicitly; the two agree bit for bit, tests/test_gpu_parity.py).
+constexpr int PT = 64;        // sequences per tile side
+constexpr int PWC = 16;       // plane words staged per chunk
+constexpr int PWS = PWC + 1;  // padded LDS row (uint4): 16 lanes reading 16 rows hit 64 distinct banks
+
+// Tile grid: x rows [x0, x0 + nx), y columns [y0, y0 + ny); tiles_y tiles per tile row.
+// MODE PAIRS_TRI: pair (a, b) exists for b > a, output slot tri(a, b) - ps.k0 when that lies in
+// [0, ps.count); PAIRS_RECT: output slot (a * ps.R + b) - ps.k0 (b indexes YS).
+template <int MODE>
+__global__ void __launch_bounds__(256)
+k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, int64_t y0, int64_t ny,
+                  int64_t tiles_y, int nwords, MetricSpec ms, double* __restrict__ out) {
+    __shared__ uint4 sx[PT * PWS], sy[PT * PWS];
+    const int tid = (int)threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+    const int64_t bx = (int64_t)blockIdx.x / tiles_y, by = (int64_t)blockIdx.x - bx * tiles_y;
+    const int64_t xa = x0 + bx * PT, ya = y0 + by * PT;
+    // the whole tile at or below the diagonal: nothing to do (uniform, before any barrier)
+    if (MODE == PAIRS_TRI && ya + PT - 1 <= xa) return;
+    const int64_t xe = min(x0 + nx, xa + PT), ye = min(y0 + ny, ya + PT);
+    uint32_t c[4][4][4];  // [i][j][valid, ts, tv, gap]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[i][j][q] = 0u;
+    for (int w0 = 0; w0 < nwords; w0 += PWC) {
+        __syncthreads();  // the previous chunk's readers are done
+        // stage: PT sequences x PWC words per side, one uint4 per thread and pass
+        for (int e = tid; e < PT * PWC; e += 256) {
+            const int r = e / PWC, wd = e - r * PWC;
+            uint4 vx = make_uint4(0u, 0u, 0u, 0u), vy = vx;
+            const int64_t s = xa + r, t = ya + r;
+            if (s < xe) {
+                const int4 m = XS.meta[s];
+                if (w0 + wd < (m.x + 31) / 32) vx = XS.planes[m.w + w0 + wd];
+            }
+            if (t < ye) {
+                const int4 m = YS.meta[t];
+                if (w0 + wd < (m.x + 31) / 32) vy = YS.planes[m.w + w0 + wd];
+            }
+            sx[r * PWS + wd] = vx;
+            sy[r * PWS + wd] = vy;
+        }
+        __syncthreads();
+        const int wn = min(PWC, nwords - w0);
+        for (int wd = 0; wd < wn; ++wd) {
+            uint4 a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = sx[(tx + 16 * i) * PWS + wd];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = sy[(ty + 16 * j) * PWS + wd];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t both = a[i].z & b[j].z;
+                    const uint32_t tvb = both & (a[i].x ^ b[j].x);           // lo bits differ: transversion
+                    const uint32_t tsb = (both ^ tvb) & (a[i].y ^ b[j].y);   // only the hi bit differs
+                    c[i][j][0] += __popc(both);
+                    c[i][j][1] += __popc(tsb);
+                    c[i][j][2] += __popc(tvb);
+                    c[i][j][3] += __popc((a[i].w & b[j].z) | (b[j].w & a[i].z));
+                }
+        }
+    }
+    const int nm = ms.n;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t x = xa + tx + 16 * i;
+        if (x >= xe) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t y = ya + ty + 16 * j;
+            if (y >= ye) continue;
+            int64_t slot;
+            if (MODE == PAIRS_TRI) {
+                if (y <= x) continue;
+                slot = x * (2 * ps.N - x - 1) / 2 + (y - x - 1) - ps.k0;
+                if (slot < 0 || slot >= ps.count) continue;
+            } else {
+                slot = x * ps.R + y - ps.k0;
+                if (slot < 0 || slot >= ps.count) continue;  // a launch may start / end inside a row
+            }
+            for (int m = 0; m < nm; ++m)
+                out[slot * nm + m] = metric_value(ms.code[m], c[i][j][0], c[i][j][1], c[i][j][2], c[i][j][3]);
+        }
     }
 }
 

@@ -1,0 +1,270 @@
+// Subset aggregation on the GPU, exact and parallel (round 3): DistanceAggregator
+// (versus_all.py:57-96) fed x-major by _aggregate_distances (:617-640).  Per key (subset x a,
+// subset y b, metric k) the reference keeps a running `sum += v` over the key's values in x-major
+// order, so the mean is a function of that order (floating-point addition is not associative).
+// The round-2 kernel summed each key in one thread: with few subsets (a two-genus partition) a
+// handful of threads did all N^2 additions.
+//
+// Exact parallel summation.  While the running sum s stays inside one binade [2^(E-1), 2^E), the
+// representable values are the multiples of u = 2^(E-53), and for v >= 0 that keeps s + v inside
+// the binade, fl(s + v) = s + R u with R = v / u rounded to the nearest integer -- INDEPENDENT of
+// s, unless v / u lies exactly halfway (then the even neighbour of s + v wins, which depends on
+// s).  So over a run of values with no tie, no negative value and no binade change, the
+// sequential result is s + (sum of the R) u, and the R are exact integers (< 2^53) whose sum is
+// the same in any order.  Per block of rows:
+//   k_subset_rows     one wave per (row x, column subset b): for each metric, R of every value of
+//                     the row's key (u from the key's sum at block start), the row's integer sum,
+//                     count, first minimum, maximum, and flags (tie / negative / no grid: s = 0)
+//   k_subset_combine  one thread per (row group a, b, metric): walks the block's rows of subset a
+//                     in ascending x, adds the integer sums while S + sum <= 2^53 - 1 (the binade
+//                     holds) and nothing is flagged, merges count / min / max (in row order, so the
+//                     first minimum and the sign of a zero minimum are the sequential ones); at the
+//                     first row it cannot take, it queues the key with that row
+//   k_subset_fixup    one wave per queued key: the remaining rows in order, 64 values at a time --
+//                     the same integer step when the chunk qualifies, else 64 sequential f64 adds
+// Binade changes are rare (the sum of non-negative values doubles ~log2(N^2) times per key), so
+// the fixup runs on a key's first block and then on a few blocks only.  None (non-finite)
+// values are skipped as SimpleAggregator.add does (in the sums they add +0.0, an exact no-op:
+// the running sum starts at +0.0 and never becomes -0.0).
+#pragma once
+#include "common.hpp"
+
+namespace taxi2 {
+
+struct SubPart {    // one (block row, column subset b, metric k)
+    double rsum;    // sum of R over the row's values of the key (exact while < 2^53)
+    double mn, mx;  // first minimum (from +inf), maximum (from 0.0)
+    long long cnt;  // defined values
+    uint32_t flags; // SP_*: the integer step does not reproduce the sequential sum
+    int32_t pad;
+};
+enum : uint32_t { SP_NOGRID = 1, SP_NEG = 2, SP_TIE = 4 };
+struct SubWork {  // a key the combine could not finish: its rows from grp_rows[r0] on
+    int64_t key;
+    int32_t g, r0;
+};
+constexpr double SUB_TOP = 9007199254740991.0;  // 2^53 - 1: largest integer multiple of u below 2^E
+constexpr int SUB_MAX_ROWS = 8192;              // rows per k_subset_groups call (LDS sort)
+
+// The grid of running sum s: true with s in [2^(e-1), 2^e) when s is a positive normal number.
+__device__ __forceinline__ bool sub_grid(double s, int& e) {
+    e = 0;
+    if (!(s >= 2.2250738585072014e-308) || !(s <= 1.7976931348623157e308)) return false;
+    (void)frexp(s, &e);
+    return true;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_subset_init(int64_t nk, double* __restrict__ sum, double* __restrict__ mn,
+                                                     double* __restrict__ mx, int64_t* __restrict__ count) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nk; t += (int64_t)gridDim.x * blockDim.x) {
+        sum[t] = 0.0;  // SimpleAggregator.__init__
+        mn[t] = __builtin_inf();
+        mx[t] = 0.0;
+        count[t] = 0;
+    }
+}
+
+// The block's rows grouped by subset: rows sorted by (code, row) (bitonic sort of 64-bit keys in
+// LDS, nrows <= SUB_MAX_ROWS), groups [grp_start[g], grp_start[g + 1]) of equal code grp_code[g].
+__global__ void __launch_bounds__(1024) k_subset_groups(const int32_t* __restrict__ row_code, int nrows,
+                                                        int32_t* __restrict__ grp_rows, int32_t* __restrict__ grp_code,
+                                                        int32_t* __restrict__ grp_start, int32_t* __restrict__ ngrp) {
+    __shared__ unsigned long long keys[SUB_MAX_ROWS];
+    int P = 1;
+    while (P < nrows) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x)
+        keys[i] = i < nrows ? ((unsigned long long)(uint32_t)row_code[i] << 32) | (uint32_t)i : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned long long a = keys[i], b = keys[l];
+                    if (((i & k) == 0) == (a > b)) {
+                        keys[i] = b;
+                        keys[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // group index of a boundary = boundaries before it: each thread counts its SUB_MAX_ROWS / 1024
+    // consecutive positions, then a scan over the threads' counts (Hillis-Steele in LDS)
+    __shared__ int part[1024];
+    constexpr int PER = SUB_MAX_ROWS / 1024;
+    const int t = threadIdx.x;
+    auto boundary = [&](int i) { return i < nrows && (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32)); };
+    int cnt = 0;
+    for (int q = 0; q < PER; ++q) cnt += boundary(t * PER + q);
+    part[t] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int g = part[t] - cnt;  // boundaries before this thread's first position
+    for (int q = 0; q < PER; ++q) {
+        const int i = t * PER + q;
+        if (i < nrows) grp_rows[i] = (int32_t)(uint32_t)keys[i];
+        if (boundary(i)) {
+            grp_code[g] = (int32_t)(keys[i] >> 32);
+            grp_start[g] = i;
+            ++g;
+        }
+    }
+    if (t == 1023) {
+        grp_start[part[1023]] = nrows;
+        *ngrp = part[1023];
+    }
+}
+
+// One wave per (block row x, column subset b), every metric.
+__global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ vals, int64_t nrows, int64_t ncols,
+                                                     int m, const int32_t* __restrict__ row_code,
+                                                     const int64_t* __restrict__ col_start,
+                                                     const int32_t* __restrict__ col_idx, int ns,
+                                                     const double* __restrict__ sum, SubPart* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nrows * ns) return;
+    const int64_t x = w / ns;
+    const int b = (int)(w - x * ns);
+    const int a = row_code[x];
+    const int64_t j0 = col_start[b], j1 = col_start[b + 1];
+    const double* row = vals + x * ncols * m;
+    for (int k = 0; k < m; ++k) {
+        int e;
+        const bool grid = sub_grid(sum[((int64_t)a * ns + b) * m + k], e);
+        const int sc = 53 - e;
+        double rs = 0.0, mn = __builtin_inf(), mx = 0.0;
+        long long c = 0, mnp = 0x7FFFFFFFFFFFFFFFll;
+        uint32_t fl = grid ? 0u : SP_NOGRID;
+        for (int64_t j = j0 + lane; j < j1; j += 64) {
+            const double v = row[(int64_t)col_idx[j] * m + k];
+            if (!isfinite(v)) continue;
+            ++c;
+            if (v < mn) {
+                mn = v;
+                mnp = j;
+            }
+            if (v > mx) mx = v;
+            if (grid) {
+                if (v < 0.0) fl |= SP_NEG;
+                const double r = ldexp(v, sc);
+                const double R = rint(r);
+                if (fabs(r - R) == 0.5) fl |= SP_TIE;
+                rs += R;
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            rs += __shfl_xor(rs, o);
+            c += __shfl_xor(c, o);
+            fl |= (uint32_t)__shfl_xor((int)fl, o);
+            const double omx = __shfl_xor(mx, o);
+            if (omx > mx) mx = omx;
+            const double omn = __shfl_xor(mn, o);
+            const long long omp = __shfl_xor(mnp, o);
+            if (omn < mn || (omn == mn && omp < mnp)) {  // the first position among equal minima
+                mn = omn;
+                mnp = omp;
+            }
+        }
+        if (lane == 0) part[(x * ns + b) * m + k] = SubPart{rs, mn, mx, c, fl, 0};
+    }
+}
+
+// One thread per (row group g, column subset b, metric k).
+__global__ void __launch_bounds__(256) k_subset_combine(int64_t maxg, int ns, int m, const int32_t* __restrict__ ngrp,
+                                                        const int32_t* __restrict__ grp_code,
+                                                        const int32_t* __restrict__ grp_start,
+                                                        const int32_t* __restrict__ grp_rows,
+                                                        const SubPart* __restrict__ part, double* __restrict__ sum,
+                                                        double* __restrict__ mn, double* __restrict__ mx,
+                                                        int64_t* __restrict__ count, SubWork* __restrict__ work,
+                                                        unsigned int* __restrict__ wcount) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= maxg * ns * m) return;
+    const int g = (int)(t / ((int64_t)ns * m));
+    if (g >= *ngrp) return;
+    const int b = (int)((t / m) % ns);
+    const int k = (int)(t % m);
+    const int64_t key = ((int64_t)grp_code[g] * ns + b) * m + k;
+    double s = sum[key], lo = mn[key], hi = mx[key];
+    long long c = count[key];
+    int e;
+    const bool grid = sub_grid(s, e);
+    double S = grid ? ldexp(s, 53 - e) : 0.0;
+    int resume = -1;
+    for (int r = grp_start[g]; r < grp_start[g + 1]; ++r) {
+        const SubPart P = part[((int64_t)grp_rows[r] * ns + b) * m + k];
+        c += P.cnt;
+        if (P.mn < lo) lo = P.mn;
+        if (P.mx > hi) hi = P.mx;
+        if (resume < 0) {
+            if (grid && P.flags == 0u && S + P.rsum <= SUB_TOP) S += P.rsum;
+            else resume = r;
+        }
+    }
+    if (grid) s = ldexp(S, e - 53);
+    sum[key] = s;
+    mn[key] = lo;
+    mx[key] = hi;
+    count[key] = c;
+    if (resume >= 0) work[atomicAdd(wcount, 1u)] = SubWork{key, g, resume};
+}
+
+// Persistent waves over the queued keys: the key's remaining rows of the block in order.
+__global__ void __launch_bounds__(256) k_subset_fixup(const double* __restrict__ vals, int64_t ncols, int m, int ns,
+                                                      const int64_t* __restrict__ col_start,
+                                                      const int32_t* __restrict__ col_idx,
+                                                      const int32_t* __restrict__ grp_start,
+                                                      const int32_t* __restrict__ grp_rows,
+                                                      const SubWork* __restrict__ work,
+                                                      const unsigned int* __restrict__ wcount,
+                                                      double* __restrict__ sum) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t total = *wcount;
+    for (int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < total; q += nw) {
+        const SubWork it = work[q];
+        const int k = (int)(it.key % m);
+        const int b = (int)((it.key / m) % ns);
+        const int64_t j0 = col_start[b], j1 = col_start[b + 1];
+        double s = sum[it.key];
+        for (int r = it.r0; r < grp_start[it.g + 1]; ++r) {
+            const double* row = vals + (int64_t)grp_rows[r] * ncols * m;
+            for (int64_t c0 = j0; c0 < j1; c0 += 64) {
+                const int64_t j = c0 + lane;
+                double v = j < j1 ? row[(int64_t)col_idx[j] * m + k] : 0.0;
+                if (!isfinite(v)) v = 0.0;  // None: skipped (+0.0 adds nothing)
+                int e;
+                if (sub_grid(s, e)) {  // the integer step, when the whole chunk qualifies
+                    const double rr = ldexp(v, 53 - e);
+                    const double R = rint(rr);
+                    const bool bad = v < 0.0 || fabs(rr - R) == 0.5;
+                    if (!__any(bad)) {
+                        const double tot = wave_sum_f64(R);
+                        const double S = ldexp(s, 53 - e);
+                        if (S + tot <= SUB_TOP) {
+                            s = ldexp(S + tot, e - 53);
+                            continue;
+                        }
+                    }
+                }
+                const int n = (int)min((int64_t)64, j1 - c0);
+                for (int l = 0; l < n; ++l) s = s + __shfl(v, l);  // the reference's own additions
+            }
+        }
+        if (lane == 0) sum[it.key] = s;
+    }
+}
+
+}  // namespace taxi2

@@ -211,6 +211,11 @@ class SubsetAggregatorDev:
                                       self.sum.data_ptr(), self.min.data_ptr(), self.max.data_ptr(),
                                       self.count.data_ptr(), st)
 
+    def state(self) -> tuple:
+        """The running state tensors (sum, min, max, count), passed rank to rank by the sharded
+        pre-aligned chain (VersusAll._stream_prealigned)."""
+        return (self.sum, self.min, self.max, self.count)
+
     def result(self) -> SubsetStats:
         s, lo, hi, c = (t.cpu().numpy() for t in (self.sum, self.min, self.max, self.count))
         with np.errstate(invalid="ignore", divide="ignore"):

@@ -94,6 +94,13 @@ class VersusAll:
         self.params.engine.write_summary = True
         self.params.engine.row_minima = None
         self.row_minima = None
+        # streamed pre-aligned path: a sharded rank keeps its computed row blocks in HBM for the
+        # rank-ordered subset chain when they fit this many bytes (else recomputes them);
+        # timings = True synchronises after each phase and fills task.timings (seconds)
+        self.params.engine.hold_bytes = 160 << 30
+        self.params.engine.timings = False
+        self.timings = None
+        self.subset_stats = None  # {"genera" / "species": SubsetStats} after start() (engine extra)
 
         self.distances: np.ndarray | None = None  # (N, N, M) after start(), NaN = None
 
@@ -334,11 +341,12 @@ class VersusAll:
         from .subsets import aggregate, write_subset_statistics
 
         ids = [s.id for s in seqs]
+        self.subset_stats = {}
         for partition, name in ((self.input.genera, "genera"), (self.input.species, "species")):
             if partition:
-                write_subset_statistics(self.paths.subsets / name, aggregate(A, ids, partition),
-                                        self.params.distances.metrics, self.params.format.float,
-                                        self.params.format.stats_template)
+                st = self.subset_stats[name] = aggregate(A, ids, partition)
+                write_subset_statistics(self.paths.subsets / name, st, self.params.distances.metrics,
+                                        self.params.format.float, self.params.format.stats_template)
 
     # ------------------------------------------------------------------ streamed driver
     def _streaming(self, seqs: list) -> bool:
@@ -389,14 +397,124 @@ class VersusAll:
         eng = self._engine()
         cuda = torch.device("cuda", eng.device)
         store_dev = cuda if group_backend in (None, "nccl") else torch.device("cpu")
-        store = TriangleStore(n, world, rank, device=store_dev)
         st = eng.upload([s.seq for s in seqs], align=align)
         # one real stream for the torch ops and the engine's *_dev calls of this path (the legacy
         # default stream has handle 0, which the engine would read as "its own stream")
         stream = torch.cuda.Stream(cuda)
         with torch.cuda.stream(stream):
+            if not align and not nidx:
+                self._stream_prealigned(seqs, eng, st, stream, scores, labels, world, rank, group_backend)
+                return
+            store = TriangleStore(n, world, rank, device=store_dev)
             self._stream_blocks(seqs, eng, st, store, stream, align, scores, labels, cidx, nidx, clabels,
                                 world, rank, total)
+
+    def _stream_prealigned(self, seqs, eng, st, stream, scores, labels, world, rank, backend) -> None:
+        """Pre-aligned streamed versusAll (config 5: 200 000 x 1 000 bp, p / jc / k2p): every
+        x-major row block [x0, x1) x [0, N) is computed directly by the tiled pre-aligned kernel
+        (taxi2_rect_pairs_dev).  That evaluates each unordered pair once per orientation instead of
+        once, but a pre-aligned pair costs a few hundred VALU ops: recomputing is far cheaper than
+        storing the triangle (16 B per pair, 320 GB at N = 200 000) and gathering it.
+
+        One rank: the blocks in order, each fed to the diagonal rule, the writers and the
+        reductions.  Several ranks, reductions only: each rank takes a contiguous row range; the
+        row minima are per row (gathered at the end), and the subset statistics -- whose sums must
+        follow the reference's x-major order -- are passed rank to rank: rank r accumulates its rows
+        into the state it receives from rank r - 1 (the blocks it computed are kept in HBM when they
+        fit params.engine.hold_bytes, else recomputed).  With N x N text to write the funnel is the
+        host's file stream anyway, and rank 0 computes every block itself."""
+        import torch
+
+        from ..sharding import gather_blocks, shard_range
+        from ..streaming import block_rows
+
+        p = self.params
+        n, M = len(seqs), len(labels)
+        text = bool(p.distances.write_linear or p.distances.write_matricial or p.pairs.write or p.engine.write_summary)
+        sharded = world > 1 and not text
+        if not sharded and rank != 0:
+            return
+        rows = shard_range(n, world) if sharded else [(0, n)]
+        r0, r1 = rows[rank if sharded else 0]
+        times = dict(compute_s=0.0, reduce_s=0.0, text_s=0.0, comm_s=0.0)
+        timed = bool(p.engine.timings)
+        cuda = stream.device
+
+        def tick(key, t0):
+            if timed:
+                stream.synchronize()
+                times[key] += perf_counter() - t0
+            return perf_counter()
+
+        sink = _BlockWriters(self, seqs, eng, files=(rank == 0))
+        groups: dict = {}
+        for i, s in enumerate(seqs):
+            groups.setdefault(seq_key(s), []).append(i)
+        sink.diag = (list(groups.values()), None, None)
+        scale = 100.0 if p.format.percentage_multiply else 1.0
+        B = block_rows(n, 8 * M, int(p.engine.block_bytes))
+        hold = sharded and (r1 - r0) * n * M * 8 <= int(p.engine.hold_bytes)
+        held = []
+        total = M * n * n
+
+        def block(x0, x1):
+            t = perf_counter()
+            D = torch.empty((x1 - x0, n, M), dtype=torch.float64, device=cuda)
+            eng.rect_pairs_dev(st, st, x0, x1, labels, D.data_ptr(), scores, None, stream.cuda_stream)
+            if scale != 1.0:
+                D.mul_(scale)
+            sink.diagonal(x0, x1, D, scale)
+            tick("compute_s", t)
+            return D
+
+        try:
+            for x0 in range(r0, r1, B):
+                x1 = min(r1, x0 + B)
+                D = block(x0, x1)
+                t = perf_counter()
+                sink.row_minima(x0, x1, D)
+                if not sharded:
+                    sink.aggregate(x0, x1, D)
+                t = tick("reduce_s", t)
+                if not sharded:
+                    sink.write_text(x0, x1, D)
+                    tick("text_s", t)
+                elif hold:
+                    held.append((x0, x1, D))
+                del D
+                report(self.progress_handler, "distance.x.id", min(total, M * n * x1 * (world if sharded else 1)),
+                       total)
+            if sharded:
+                comm = torch.device("cuda", eng.device) if backend == "nccl" else torch.device("cpu")
+                t = perf_counter()
+                if sink.aggs:
+                    if rank > 0:
+                        sink.recv_state(rank - 1, comm)
+                    t = tick("comm_s", t)
+                    for x0 in range(r0, r1, B):
+                        x1 = min(r1, x0 + B)
+                        D = held.pop(0)[2] if hold else block(x0, x1)
+                        t = perf_counter()
+                        sink.aggregate(x0, x1, D)
+                        t = tick("reduce_s", t)
+                        del D
+                    sink.send_state((rank + 1) % world, comm)
+                    if rank == 0:
+                        sink.recv_state(world - 1, comm)
+                    t = tick("comm_s", t)
+                if sink.rmin_k is not None:
+                    lo, hi = r0, r1
+                    loc = np.stack([sink.rmin_idx[lo:hi].astype(np.float64), sink.rmin_d[lo:hi]], axis=1)
+                    allr = gather_blocks(loc, [b - a for a, b in rows],
+                                         device=comm if backend == "nccl" else None)
+                    sink.rmin_idx[:] = allr[:, 0].astype(np.int64)
+                    sink.rmin_d[:] = allr[:, 1]
+                    tick("comm_s", t)
+            if rank == 0:
+                sink.close()
+        finally:
+            st.free()
+        self.timings = times
 
     def _stream_blocks(self, seqs, eng, st, store, stream, align, scores, labels, cidx, nidx, clabels, world,
                        rank, total) -> None:
@@ -518,12 +636,13 @@ class _BlockWriters:
     taxi2_subset_aggregate_dev), each fed the rows [x0, x1) in x-major order -- the file contents
     are those of the dense path (tests/test_gpu_streaming.py)."""
 
-    def __init__(self, task: VersusAll, seqs: list, eng):
+    def __init__(self, task: VersusAll, seqs: list, eng, files: bool = True):
         import torch
 
         from .subsets import SubsetAggregatorDev, subset_codes
 
         self.task, self.seqs, self.eng = task, seqs, eng
+        self.files = files  # False: a sharded rank's reductions only (rank 0 writes every file)
         p = task.params
         self.metrics = p.distances.metrics
         self.fmt, self.missing = p.format.float, p.format.missing
@@ -536,13 +655,13 @@ class _BlockWriters:
         self.pre = ["\t".join([s.id, *[v if v is not None else self.missing for v in s.extras.values()]])
                     for s in seqs]
         self.lin = self.mats = None
-        if p.distances.write_linear:
+        if p.distances.write_linear and files:
             create_parents(task.paths.distances_linear)
             self.lin = open(task.paths.distances_linear, "wb")
             head = ["seqid (query)", *[k + " (query)" for k in ex0], "seqid (reference)",
                     *[k + " (reference)" for k in ex0], *[str(m) for m in self.metrics]]
             self.lin.write(("\t".join(head) + "\n").encode("utf-8"))
-        if p.distances.write_matricial:
+        if p.distances.write_matricial and files:
             create_parents(task.paths.distances_matricial)
             self.mats = []
             for metric in self.metrics:
@@ -561,7 +680,7 @@ class _BlockWriters:
         scode = subset_codes(self.ids, species)[0] if species else np.zeros(n, np.int32)
         self.codes = np.stack([gcode, scode], axis=1)
         self.summ = None
-        if p.engine.write_summary:
+        if p.engine.write_summary and files:
             create_parents(task.paths.summary)
             self.summ = open(task.paths.summary, "wb")
             head = ["seqid (query 1)", "seqid (query 2)", *[str(m) for m in self.metrics],
@@ -580,7 +699,7 @@ class _BlockWriters:
         self.aggs = [(name, SubsetAggregatorDev(eng, self.ids, part, len(self.metrics)))
                      for part, name in ((genera, "genera"), (species, "species")) if part]
         self.pairs_fh = None
-        if p.pairs.write:
+        if p.pairs.write and files:
             create_parents(task.paths.aligned_pairs)
             self.pairs_fh = SequencePairHandler.Formatted(task.paths.aligned_pairs, "w")
             self.aligner = (PairwiseAligner.Biopython(p.pairs.scores, engine=eng) if p.pairs.align else None)
@@ -588,23 +707,47 @@ class _BlockWriters:
 
     def consume(self, x0: int, x1: int, D, scale: float) -> None:
         """D: (x1 - x0, n, M) device tensor of the rows' values, x100 applied, diagonal not yet."""
+        self.diagonal(x0, x1, D, scale)
+        self.aggregate(x0, x1, D)
+        self.row_minima(x0, x1, D)
+        self.write_text(x0, x1, D)
+
+    @property
+    def has_text(self) -> bool:
+        return any(f is not None for f in (self.lin, self.summ, self.pairs_fh)) or bool(self.mats)
+
+    def diagonal(self, x0: int, x1: int, D, scale: float) -> None:
+        """Diagonal rule (versus_all.py:549) on rows [x0, x1): every (x, x) is None (one indexed
+        store for the block), then the groups of identical full tuples with more than one member
+        (every pair inside is None) and the sequences whose alignment with themselves is not the
+        identity (their own values), from an index built once (N = 200 000: no per-row Python)."""
         torch = self.torch
         dup, self_vals, strings = self.diag
-        # diagonal rule (versus_all.py:549): per group of identical full tuples
-        for gi, g in enumerate(dup):
-            rows = [i for i in g if x0 <= i < x1]
-            if not rows:
-                continue
+        if getattr(self, "_special", None) is None:
+            special = []  # (row, group index) of rows whose group needs more than the NaN diagonal
+            for gi, g in enumerate(dup):
+                if len(g) > 1 or (strings is not None and strings[gi][0] != strings[gi][1]):
+                    special.extend((i, gi) for i in g)
+            special.sort()
+            self._special = special
+            self._special_rows = np.array([i for i, _ in special], dtype=np.int64)
+        r = torch.arange(x1 - x0, device=D.device)
+        D[r, r + x0] = float("nan")
+        lo, hi = np.searchsorted(self._special_rows, [x0, x1])
+        for i, gi in self._special[lo:hi]:
+            g = dup[gi]
             if strings is not None and strings[gi][0] != strings[gi][1]:
-                sv = torch.as_tensor(self_vals[gi] * scale if scale != 1.0 else self_vals[gi], device=D.device)
-                for i in rows:
-                    D[i - x0, i] = sv
-                continue
-            cols = torch.as_tensor(g, device=D.device)
-            for i in rows:
-                D[i - x0, cols] = float("nan")
+                D[i - x0, i] = torch.as_tensor(self_vals[gi] * scale if scale != 1.0 else self_vals[gi],
+                                               device=D.device)
+            else:
+                D[i - x0, torch.as_tensor(g, device=D.device)] = float("nan")
+
+    def aggregate(self, x0: int, x1: int, D) -> None:
         for _, agg in self.aggs:
             agg.add(D, x0, x1)
+
+    def row_minima(self, x0: int, x1: int, D) -> None:
+        torch = self.torch
         if self.rmin_k is not None:  # first minimum over defined values (-0.0 == 0.0), None skipped
             v = D[:, :, self.rmin_k]
             v = torch.where(torch.isfinite(v), v, torch.full_like(v, float("inf")))
@@ -612,6 +755,27 @@ class _BlockWriters:
             ok = torch.isfinite(d)
             self.rmin_idx[x0:x1] = torch.where(ok, idx, torch.full_like(idx, -1)).cpu().numpy()
             self.rmin_d[x0:x1] = torch.where(ok, d, torch.full_like(d, float("nan"))).cpu().numpy()
+
+    def send_state(self, dst: int, comm) -> None:
+        """The subset aggregators' running state to rank `dst` (the sharded x-major chain)."""
+        import torch.distributed as dist
+
+        for _, agg in self.aggs:
+            for t in agg.state():
+                dist.send(t.to(comm), dst=dst)
+
+    def recv_state(self, src: int, comm) -> None:
+        import torch.distributed as dist
+
+        for _, agg in self.aggs:
+            for t in agg.state():
+                buf = self.torch.empty_like(t, device=comm)
+                dist.recv(buf, src=src)
+                t.copy_(buf)
+
+    def write_text(self, x0: int, x1: int, D) -> None:
+        if not self.has_text:  # reductions only: the block never leaves HBM
+            return
         A = D.cpu().numpy()
         seqs, ids = self.seqs, self.ids
         if self.pairs_fh is not None:
@@ -661,6 +825,9 @@ class _BlockWriters:
     def close(self) -> None:
         from .subsets import write_subset_statistics
 
+        if not self.files:
+            return
+
         for fh in [self.lin, self.summ, *(self.mats or [])]:
             if fh is not None:
                 fh.close()
@@ -677,6 +844,8 @@ class _BlockWriters:
         if self.pairs_fh is not None:
             self.pairs_fh.close()
         p = self.task.params
+        self.task.subset_stats = {}
         for name, agg in self.aggs:
-            write_subset_statistics(self.task.paths.subsets / name, agg.result(), self.metrics, p.format.float,
+            st = self.task.subset_stats[name] = agg.result()
+            write_subset_statistics(self.task.paths.subsets / name, st, self.metrics, p.format.float,
                                     p.format.stats_template)

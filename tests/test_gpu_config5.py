@@ -1,0 +1,82 @@
+"""Config 5 (BASELINE.json configs[4]: versusAll 200 000 x 1 000 bp) through VersusAll.start(),
+pre-aligned p / jc / k2p, reductions only ("gather only reductions" at that size).
+
+* Full size, one GPU: every ordered pair evaluated on the streamed pre-aligned path; the row
+  minima of 64 sampled rows equal the C restatement's first minimum over the whole row (x100 and
+  None rules applied), the genus and species statistics cover the same number of values, and the
+  per-phase times are reported (tools/bench_config5_task.py writes the same as JSON).
+* Mid size (N = 4 000): the streamed subset statistics (exact parallel sums, subset_kernels.hpp)
+  equal the dense path's sequential host aggregation bit for bit (means, minima, maxima, counts).
+Reference: /root/reference/src/itaxotools/taxi2/tasks/versus_all.py:57-96, 617-640, 732-773."""
+
+from __future__ import annotations
+
+import json
+import sys
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.int64)
+
+
+@pytest.mark.timeout(900)
+def test_config5_task_full_size(tmp_path, engine, oracle_c):
+    from tools.bench_config5_task import build_task
+
+    n, L = 200_000, 1000
+    task, buf, offs = build_task(n, L, engine, tmp_path, 2.0)
+    res = task.start()
+    t = task.timings
+    print(json.dumps({"n": n, "seconds": res.seconds_taken, "phases_s": t}))
+    idx, d = task.row_minima
+    rng = np.random.default_rng(5)
+    rows = np.sort(rng.choice(n, 64, replace=False))
+    for x in rows:
+        pa = np.full(n, x, dtype=np.int64)
+        pb = np.arange(n, dtype=np.int64)
+        exp, _ = oracle_c.batch((buf, offs), pa, pb, align=False, scores=(1, -1, -8, -1, -1, -1), metrics=("p",),
+                                threads=16)
+        v = exp[:, 0, 0] * 100.0
+        v[x] = np.nan  # diagonal rule (unique full tuples)
+        v = np.where(np.isfinite(v), v, np.inf)
+        j = int(np.argmin(v))
+        if np.isfinite(v[j]):
+            assert idx[x] == j and _bits(d[x]) == _bits(v[j]), (x, idx[x], j, d[x], v[j])
+        else:
+            assert idx[x] == -1
+    g, s = task.subset_stats["genera"], task.subset_stats["species"]
+    assert len(g.subsets) == 2 and len(s.subsets) > 900
+    assert np.array_equal(g.count.sum(axis=(0, 1)), s.count.sum(axis=(0, 1)))
+    assert (g.count.sum(axis=(0, 1)) <= n * (n - 1)).all()
+    assert set(t) == {"compute_s", "reduce_s", "text_s", "comm_s"}
+
+
+def test_streamed_subsets_exact_vs_dense(tmp_path, engine):
+    from tools.bench_config5_task import build_task
+
+    n, L = 4000, 600
+    dense, _, _ = build_task(n, L, engine, tmp_path / "dense", 0.05)
+    dense.params.engine.stream = False
+    dense.params.engine.row_minima = None
+    dense.start()
+    streamed, _, _ = build_task(n, L, engine, tmp_path / "stream", 0.05)  # ~1 MB blocks: many blocks
+    streamed.start()
+    for name in ("genera", "species"):
+        a, b = dense.subset_stats[name], streamed.subset_stats[name]
+        assert a.subsets == b.subsets
+        assert np.array_equal(a.count, b.count)
+        for x, y in ((a.mean, b.mean), (a.min, b.min), (a.max, b.max)):
+            assert np.array_equal(_bits(np.nan_to_num(x, nan=-7.0)), _bits(np.nan_to_num(y, nan=-7.0))), name
+    for f in sorted((tmp_path / "dense" / "subsets").rglob("*.tsv")):
+        rel = f.relative_to(tmp_path / "dense")
+        assert (tmp_path / "stream" / rel).read_bytes() == f.read_bytes(), rel

@@ -132,6 +132,17 @@ TASK = textwrap.dedent(
         elif variant == "prealigned":
             t.params.pairs.align = False
             t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.JukesCantor()]
+        elif variant == "reductions":  # config-5 shape: pre-aligned, no N x N text, reductions only
+            t.params.pairs.align = False
+            t.params.pairs.write = False
+            t.params.distances.write_linear = t.params.distances.write_matricial = False
+            t.params.engine.write_summary = False
+            t.params.engine.row_minima = "p"
+            t.params.format.percentage_multiply = True
+            t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.JukesCantor(),
+                                          DistanceMetric.Kimura2P()]
+            t.input.species = Partition({{s.id: "sp%d" % (k % 4) for k, s in enumerate(seqs) if k % 5}})
+            t.input.genera = Partition({{s.id: "g%d" % (k % 2) for k, s in enumerate(seqs)}})
         t.start()
     """
 )
@@ -167,7 +178,7 @@ WORKER = TASK + textwrap.dedent(
     else:
         dist.init_process_group("gloo")
     from taxi2_amd._native import Engine
-    run(Engine(local if backend == "nccl" else 0), Path(os.environ["OUT"]), True, "full")
+    run(Engine(local if backend == "nccl" else 0), Path(os.environ["OUT"]), True, os.environ.get("VARIANT", "full"))
     dist.barrier()
     dist.destroy_process_group()
     """
@@ -175,7 +186,8 @@ WORKER = TASK + textwrap.dedent(
 
 
 @pytest.mark.parametrize("backend", ["gloo", "nccl"])
-def test_streamed_task_two_ranks(tmp_path, engine, backend):
+@pytest.mark.parametrize("variant", ["full", "reductions"])
+def test_streamed_task_two_ranks(tmp_path, engine, backend, variant):
     """2 ranks stream their row blocks to rank 0 (gloo: both ranks on this GPU, stores in host
     memory; nccl = RCCL: one rank per GPU, stores in HBM, point-to-point sends)."""
     import torch
@@ -184,10 +196,12 @@ def test_streamed_task_two_ranks(tmp_path, engine, backend):
         pytest.skip("RCCL path needs two GPUs (one process per GPU); this box has one")
     ns: dict = {}
     exec(TASK.format(root=str(ROOT)), ns)
-    ns["run"](engine, tmp_path / "single", False, "full")
+    # "reductions": the sharded pre-aligned chain (row ranges per rank, subset state passed rank to
+    # rank, row minima gathered) against one rank streaming every block
+    ns["run"](engine, tmp_path / "single", variant == "reductions", variant)
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=str(ROOT)))
-    env = dict(os.environ, OUT=str(tmp_path / "dist"), OMP_NUM_THREADS="1", BACKEND=backend)
+    env = dict(os.environ, OUT=str(tmp_path / "dist"), OMP_NUM_THREADS="1", BACKEND=backend, VARIANT=variant)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
