@@ -164,6 +164,29 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
                         int64_t count, const taxi2_scores* sc, int both, int32_t cap, uint8_t* out_x,
                         uint8_t* out_y, int32_t* out_len);
 
+/* Metrics (nmetrics may be 0) AND aligned strings of the rectangle's pairs from ONE fill each: the
+ * packed trace-and-walk aligner's walkers write every alignment while they walk it, as
+ * versus_all.py:746-750 feeds one aligned pair to both the metrics and aligned_pairs.txt.  Device
+ * outputs on `stream` (asynchronous): d_out[(q - q0) * R + r][nmetrics] as taxi2_rect_pairs_dev,
+ * slots d_sx / d_sy [(q - q0) * R + r][cap] (right-aligned as taxi2_align_strings' slot 0, cap >=
+ * longest q + longest r) and lengths d_slen[(q - q0) * R + r].  Gotoh scores within int16, pairs up
+ * to 2 048 bp (else an error: use taxi2_align_strings). */
+int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1,
+                           const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* d_out,
+                           int32_t cap, uint8_t* d_sx, uint8_t* d_sy, int32_t* d_slen, void* stream);
+
+/* aligned_pairs.txt text (pairs.py:51-97 SequencePairHandler.Formatted) of the rectangle rows
+ * [q0, q1) x every r from taxi2_rect_strings_dev slots (device): per pair "idx / idy" LF, the
+ * aligned x, the pattern ('|' equal non-gap, '-' gap, '.' mismatch), the aligned y, each LF-ended;
+ * pairs separated by one LF, none before pair (q0, 0) when `first`.  Ids: concatenated bytes +
+ * offsets (rows: [q1 - q0 + 1], columns: [R + 1]).  Writes out[0, *out_len) on the host; returns 1
+ * without writing when out_cap < *out_len (retry with that capacity; the slots stay valid). */
+int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, int32_t cap,
+                           const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen,
+                           const uint8_t* row_ids, const int64_t* row_offs, const uint8_t* col_ids,
+                           const int64_t* col_offs, int first, uint8_t* out, int64_t out_cap,
+                           int64_t* out_len, void* stream);
+
 /* ---- NCD (distances.py:351-358 NCD._calculate -> alfpy 1.0.6 ncd.Distance) ---------------- *
  * NCD(x, y) = (C(X+Y) - min(C(X), C(Y))) / max(C(X), C(Y)), X / Y = upper-cased strings,
  * C(s) = len(zlib.compress(s)) with zlib 1.2.11 level 6 (computed exactly on the GPU).

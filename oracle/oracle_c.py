@@ -13,7 +13,8 @@ from pathlib import Path
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "_build" / "libtaxi2_oracle.so"
+# TAXI2_ORACLE_LIB: another build of the same source in _build/ (the sanitizer build, `make -C oracle san`)
+LIB_PATH = HERE / "_build" / os.path.basename(os.environ.get("TAXI2_ORACLE_LIB", "libtaxi2_oracle.so"))
 
 METRIC_CODES = {"p": 0, "p-gaps": 1, "jc": 2, "k2p": 3}
 
@@ -32,6 +33,8 @@ class CScores(ctypes.Structure):
 
 
 def build() -> Path:
+    if "TAXI2_ORACLE_LIB" in os.environ:
+        return LIB_PATH
     if not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < (HERE / "taxi2_oracle.c").stat().st_mtime:
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB_PATH

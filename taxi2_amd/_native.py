@@ -39,11 +39,13 @@ EXPORTS = (
     "taxi2_counts_metrics_dev",
     "taxi2_rect_pairs",
     "taxi2_rect_pairs_dev",
+    "taxi2_rect_strings_dev",
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
     "taxi2_ncd_pairs",
     "taxi2_zlib_lengths",
+    "taxi2_format_pairs_dev",
     "taxi2_format_rows",
     "taxi2_format_ragged",
     "taxi2_format_summary",
@@ -97,6 +99,10 @@ _SIGNATURES = {
     "taxi2_counts_metrics_dev": (_INT, [_P, _P, _I64, _P, _INT, ctypes.c_double, _P, _P]),
     "taxi2_rect_pairs": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_rect_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
+    "taxi2_rect_strings_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _I32, _P, _P,
+                                      _P, _P]),
+    "taxi2_format_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
+                                      ctypes.POINTER(_I64), _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
@@ -403,6 +409,47 @@ class Engine:
                 ),
                 "taxi2_rect_pairs_dev",
             )
+
+    def rect_strings_dev(self, q: SeqSet, r: SeqSet, q0: int, q1: int, metrics, out_ptr: int | None, cap: int,
+                         sx_ptr: int, sy_ptr: int, slen_ptr: int, scores=None, stream: int | None = None) -> None:
+        """Metrics (may be empty) and aligned strings of rows [q0, q1) x every r, one fill per pair
+        (device slots [(q - q0) * R + r][cap], right-aligned; see taxi2_rect_strings_dev)."""
+        codes = metric_codes(metrics) if metrics else np.zeros(0, dtype=np.int32)
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_rect_strings_dev(
+                    self._ctx, q.id, r.id, int(q0), int(q1), ctypes.byref(cs), codes.ctypes.data if len(codes) else None,
+                    len(codes), ctypes.c_void_p(out_ptr) if out_ptr else None, int(cap), ctypes.c_void_p(sx_ptr),
+                    ctypes.c_void_p(sy_ptr), ctypes.c_void_p(slen_ptr), ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_rect_strings_dev",
+            )
+
+    def format_pairs_dev(self, q: SeqSet, r: SeqSet, q0: int, q1: int, cap: int, sx_ptr: int, sy_ptr: int,
+                         slen_ptr: int, row_ids, col_ids, *, first: bool, stream: int | None = None) -> bytes:
+        """aligned_pairs.txt text of the slots of rows [q0, q1) (taxi2_format_pairs_dev).  row_ids /
+        col_ids: (bytes, offsets) from pack_strings."""
+        rb, ro = row_ids
+        cb, co = col_ids
+        need = _I64()
+        buf = getattr(self, "_pairs_buf", None)
+        if buf is None:
+            buf = np.empty(1 << 20, dtype=np.uint8)
+        for _ in range(2):
+            with self._lock:
+                rc = self._lib.taxi2_format_pairs_dev(
+                    self._ctx, q.id, r.id, int(q0), int(q1), int(cap), ctypes.c_void_p(sx_ptr), ctypes.c_void_p(sy_ptr),
+                    ctypes.c_void_p(slen_ptr), rb.ctypes.data, ro.ctypes.data, cb.ctypes.data, co.ctypes.data,
+                    1 if first else 0, buf.ctypes.data, buf.size, ctypes.byref(need),
+                    ctypes.c_void_p(stream) if stream else None)
+            if rc == 1:
+                buf = np.empty(max(int(need.value), 2 * buf.size), dtype=np.uint8)
+                continue
+            self._check(rc, "taxi2_format_pairs_dev")
+            self._pairs_buf = buf
+            return buf[: need.value].tobytes()
+        raise NativeError("taxi2_format_pairs_dev: output buffer sizing failed")
 
     def list_pairs(self, x: SeqSet, y: SeqSet, xs, ys, metrics, scores=None, *, with_scores=False):
         """Explicit pairs.  ALIGN: (count, 2, M) [(x,y), (y,x)]; else (count, M)."""

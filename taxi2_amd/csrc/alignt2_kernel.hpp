@@ -258,6 +258,19 @@ __device__ __forceinline__ uint2 a2_row_record(const ChainPair* __restrict__ tab
     return make_uint2(w0 | (w1 << 16), y);
 }
 
+// Optional aligned strings (round 3): every walk also writes its alignment, right-aligned in the
+// slot of its ordered pair -- bytes [nA + nB - len, nA + nB) of sx / sy + slot * cap, len in
+// slen[slot], slot = p * nslot + o (o = 0 the (a, b) alignment, 1 the (b, a) one; nslot = 1 for
+// single-orientation launches) -- in (a, b) column order: sx holds a's side, sy b's, whichever
+// sequence the chain put on the rows.  One fill then serves the metrics AND aligned_pairs.txt
+// (versus_all.py:746-750 feeds the same aligned pair to both).
+struct StrOut {
+    uint8_t* sx;
+    uint8_t* sy;
+    int32_t* slen;
+    int cap, nslot;
+};
+
 // RAW: the raw-difference trace (default scores; 4 K bytes per lane and step, [step][lane][k] words),
 // else the sign-digit code (2 K bytes per lane and step, [step][lane][k][stream] bytes)
 template <int K, int W, bool DEF, bool RAW>
@@ -265,7 +278,7 @@ __device__ __forceinline__ void
 alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
              double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
              int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
-             unsigned long long* __restrict__ esc_n) {
+             unsigned long long* __restrict__ esc_n, StrOut so) {
     static_assert(K % 2 == 0 && K <= 16, "16-bit score fields: K / 2 words per stream and base");
     static_assert(!RAW || DEF, "the raw-difference bounds are those of the default scores");
     constexpr int TB = RAW ? 4 * K : 2 * K;  // trace bytes per lane and step
@@ -368,7 +381,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         int i = W_.i, j = W_.j, first = W_.first;
         uint32_t cb = W_.cb, xa = W_.xa, yb = W_.yb;
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
-        int sc2 = W_.sc2;
+        int sc2 = W_.sc2, ncol = W_.ncol;
         const int nA_ = cp.nA, nB_ = ch.nB;
         for (int h = 0; budget < 0 || h < budget; ++h) {
             if (!__any(st < AT_DONE)) break;
@@ -397,6 +410,14 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 ni = i;
                 nj = j - 1;
             }
+            if (so.sx && !first) {  // this column of the alignment, right to left, in (a, b) order
+                const uint32_t rc = st == AT_IY ? (uint32_t)'-' : xa, cc = st == AT_IX ? (uint32_t)'-' : yb;
+                const size_t o = ((size_t)cp.p * so.nslot + ((prio ^ cp.swp) & (so.nslot - 1))) * (size_t)so.cap +
+                                 (size_t)(nA_ + nB_ - 1 - ncol);
+                so.sx[o] = (uint8_t)(cp.swp ? cc : rc);
+                so.sy[o] = (uint8_t)(cp.swp ? rc : cc);
+                ++ncol;
+            }
             first = 0;
             if constexpr (RAW) {
                 if (ni == 0 && nj == 0) {  // the gap run (if any) opened at the start: end-gap open
@@ -419,6 +440,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                     o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
                 if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK && fin[pb][pi] != (int)AT_POISON_LDS, AG_FIN))  // undo the drift of cell (nA, nB)
                     sout[p] = (fin[pb][pi] + (cp.nA + chs[pb].nB) * dz) >> 1;
+                if (so.slen) so.slen[p * so.nslot + ((prio ^ cp.swp) & (so.nslot - 1))] = ncol;
                 st = AT_DONE;
                 continue;
             }
@@ -540,6 +562,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         W_.tv = tv;
         W_.gap = gap;
         W_.sc2 = sc2;
+        W_.ncol = ncol;
     };
 
     // The fill waves and the walker wave run separate copies of the chain loop (same barrier
@@ -580,6 +603,20 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                             if (sout) {
                                 const int ne = ma.x + mb.x;
                                 sout[p] = ne == 0 ? 0 : sc0.eo + sc0.ee * (ne - 1);
+                            }
+                            if (so.sx) {  // the other sequence against gaps, every slot alike
+                                const int L = ma.x + mb.x;
+                                const uint8_t* xs_ = XS.bytes + XS.offs[a];
+                                const uint8_t* ys_ = YS.bytes + YS.offs[b];
+                                for (int o = 0; o < so.nslot; ++o) {
+                                    uint8_t* ox = so.sx + ((size_t)p * so.nslot + o) * (size_t)so.cap;
+                                    uint8_t* oy = so.sy + ((size_t)p * so.nslot + o) * (size_t)so.cap;
+                                    for (int t = 0; t < L; ++t) {
+                                        ox[t] = ma.x ? xs_[t] : (uint8_t)'-';
+                                        oy[t] = mb.x ? ys_[t] : (uint8_t)'-';
+                                    }
+                                    so.slen[p * so.nslot + o] = L;
+                                }
                             }
                             continue;
                         }
@@ -942,9 +979,9 @@ __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
           double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
           int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
-          unsigned long long* __restrict__ esc_n) {
+          unsigned long long* __restrict__ esc_n, StrOut so) {
     alignt2_body<K, W, DEF, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
-                                 hops, next, band, esc_list, esc_n);
+                                 hops, next, band, esc_list, esc_n, so);
 }
 // ... and the full-trace pass over the pairs it queued (ps.sel / ps.dcount): a kernel of its own
 // name, so a profile shows the second pass (normally empty) apart from the first.  It stores the
@@ -954,9 +991,9 @@ template <int K, int W, bool DEF, int OCC>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2_queued(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
                  double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
-                 int cap_rows, int hops, unsigned long long* __restrict__ next) {
+                 int cap_rows, int hops, unsigned long long* __restrict__ next, StrOut so) {
     alignt2_body<K, W, DEF, false>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
-                                   hops, next, 0, nullptr, nullptr);
+                                   hops, next, 0, nullptr, nullptr, so);
 }
 
 }  // namespace taxi2

@@ -78,7 +78,8 @@ struct AtWalk {  // one walk: position, state, its cell's trace byte, bytes of t
     int i, j, st, first, pi, prio;
     uint32_t cb, xa, yb;
     int valid, ts, tv, gap;
-    int sc2;  // raw-difference walks (alignt2_kernel.hpp): doubled score of the moves so far
+    int sc2;   // raw-difference walks (alignt2_kernel.hpp): doubled score of the moves so far
+    int ncol;  // alignt2_kernel.hpp string output: alignment columns written so far
 };
 
 template <int K, int W, bool DEF, int OCC>

@@ -391,13 +391,13 @@ struct VariantT {
     bool def;
     const void* fn;
     void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int, int, double*,
-                   int32_t*, uint8_t*, int64_t, int, int, unsigned long long*, BandArgs);
+                   int32_t*, uint8_t*, int64_t, int, int, unsigned long long*, BandArgs, StrOut);
 };
 
 template <int K, int W, bool DEF, int OCC>
 void launch_alignt(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                    int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
-                   unsigned long long* nx, BandArgs) {
+                   unsigned long long* nx, BandArgs, StrOut) {  // no string output (launch_packed_strings)
     hipLaunchKernelGGL((k_alignt<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
                        hops, nx);
 }
@@ -425,13 +425,13 @@ const VariantT* pick_variantt(const KScores& k, int max_len) {
 template <int K, int W, bool DEF, int OCC>
 void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                     int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
-                    unsigned long long* nx, BandArgs ba) {
+                    unsigned long long* nx, BandArgs ba, StrOut str) {
     if (ps.sel)  // the queued pairs of a band pass, full trace
         hipLaunchKernelGGL((k_alignt2_queued<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr,
-                           bb, cap, hops, nx);
+                           bb, cap, hops, nx, str);
     else
         hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
-                           hops, nx, ba.band, ba.esc_list, ba.esc_n);
+                           hops, nx, ba.band, ba.esc_list, ba.esc_n, str);
 }
 
 const VariantT kAlignT2[] = {
@@ -451,7 +451,7 @@ const VariantT* pick_variantt2(const KScores& k, int max_len) {
 // packed: two streams per chain, two trace bytes per lane-column and step
 int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
-                        hipStream_t st, int max_len, bool packed) {
+                        hipStream_t st, int max_len, bool packed, StrOut str = StrOut{}) {
     // resident workgroups of the kernel (VGPR and LDS limits), persistent grid
     int per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 64 * (v.W + 1), 0));
@@ -503,14 +503,14 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 64, st));
     v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), ps, k, ms, chunk, out_mode, d_out,
              d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next,
-             BandArgs{band, queue ? esc_list : nullptr, esc_n});
+             BandArgs{band, queue ? esc_list : nullptr, esc_n}, str);
     HIP_TRY(ctx, hipGetLastError());
     if (queue) {  // the queued pairs (usually none: the workgroups exit at once), full trace
         PairSrc p2 = ps;
         p2.sel = esc_list;
         p2.dcount = esc_n;
         v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), p2, k, ms, chunk, out_mode, d_out,
-                 d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next2, BandArgs{0, nullptr, nullptr});
+                 d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next2, BandArgs{0, nullptr, nullptr}, str);
         HIP_TRY(ctx, hipGetLastError());
         if (getenv("TAXI2_AT_BAND_STATS")) {  // diagnostics: queued pairs of this call on stderr
             unsigned long long q = 0;
@@ -659,6 +659,27 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
               out_mode, d_out, d_scores);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
+}
+
+// Metrics (optional) AND aligned strings from one fill per launched pair: the packed trace-and-walk
+// kernel's walkers write each alignment as they walk it (alignt2_kernel.hpp StrOut).  Returns 1
+// without launching when that kernel does not cover the shape (linear scores, past 2 048 columns,
+// scores outside int16); the caller then uses the trace kernels (Tracer) or the column-tiled aligner.
+int launch_packed_strings(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps, const taxi2_scores* sc,
+                          const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores, hipStream_t st,
+                          StrOut str) {
+    const KScores k = kscores(sc);
+    const int max_len = std::max(X.max_len, Y.max_len);
+    if (is_linear(k) || !at_fits16(k, max_len) || getenv("TAXI2_NO_ALIGNT") || getenv("TAXI2_NO_PACKED") ||
+        getenv("TAXI2_LONG") || getenv("TAXI2_NO_WALK_STRINGS"))
+        return 1;
+    const VariantT* vt = pick_variantt2(k, max_len);
+    if (!vt) return 1;
+    if (ps.count <= 0) return 0;
+    if (str.cap < X.max_len + Y.max_len)
+        return fail(ctx, "string slots of %d bytes < longest x + longest y (%d)", str.cap, X.max_len + Y.max_len);
+    const int rc = launch_alignt_pairs(ctx, *vt, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, max_len, true, str);
+    return rc ? -1 : 0;
 }
 
 // host copy of the triangle row of linear pair index g (common.hpp decode_pair)
@@ -1152,6 +1173,28 @@ int taxi2_rect_pairs(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q
     return run_pairs(ctx, *Q, *R, ps, sc, ms, OUT_AB, out, scores_out);
 }
 
+int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
+                           const int32_t* metrics, int nmetrics, double* d_out, int32_t cap, uint8_t* d_sx,
+                           uint8_t* d_sy, int32_t* d_slen, void* stream) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (Q->mode != TAXI2_MODE_ALIGN || R->mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need ALIGN sets");
+    if (!sc) return fail(ctx, "scores required");
+    MetricSpec ms{};
+    if (nmetrics > 0 && check_metrics(ctx, metrics, nmetrics, ms, true, std::max(Q->max_len, R->max_len))) return -1;
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if ((q1 - q0) * R->n > 0 && (!d_sx || !d_sy || !d_slen || (nmetrics > 0 && !d_out))) return fail(ctx, "null output");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairSrc ps{PAIRS_RECT, q0 * R->n, (q1 - q0) * R->n, 0, R->n, nullptr, nullptr};
+    const int rc = launch_packed_strings(ctx, *Q, *R, ps, sc, ms, OUT_AB, d_out, nullptr, st,
+                                         StrOut{d_sx, d_sy, d_slen, cap, 1});
+    if (rc > 0) return fail(ctx, "walker strings need the packed aligner (Gotoh scores within int16, <= 2 048 bp)");
+    return rc;
+}
+
 int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
                          const int32_t* metrics, int nmetrics, double* d_out, int32_t* d_scores, void* stream) {
     if (!ctx) return -1;
@@ -1298,6 +1341,33 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
     if (cap < X->max_len + Y->max_len) return fail(ctx, "cap %d < longest x + longest y", cap);
     if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (X->mode != TAXI2_MODE_ALIGN || Y->mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need ALIGN sets");
+    {  // the packed trace-and-walk kernel writes the strings while it walks (one fill per pair)
+        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)1 << 30) / (4 * (int64_t)cap + 16)));
+        const size_t bytes = (size_t)chunk * 2 * (8 + 4) + (size_t)chunk * 2 * 2 * cap;
+        if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, bytes)) return -1;
+        int64_t* d_idx = (int64_t*)ctx->d_aux;
+        int32_t* d_len = (int32_t*)(d_idx + 2 * chunk);
+        uint8_t* d_sx = (uint8_t*)(d_len + 2 * chunk);
+        uint8_t* d_sy = d_sx + (size_t)chunk * 2 * cap;
+        MetricSpec none{};
+        int rc = 1;
+        for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+            const int64_t n = std::min(chunk, count - c0);
+            HIP_TRY(ctx, hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+            PairSrc ps{PAIRS_LIST, 0, n, 0, 0, d_idx, d_idx + chunk};
+            rc = launch_packed_strings(ctx, *X, *Y, ps, sc, none, both ? OUT_BOTH : OUT_AB, nullptr, nullptr,
+                                       ctx->stream, StrOut{d_sx, d_sy, d_len, cap, 2});
+            if (rc < 0) return -1;
+            if (rc > 0) break;  // not this kernel's shape: the trace kernels below
+            HIP_TRY(ctx, hipMemcpyAsync(out_x + c0 * 2 * cap, d_sx, (size_t)n * 2 * cap, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(out_y + c0 * 2 * cap, d_sy, (size_t)n * 2 * cap, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(out_len + c0 * 2, d_len, (size_t)n * 2 * 4, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        if (rc == 0) return 0;
+    }
     Tracer tr;
     if (tr.setup(ctx, *X, *Y, kscores(sc), cap)) return -1;
     for (int64_t c0 = 0; c0 < count; c0 += tr.chunk) {
@@ -1568,6 +1638,62 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
 }
 
 extern "C" {
+
+int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, int32_t cap,
+                           const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, const uint8_t* row_ids,
+                           const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, int first,
+                           uint8_t* out, int64_t out_cap, int64_t* out_len, void* stream) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if (!out_len || !row_offs || !col_offs) return fail(ctx, "null argument");
+    const int64_t nrows = q1 - q0, ncols = R->n;
+    *out_len = 0;
+    if (nrows == 0 || ncols == 0) return 0;
+    if (!d_sx || !d_sy || !d_slen) return fail(ctx, "null string slots");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    const int64_t rb = row_offs[nrows] - row_offs[0], cb = col_offs[ncols] - col_offs[0];
+    auto al = [](size_t v) { return (v + 255) / 256 * 256; };
+    const size_t o_ro = 0, o_co = o_ro + al((size_t)(nrows + 1) * 8), o_rid = o_co + al((size_t)(ncols + 1) * 8);
+    const size_t o_cid = o_rid + al((size_t)rb + 1), o_len = o_cid + al((size_t)cb + 1);
+    const size_t o_base = o_len + al((size_t)nrows * 8), fixed = o_base + al((size_t)nrows * 8);
+    if (ensure(ctx, &ctx->d_fmt, &ctx->d_fmt_bytes, fixed)) return -1;
+    char* b = (char*)ctx->d_fmt;
+    std::vector<int64_t> ro(nrows + 1), co(ncols + 1);
+    for (int64_t r = 0; r <= nrows; ++r) ro[r] = row_offs[r] - row_offs[0];
+    for (int64_t c = 0; c <= ncols; ++c) co[c] = col_offs[c] - col_offs[0];
+    HIP_TRY(ctx, hipMemcpyAsync(b + o_ro, ro.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx, hipMemcpyAsync(b + o_co, co.data(), (ncols + 1) * 8, hipMemcpyHostToDevice, st));
+    if (rb) HIP_TRY(ctx, hipMemcpyAsync(b + o_rid, row_ids + row_offs[0], rb, hipMemcpyHostToDevice, st));
+    if (cb) HIP_TRY(ctx, hipMemcpyAsync(b + o_cid, col_ids + col_offs[0], cb, hipMemcpyHostToDevice, st));
+    PairFmtArgs a{d_sx, d_sy, d_slen, (int64_t)cap, Q->meta + q0, R->meta, ncols, (const uint8_t*)(b + o_rid),
+                  (const int64_t*)(b + o_ro), (const uint8_t*)(b + o_cid), (const int64_t*)(b + o_co), first ? 1 : 0};
+    int64_t* d_rlen = (int64_t*)(b + o_len);
+    int64_t* d_rbase = (int64_t*)(b + o_base);
+    hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rlen);
+    HIP_TRY(ctx, hipGetLastError());
+    std::vector<int64_t> rlen(nrows), rbase(nrows);
+    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nrows * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(ctx, hipStreamSynchronize(st));
+    int64_t total = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+        rbase[r] = total;
+        total += rlen[r];
+    }
+    *out_len = total;
+    if (total > out_cap) return 1;  // caller retries with a buffer of *out_len bytes
+    if (!out) return fail(ctx, "null output buffer");
+    if (ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 1)) return -1;
+    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nrows * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rbase, (char*)ctx->d_out);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(ctx, hipStreamSynchronize(st));
+    return 0;
+}
 
 int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,
                       const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,

@@ -237,6 +237,113 @@ k_fmt_rows(FmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ o
         __syncthreads();
     }
 }
+
+// ---- aligned_pairs.txt (pairs.py:51-97 SequencePairHandler.Formatted, fed x-major by
+// versus_all.py:746-750): per ordered pair
+//   idx " / " idy LF  X LF  pattern LF  Y LF
+// blocks separated by one LF (none before the file's first pair); pattern[c] = '|' for equal
+// non-gap bytes, '-' when either side is a gap, '.' otherwise (Formatted._format_char).  The
+// aligned strings come from the packed aligner's walkers (alignt2_kernel.hpp StrOut, one slot per
+// pair): right-aligned, the alignment of (x, y) ends at byte len(x) + len(y) of its slot.
+struct PairFmtArgs {
+    const uint8_t* sx;
+    const uint8_t* sy;
+    const int32_t* slen;
+    int64_t cap;
+    const int4* qmeta;  // lengths of the row set, from q0
+    const int4* rmeta;  // lengths of the column set
+    int64_t ncols;
+    const uint8_t* rid;  // ids: concatenated bytes + offsets (row ids start at row q0)
+    const int64_t* roffs;
+    const uint8_t* cid;
+    const int64_t* coffs;
+    int first;  // 1: the block's pair (0, 0) opens the file (no separator before it)
+};
+
+__device__ __forceinline__ int64_t pair_fmt_len(const PairFmtArgs& a, int64_t r, int64_t c) {
+    const int64_t L = a.slen[r * a.ncols + c];
+    const int64_t lx = a.roffs[r + 1] - a.roffs[r], ly = a.coffs[c + 1] - a.coffs[c];
+    return ((r | c) || !a.first ? 1 : 0) + lx + 3 + ly + 1 + 3 * (L + 1);
+}
+
+// Pass 1: text length of each row of pairs.
+__global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_len(PairFmtArgs a, int64_t* __restrict__ row_len) {
+    __shared__ int64_t red[FMT_BLOCK];
+    const int64_t r = blockIdx.x;
+    int64_t s = 0;
+    for (int64_t c = threadIdx.x; c < a.ncols; c += FMT_BLOCK) s += pair_fmt_len(a, r, c);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = FMT_BLOCK / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) row_len[r] = red[0];
+}
+
+// Pass 2: one workgroup per row; the pair offsets of 256 columns at a time by an LDS scan, then
+// each wave writes whole pairs, its lanes striding over the pair's bytes (coalesced stores).
+__global__ void __launch_bounds__(FMT_BLOCK)
+k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out) {
+    __shared__ int64_t scan[FMT_BLOCK];
+    const int64_t r = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int64_t base = row_base[r];
+    const int lx = (int)(a.roffs[r + 1] - a.roffs[r]);
+    const uint8_t* idx = a.rid + a.roffs[r];
+    const int nx = a.qmeta[r].x;
+    for (int64_t c0 = 0; c0 < a.ncols; c0 += FMT_BLOCK) {
+        const int64_t c = c0 + threadIdx.x;
+        const int64_t len = c < a.ncols ? pair_fmt_len(a, r, c) : 0;
+        scan[threadIdx.x] = len;
+        __syncthreads();
+        for (int w = 1; w < FMT_BLOCK; w <<= 1) {
+            const int64_t add = threadIdx.x >= w ? scan[threadIdx.x - w] : 0;
+            __syncthreads();
+            scan[threadIdx.x] += add;
+            __syncthreads();
+        }
+        const int nc = (int)min((int64_t)FMT_BLOCK, a.ncols - c0);
+        for (int q = wv; q < nc; q += FMT_BLOCK / 64) {
+            const int64_t cc = c0 + q;
+            const int64_t k = r * a.ncols + cc;
+            const int64_t plen = scan[q] - (q ? scan[q - 1] : 0);
+            char* o = out + base + scan[q] - plen;
+            const int sep = ((r | cc) || !a.first) ? 1 : 0;
+            const int ly = (int)(a.coffs[cc + 1] - a.coffs[cc]);
+            const uint8_t* idy = a.cid + a.coffs[cc];
+            const int L = a.slen[k];
+            const int64_t end = (int64_t)nx + a.rmeta[cc].x;
+            const uint8_t* X = a.sx + k * a.cap + end - L;
+            const uint8_t* Y = a.sy + k * a.cap + end - L;
+            const int h = sep + lx + 3 + ly + 1;  // header with its separator
+            for (int64_t t = lane; t < plen; t += 64) {
+                char ch;
+                if (t < h) {
+                    const int u = (int)t - sep;
+                    ch = u < 0 ? '\n' : u < lx ? (char)idx[u] : u < lx + 3 ? " / "[u - lx] : u < lx + 3 + ly ? (char)idy[u - lx - 3] : '\n';
+                } else {
+                    const int64_t v = t - h;
+                    const int line = (int)(v / (L + 1));
+                    const int col = (int)(v - (int64_t)line * (L + 1));
+                    if (col == L) {
+                        ch = '\n';
+                    } else if (line == 0) {
+                        ch = (char)X[col];
+                    } else if (line == 2) {
+                        ch = (char)Y[col];
+                    } else {
+                        const uint8_t p = X[col], q2 = Y[col];
+                        ch = (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
+                    }
+                }
+                o[t] = ch;
+            }
+        }
+        base += scan[FMT_BLOCK - 1];
+        __syncthreads();
+    }
+}
 #endif
 
 }  // namespace taxi2

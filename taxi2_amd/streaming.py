@@ -142,13 +142,25 @@ class TriangleStore:
         if self.world > 1:
             import torch.distributed as dist
 
+            # every peer's entries in flight at once (one receive per rank, posted together: RCCL
+            # groups them into one launch, so all xGMI links into rank 0 carry data concurrently)
+            recvs = []
             for r in range(1, self.world):
                 q0, q1 = self.rows[r]
                 cnt = block_entry_count(self.n, q0, q1, x0, x1)
                 if cnt == 0:
                     continue
                 buf = torch.empty(cnt * len(names), dtype=torch.int64, device=self.device)
-                dist.recv(buf, src=_global(group, r), group=group)
+                recvs.append((r, q0, q1, buf))
+            if recvs:
+                if dist.get_backend(group) == "nccl":
+                    ops = [dist.P2POp(dist.irecv, buf, _global(group, r), group) for r, _, _, buf in recvs]
+                    reqs = dist.batch_isend_irecv(ops)
+                else:
+                    reqs = [dist.irecv(buf, src=_global(group, r), group=group) for r, _, _, buf in recvs]
+                for q in reqs:
+                    q.wait()
+            for r, q0, q1, buf in recvs:
                 parts.append((block_entries(self.n, q0, q1, x0, x1, self.device)[1], buf))
         out = {nm: self._blank(nm, x1 - x0) for nm in names}
         for d, buf in parts:

@@ -123,6 +123,64 @@ def write_summary(path: Path, seqs: list, A: np.ndarray, metrics: list, genera, 
             )) + "\n")
 
 
+class SummaryRuns:
+    """summary.tsv with the handler's line grouping (runs of consecutive pairs with equal
+    (x.id, y.id) share one line; the header repeats the metric labels for the FIRST run's length,
+    as write_summary's grouped path) fed x-major row blocks: a run may span two blocks (the last
+    pair of a block's last row and the first of the next block's first row), so the open run is
+    carried over.  For duplicate ids on the streamed path."""
+
+    def __init__(self, fh, seqs: list, metrics: list, genera, species, fmt: str, missing: str):
+        self.fh, self.seqs, self.metrics = fh, seqs, metrics
+        self.fmt, self.missing = fmt, missing
+        self.ids = [s.id for s in seqs]
+        self.gx = [genera.get(i, None) for i in self.ids] if genera else None
+        self.sx = [species.get(i, None) for i in self.ids] if species else None
+        self.head = ["seqid (query 1)", "seqid (query 2)", *[str(m) for m in metrics],
+                     *[k + " (query 1)" for k in seqs[0].extras], *[k + " (query 2)" for k in seqs[0].extras],
+                     "genus (query 1)", "species (query 1)", "genus (query 2)", "species (query 2)",
+                     "comparison_type"]
+        self.first = True
+        self.run: list = []
+        self.key = None
+
+    def feed(self, A: np.ndarray, x0: int) -> None:
+        text = _values_text(A, self.fmt, self.missing)
+        ids = self.ids
+        for r in range(A.shape[0]):
+            i = x0 + r
+            for j in range(len(ids)):
+                k = (ids[i], ids[j])
+                if self.run and k != self.key:
+                    self._emit()
+                self.key = k
+                self.run.append((i, j, text[r, j]))
+
+    def _emit(self) -> None:
+        run, self.run = self.run, []
+        i0, j0, _ = run[0]
+        if self.first:
+            self.head[2 : 2 + len(self.metrics)] = [str(m) for _ in run for m in self.metrics]
+            self.fh.write("\t".join(self.head) + "\n")
+            self.first = False
+        x, y = self.seqs[i0], self.seqs[j0]
+        gx, sx, missing = self.gx, self.sx, self.missing
+        g = SubsetPair(gx[i0], gx[j0]) if gx is not None else None
+        s = SubsetPair(sx[i0], sx[j0]) if sx is not None else None
+        self.fh.write("\t".join((
+            x.id, y.id, *[t for _, _, tt in run for t in tt],
+            *[v if v is not None else missing for v in x.extras.values()],
+            *[v if v is not None else missing for v in y.extras.values()],
+            (g.x if g else None) or "-", (s.x if s else None) or "-",
+            (g.y if g else None) or "-", (s.y if s else None) or "-",
+            comparison_type(g, s),
+        )) + "\n")
+
+    def close(self) -> None:
+        if self.run:
+            self._emit()
+
+
 def summary_lines(A: np.ndarray, x0: int, seqs: list, metrics: list, genera, species, fmt: str,
                   missing: str) -> str:
     """summary.tsv lines of the rows [x0, x0 + len(A)) x all columns, unique ids (one line per

@@ -132,6 +132,13 @@ TASK = textwrap.dedent(
         elif variant == "prealigned":
             t.params.pairs.align = False
             t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.JukesCantor()]
+        elif variant == "dupids":  # duplicate ids (handler line grouping across row blocks), %g formatter
+            for k in (2, 3, 4, 9):
+                seqs[k] = Sequence("same", seqs[k].seq, seqs[k].extras)
+            seqs[6] = Sequence("s5", seqs[6].seq, seqs[6].extras)
+            t.input.sequences = Sequences(seqs)
+            t.params.format.float = "{:.5g}"
+            t.input.genera = Partition({{s.id: "g%d" % (k % 2) for k, s in enumerate(seqs)}})
         elif variant == "reductions":  # config-5 shape: pre-aligned, no N x N text, reductions only
             t.params.pairs.align = False
             t.params.pairs.write = False
@@ -152,7 +159,7 @@ def _files(root):
     return sorted(p.relative_to(root) for p in root.rglob("*") if p.is_file())
 
 
-@pytest.mark.parametrize("variant", ["full", "generic", "prealigned"])
+@pytest.mark.parametrize("variant", ["full", "generic", "prealigned", "dupids"])
 def test_streamed_task_matches_dense(tmp_path, engine, variant):
     ns: dict = {}
     exec(TASK.format(root=str(ROOT)), ns)
@@ -260,3 +267,30 @@ def test_streamed_reductions_only(tmp_path, engine):
     for f in sorted((tmp_path / "dense" / "subsets").rglob("*.tsv")):
         rel = f.relative_to(tmp_path / "dense")
         assert (tmp_path / "red" / rel).read_bytes() == f.read_bytes(), rel
+
+
+def test_streamed_wide_sequences_match_dense(tmp_path, engine):
+    """Past 32 767 bp the streamed store keeps f64 metric planes instead of 16-bit packed counters
+    (aligned pairs of ~33 kb, the column-tiled aligner)."""
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    base = random_sequences(1, 33000, 33000, 301, "ACGT")[0]
+    raw = [base, mutate([base], 302, rate=0.02)[0], mutate([base], 303, rate=0.05)[0][:32900]]
+    seqs = Sequences([Sequence(f"w{k}", s) for k, s in enumerate(raw)])
+
+    def run(out, stream):
+        t = VersusAll()
+        t.engine, t.progress_handler, t.work_dir = engine, None, out
+        t.input.sequences = seqs
+        t.params.pairs.write = False
+        t.params.engine.stream = stream
+        t.params.engine.block_bytes = 2 * len(raw) * 8 * 8
+        t.start()
+
+    run(tmp_path / "dense", False)
+    run(tmp_path / "stream", True)
+    files = _files(tmp_path / "dense")
+    assert files and files == _files(tmp_path / "stream")
+    for f in files:
+        assert (tmp_path / "stream" / f).read_bytes() == (tmp_path / "dense" / f).read_bytes(), f

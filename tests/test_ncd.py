@@ -8,6 +8,7 @@ value: parity is pinned to zlib's own output.
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 import shutil
 import subprocess
@@ -20,11 +21,11 @@ from tests.conftest import ROOT
 
 @pytest.fixture(scope="module")
 def zlen_host(tmp_path_factory):
-    gxx = shutil.which("g++")
+    gxx = os.environ.get("TAXI2_HOST_CXX") or shutil.which("g++")
     if gxx is None:
         pytest.skip("g++ not available")
     out = tmp_path_factory.mktemp("zlen") / "libzlen_host.so"
-    subprocess.run([gxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(out),
+    subprocess.run([gxx, "-O2", "-std=c++17", "-shared", "-fPIC", *os.environ.get("TAXI2_HOST_CFLAGS", "").split(), "-o", str(out),
                     str(ROOT / "tests/native/zlen_host.cpp")], check=True)
     lib = ctypes.CDLL(str(out))
     lib.zlen_host.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]

@@ -7,6 +7,7 @@ GPU: taxi2_format_rows (linear / matrix text) vs the Python rendering of the sam
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 import shutil
 import struct
@@ -42,11 +43,11 @@ def _values(seed: int, n: int) -> list[float]:
 
 @pytest.fixture(scope="module")
 def fmt_host(tmp_path_factory):
-    gxx = shutil.which("g++")
+    gxx = os.environ.get("TAXI2_HOST_CXX") or shutil.which("g++")
     if gxx is None:
         pytest.skip("g++ not available")
     out = tmp_path_factory.mktemp("fmt") / "libfmt_host.so"
-    subprocess.run([gxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(out),
+    subprocess.run([gxx, "-O2", "-std=c++17", "-shared", "-fPIC", *os.environ.get("TAXI2_HOST_CFLAGS", "").split(), "-o", str(out),
                     str(ROOT / "tests/native/fmt_host.cpp")], check=True)
     lib = ctypes.CDLL(str(out))
     lib.fmt_host.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_char_p]
