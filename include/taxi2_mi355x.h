@@ -193,15 +193,15 @@ int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
  * For each pair k: out[k*no] = value of the ordered pair (x, y) and, when both != 0 (no = 2),
  * out[k*2+1] = value of (y, x).  With scores (ALIGN sets): x, y are the first Biopython
  * alignment's gapped strings of that ordered pair, as VersusAll feeds them to the metric
- * (versus_all.py:532, 546-552); scores == NULL: the sequences as stored.  Raw sequences must
- * satisfy len(x) + len(y) <= 65273 and aligned strings 2 (len(x) + len(y)) <= 65273 (one deflate window;
- * the length accounts for every deflate block, deflate_len.hpp). */
+ * (versus_all.py:532, 546-552); scores == NULL: the sequences as stored.  Any length: the
+ * length accounts for every deflate block and every slide of zlib's 64 KiB window
+ * (deflate_len.hpp); bytes are compressed as given (the Python layer hands UTF-8). */
 int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                     int64_t count, const taxi2_scores* sc, int both, double* out);
 
 /* ---- compressed length (alfpy ncd.complexity) --------------------------------------------- *
  * out[k] = len(zlib.compress(upper(x[xs[k]]) + upper(y[ys[k]]))), zlib 1.2.11 level 6;
- * ys == NULL compresses x[xs[k]] alone.  Inputs up to 65273 bytes. */
+ * ys == NULL compresses x[xs[k]] alone.  Any length. */
 int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                        int64_t count, int32_t* out);
 

@@ -73,6 +73,11 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 #ifndef A2_SKIP_OUT_OF_BAND
 #define A2_SKIP_OUT_OF_BAND 1
 #endif
+// 1: the per-column substitution words come from ds_read_u16_d16 / _d16_hi pairs (LDS assembles
+// the (stream 0, stream 1) halves) instead of two ds_read_b128 and a v_perm per column
+#ifndef A2_D16_SUB
+#define A2_D16_SUB 0
+#endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
 #endif
@@ -785,6 +790,44 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     carry = (pk2b(c0, c0) & m) | (carry & ~m);
                                 }
                                 // substitution words of both rows
+#if A2_D16_SUB
+                                // substitution words of both rows, one per column, assembled by the LDS
+                                // itself: ds_read_u16_d16 fills the low half (stream 0's row base),
+                                // ds_read_u16_d16_hi the high half (stream 1's) -- no v_perm per column
+                                uint32_t sw[K];
+                                {
+                                    const uint32_t a0 = (uint32_t)(uintptr_t)&eqt[(rw >> 11) & 3u][tq][0];
+                                    const uint32_t a1 = (uint32_t)(uintptr_t)&eqt[(rw >> 27) & 3u][tq][0];
+    #pragma unroll
+                                    for (int k = 0; k < K; ++k)
+                                        asm volatile("ds_read_u16_d16 %0, %1 offset:%3\n\tds_read_u16_d16_hi %0, %2 offset:%3"
+                                                     : "=&v"(sw[k]) : "v"(a0), "v"(a1), "i"(2 * k));
+                                    // the words are defined only after this wait (the compiler does not
+                                    // track inline-asm LDS loads): redefine them here
+                                    static_assert(K == 8 || K == 6 || K == 4, "d16 substitution: K in {4, 6, 8}");
+                                    if constexpr (K == 8)
+                                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sw[0]), "+v"(sw[1]), "+v"(sw[2]), "+v"(sw[3]),
+                                                     "+v"(sw[4]), "+v"(sw[5]), "+v"(sw[6]), "+v"(sw[7]));
+                                    else if constexpr (K == 6)
+                                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sw[0]), "+v"(sw[1]), "+v"(sw[2]), "+v"(sw[3]),
+                                                     "+v"(sw[4]), "+v"(sw[5]));
+                                    else
+                                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sw[0]), "+v"(sw[1]), "+v"(sw[2]), "+v"(sw[3]));
+                                }
+                                if (rw & (A2_OTHER | (A2_OTHER << 16))) {  // a row byte other than A/C/G/T
+                                    const uint8_t* cseq = chs[cur].cseq;
+                                    const uint32_t b0 = rw & 0xFFu, b1 = (rw >> 16) & 0xFFu;
+    #pragma unroll
+                                    for (int k = 0; k < K; ++k) {
+                                        const int jc = j0 + k;
+                                        const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
+                                        const int s0_ = ((cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi) - 2 * dz;
+                                        const int s1_ = ((cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi) - 2 * dz;
+                                        if (rw & A2_OTHER) sw[k] = (sw[k] & 0xFFFF0000u) | ((uint32_t)s0_ & 0xFFFFu);
+                                        if (rw & (A2_OTHER << 16)) sw[k] = (sw[k] & 0xFFFFu) | ((uint32_t)s1_ << 16);
+                                    }
+                                }
+#else
                                 uint32_t eq0[KW], eq1[KW];
                                 {
                                     // the per-thread table address is recomputed here (one op) rather
@@ -816,6 +859,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         if (rw & (A2_OTHER << 16)) eq1[q] = v1;
                                     }
                                 }
+#endif
                                 // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
                                 // minus 1 because the F payload is kept odd (below)
                                 const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
@@ -844,7 +888,12 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     const at_s2 G1 = as_s2(as_u32(G) | 0x00010001u);
                                     const at_s2 nd1 = pmax(G1, X1);
                                     const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
+#if A2_D16_SUB
+                                    (void)sel;
+                                    const at_s2 sM = as_s2(sw[k]);
+#else
                                     const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
+#endif
                                     // default scores: both substitution halves are >= 0 (drift), so M is one
                                     // 32-bit add too; other scores may subtract: per-half add
                                     const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;

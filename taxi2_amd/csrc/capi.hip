@@ -38,6 +38,7 @@ struct DevSet {
     int mode = 0;
     int64_t n = 0;
     int32_t max_len = 0;
+    bool high = false;  // holds a byte >= 0x80 (latin-1 text: NCD compresses its UTF-8 upper case)
     int64_t nbytes = 0;
     int64_t nwords = 0;
     uint8_t* bytes = nullptr;
@@ -873,7 +874,7 @@ struct Tracer {
     }
 };
 
-int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n);
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1);
 
 // Raw-mode NCD with C(x) computed once per set member (when the pairs outnumber the sequences).
 int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
@@ -904,7 +905,7 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
         hipLaunchKernelGGL(k_seq_streams, dim3((unsigned)((S.n + 255) / 256)), dim3(256), 0, ctx->stream, view(S), S.n,
                            d_sst);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_sst, S.n, singles[k], S.max_len)) return -1;
+        if (launch_zlen(ctx, d_sst, S.n, singles[k], S.max_len, S.high)) return -1;
     }
     for (int64_t c0 = 0; c0 < count; c0 += chunk) {
         const int64_t n = std::min(chunk, count - c0);
@@ -914,7 +915,7 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
         hipLaunchKernelGGL(k_ncd_concat_streams, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, view(X),
                            view(Y), d_idx, d_idx + chunk, n, both, d_cst);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_cst, m, d_c, X.max_len + Y.max_len)) return -1;
+        if (launch_zlen(ctx, d_cst, m, d_c, X.max_len + Y.max_len, X.high || Y.high)) return -1;
         hipLaunchKernelGGL(k_ncd_finish_cached, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, d_c, d_cx,
                            d_cy, d_idx, d_idx + chunk, n, both, d_v);
         HIP_TRY(ctx, hipGetLastError());
@@ -925,12 +926,13 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
 }
 
 // Compressed lengths of `n` device stream descriptors, every stream at most max_n bytes.  Streams
-// up to zlw::NMAX bytes: one wave per stream with its state in LDS (k_zlen_wave, zlen_wave.hpp);
-// longer ones (or TAXI2_ZLEN_SERIAL=1): one thread per stream with per-thread HBM scratch slabs
-// kept in the context (the head tables are zeroed once at allocation).
-int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n) {
+// up to zlw::NMAX bytes of ASCII: one wave per stream with its state in LDS (k_zlen_wave,
+// zlen_wave.hpp); longer ones, latin-1 text (each byte -> 1-2 UTF-8 bytes) or TAXI2_ZLEN_SERIAL=1:
+// one thread per stream with per-thread HBM scratch slabs kept in the context (the head tables
+// are zeroed once at allocation), any length (the window slides as zlib's does).
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1) {
     if (n <= 0) return 0;
-    if (max_n <= zlw::NMAX && !getenv("TAXI2_ZLEN_SERIAL")) {
+    if (max_n <= zlw::NMAX && !latin1 && !getenv("TAXI2_ZLEN_SERIAL")) {
         const int nmax = std::max(max_n, 4);
         const size_t lds = zlw::lds_bytes(nmax);
         if (lds > 64 * 1024)
@@ -960,7 +962,7 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
         ctx->z_threads = threads;
     }
     hipLaunchKernelGGL(k_zlen, dim3((unsigned)(threads / 64)), dim3(64), 0, ctx->stream, d_st, n,
-                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out);
+                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out, (int)latin1);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
 }
@@ -1049,6 +1051,18 @@ int taxi2_set_create(taxi2_ctx* ctx, const uint8_t* bytes, const int64_t* offset
     }
     for (int64_t i = 0; i <= n; ++i) offs0[i] = offsets[i] - offsets[0];
     if (nwords > INT32_MAX) return fail(ctx, "set too large");
+    {
+        const uint8_t* p = bytes + offsets[0];
+        uint64_t acc = 0;
+        int64_t k = 0;
+        for (; k + 8 <= s.nbytes; k += 8) {
+            uint64_t w;
+            memcpy(&w, p + k, 8);
+            acc |= w;
+        }
+        for (; k < s.nbytes; ++k) acc |= p[k];
+        s.high = (acc & 0x8080808080808080ull) != 0;
+    }
     s.max_len = maxlen;
     s.nwords = nwords;
     HIP_TRY(ctx, hipMalloc(&s.bytes, std::max<int64_t>(s.nbytes, 16)));
@@ -1393,13 +1407,6 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
     if (!out || !xs || !ys) return fail(ctx, "null argument");
     if (check_pair_indices(ctx, *X, *Y, xs, ys, count)) return -1;
     const bool aligned = sc != nullptr;
-    // the compressed streams (one sequence or aligned string, and a concatenation of two) must fit
-    // one 64 KiB deflate window (deflate_len.hpp): raw x + y, or two aligned strings of up to
-    // nA + nB bytes each
-    const int64_t longest = aligned ? 2 * ((int64_t)X->max_len + Y->max_len) : (int64_t)X->max_len + Y->max_len;
-    if (longest > zl::ZMAX_INPUT)
-        return fail(ctx, "NCD: compressed inputs up to %lld bytes exceed the %d-byte deflate window", (long long)longest,
-                    zl::ZMAX_INPUT);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int no = both ? 2 : 1;
     const int cap = X->max_len + Y->max_len;
@@ -1439,7 +1446,8 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
                            aligned ? tr.d_out + tr.chunk * 2 * tr.cap : nullptr, aligned ? tr.d_len : nullptr,
                            aligned ? tr.cap : 0, d_st);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_st, m * 3, d_c, aligned ? 2 * tr.cap : X->max_len + Y->max_len)) return -1;
+        if (launch_zlen(ctx, d_st, m * 3, d_c, aligned ? 2 * tr.cap : X->max_len + Y->max_len, X->high || Y->high))
+            return -1;
         hipLaunchKernelGGL(k_ncd_finish, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, d_c, m, d_v);
         HIP_TRY(ctx, hipGetLastError());
         HIP_TRY(ctx, hipMemcpyAsync(out + c0 * no, d_v, (size_t)m * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1460,8 +1468,6 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
         if (xs[k] < 0 || xs[k] >= X->n || (ys && (ys[k] < 0 || ys[k] >= Y->n)))
             return fail(ctx, "stream %lld index out of bounds", (long long)k);
     }
-    if ((int64_t)X->max_len + (ys ? Y->max_len : 0) > zl::ZMAX_INPUT)
-        return fail(ctx, "zlib lengths: inputs longer than %d bytes exceed the deflate window", zl::ZMAX_INPUT);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const int64_t chunk = (int64_t)1 << 18;
     if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)chunk * 2 * 8)) return -1;
@@ -1476,7 +1482,8 @@ int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, 
         hipLaunchKernelGGL(k_zlen_streams, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, view(*X),
                            view(*Y), di, ys ? di + chunk : nullptr, n, d_st);
         HIP_TRY(ctx, hipGetLastError());
-        if (launch_zlen(ctx, d_st, n, d_c, X->max_len + (ys ? Y->max_len : 0))) return -1;
+        if (launch_zlen(ctx, d_st, n, d_c, X->max_len + (ys ? Y->max_len : 0), X->high || (ys && Y->high)))
+            return -1;
         HIP_TRY(ctx, hipMemcpyAsync(out + c0, d_c, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }

@@ -15,10 +15,10 @@
 // the match's strstart++ for a match, before it for a literal), and a final block at the end; each
 // block is stored, fixed or dynamic by _tr_flush_block's byte comparison, and the bits of all
 // blocks are summed exactly (3-bit headers, stored blocks' byte alignment + LEN/NLEN, the final
-// bi_windup).  Inputs up to ZMAX_INPUT (65 273) bytes: the whole input sits in the 64 KiB window
-// and fill_window never slides it (a slide moves block_start below 0 and rebases the hash chains).
+// bi_windup).  Any length: the input streams through the 64 KiB window as fill_window moves it
+// (compressed_len below).
 // Pinned against Python's zlib.compress (zlib 1.2.11) by tests/test_ncd.py on random,
-// low-entropy and DNA-like inputs, single- and multi-block.
+// low-entropy and DNA-like inputs, single- and multi-block, one window and many.
 #pragma once
 #include <stdint.h>
 
@@ -44,12 +44,30 @@ constexpr int LITERALS = 256, END_BLOCK = 256, L_CODES = 286, D_CODES = 30, BL_C
 constexpr int HEAP_SIZE = 2 * L_CODES + 1, MAX_BITS = 15, MAX_BL_BITS = 7;
 constexpr int REP_3_6 = 16, REPZ_3_10 = 17, REPZ_11_138 = 18;
 constexpr int LIT_BUFSIZE = 1 << (8 + 6);  // memLevel 8
-constexpr int ZMAX_INPUT = WSIZE + MAX_DIST - 1;  // one window: fill_window never slides
-constexpr int WIN_BYTES = ZMAX_INPUT + MAX_MATCH + 2;
+constexpr int WIN_SIZE = 2 * WSIZE, WIN_INIT = MAX_MATCH;  // s->window_size, zlib's WIN_INIT
+constexpr int ZMAX_INPUT = WSIZE + MAX_DIST - 1;  // longest input the window holds without a slide
+constexpr int WIN_BYTES = WIN_SIZE;
+
+// Python's str.upper().encode() ("UTF-8") of one latin-1 character (one stored byte), as 1 or 2
+// bytes: returns the first, sets `second` to the other or -1.  Non-ASCII: 0xB5 -> U+039C,
+// 0xDF -> "SS", 0xFF -> U+0178, 0xE0..0xFE except 0xF7 -> minus 0x20, the rest unchanged, each
+// then UTF-8 encoded (checked against Python for all 256 by tests/test_ncd.py).
+__host__ __device__ __forceinline__ uint8_t upper_utf8(uint8_t c, int& second) {
+    if (c < 0x80) {
+        second = -1;
+        return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+    }
+    if (c == 0xB5) return second = 0x9C, 0xCE;
+    if (c == 0xDF) return second = 'S', 'S';
+    if (c == 0xFF) return second = 0xB8, 0xC5;
+    const int u = (c >= 0xE0 && c != 0xF7) ? c - 0x20 : c;
+    second = 0x80 | (u & 0x3F);
+    return (uint8_t)(0xC0 | (u >> 6));
+}
 
 // Per-stream scratch the caller provides.  head[] must be all zero on entry; it is left all zero.
 struct Scratch {
-    uint8_t* win;    // >= n + MAX_MATCH + 2 bytes
+    uint8_t* win;    // WIN_BYTES (64 KiB): zlib's window
     uint16_t* prev;  // WSIZE entries (indexed pos & WMASK, as zlib's)
     uint16_t* head;  // HASH_SIZE entries
 };
@@ -308,33 +326,98 @@ __host__ __device__ inline int longest_match(const uint8_t* win, const uint16_t*
     return best_len <= lookahead ? best_len : lookahead;
 }
 
-// len(zlib.compress(upper(a[0:na]) + upper(b[0:nb]))) with level 6; -1 if na + nb > ZMAX_INPUT.
-// `upper` maps a..z to A..Z (Python str.upper on the ASCII letters the sequences hold).
+// len(zlib.compress(upper(a[0:na]) + upper(b[0:nb]))) with level 6, for any length.
+// `upper` maps a..z to A..Z (Python str.upper on the ASCII letters the sequences hold); with
+// `latin1` every byte is a latin-1 character and becomes upper_utf8's bytes, i.e. the input is
+// Python's (a + b).upper().encode() -- what alfpy compresses for non-ASCII text.
+//
+// The input streams through zlib's 64 KiB window exactly as fill_window moves it: it is read in
+// as room allows, and whenever fill_window runs (lookahead < MIN_LOOKAHEAD at the top of
+// deflate_slow's loop) with strstart >= WSIZE + MAX_DIST -- with or without input left -- the
+// upper half moves down (the bytes past the data stay as they were: zlib zeroes WIN_INIT bytes
+// past the data only up to its high-water mark, which never comes down), strstart / match_start /
+// block_start drop by WSIZE and slide_hash rebases head[] and prev[] (positions below WSIZE
+// become NIL = 0).  Python's zlib.compress runs deflate(Z_NO_FLUSH) over the whole input and
+// then deflate(Z_FINISH) with none: the extra fill_window at that boundary is idempotent, so one
+// pass with every byte available is the same parse.
 __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const uint8_t* b, int nb, Scratch& z,
-                                              Trees& t) {
-    const int n = na + nb;
-    if (n > ZMAX_INPUT) return -1;
+                                              Trees& t, bool latin1 = false) {
+    const int64_t n = (int64_t)na + nb;
     uint8_t* win = z.win;
-    for (int i = 0; i < na; i++) {
-        const uint8_t c = a[i];
-        win[i] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
-    }
-    for (int i = 0; i < nb; i++) {
-        const uint8_t c = b[i];
-        win[na + i] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
-    }
-    for (int i = 0; i < MAX_MATCH + 2; i++) win[n + i] = 0;  // fill_window's WIN_INIT zeroing
+    int64_t rd = 0;          // source bytes consumed
+    int pend = -1;           // second byte of a two-byte character not yet in the window
+    int high_water = 0;      // zlib's s->high_water
+    bool slid = false;
 
     init_block(t);
     int64_t bits = 0;        // deflate stream bits so far (after the 2-byte zlib header)
-    int block_start = 0;     // first input byte of the open block
+    int block_start = 0;     // first input byte of the open block (window position; < 0 after a slide)
     int last_lit = 0;        // symbols buffered in the open block (_tr_tally's s->last_lit)
 
     uint32_t ins_h = 0;
-    if (n >= MIN_MATCH) ins_h = (((uint32_t)win[0] << HASH_SHIFT) ^ win[1]) & HASH_MASK;
-    int strstart = 0, lookahead = n;
+    int strstart = 0, lookahead = 0;
     int match_length = MIN_MATCH - 1, prev_length, match_start = 0, prev_match;
     bool match_available = false;
+
+    auto fill_window = [&]() {
+        do {
+            int more = WIN_SIZE - lookahead - strstart;
+            if (strstart >= WSIZE + MAX_DIST) {
+                for (int i = 0; i < WSIZE - more; i++) win[i] = win[i + WSIZE];
+                match_start -= WSIZE;
+                strstart -= WSIZE;
+                block_start -= WSIZE;
+                for (int i = 0; i < HASH_SIZE; i++) {
+                    const int m = z.head[i];
+                    z.head[i] = (uint16_t)(m >= WSIZE ? m - WSIZE : 0);
+                }
+                for (int i = 0; i < WSIZE; i++) {
+                    const int m = z.prev[i];
+                    z.prev[i] = (uint16_t)(m >= WSIZE ? m - WSIZE : 0);
+                }
+                slid = true;
+                more += WSIZE;
+            }
+            if (rd == n && pend < 0) break;  // strm->avail_in == 0
+            uint8_t* dst = win + strstart + lookahead;
+            int k = 0;
+            if (!latin1) {
+                k = (int)(n - rd < more ? n - rd : more);
+                for (int i = 0; i < k; i++, rd++) {
+                    const uint8_t c = rd < na ? a[rd] : b[rd - na];
+                    dst[i] = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+                }
+            } else {
+                while (k < more) {
+                    if (pend >= 0) {
+                        dst[k++] = (uint8_t)pend;
+                        pend = -1;
+                        continue;
+                    }
+                    if (rd == n) break;
+                    const uint8_t c = rd < na ? a[rd] : b[rd - na];
+                    rd++;
+                    dst[k++] = upper_utf8(c, pend);
+                }
+            }
+            lookahead += k;
+            if (lookahead >= MIN_MATCH)  // s->insert is 0 during the parse
+                ins_h = (((uint32_t)win[strstart] << HASH_SHIFT) ^ win[strstart + 1]) & HASH_MASK;
+        } while (lookahead < MIN_LOOKAHEAD && (rd != n || pend >= 0));
+        if (high_water < WIN_SIZE) {  // WIN_INIT zeroing past the data
+            const int curr = strstart + lookahead;
+            if (high_water < curr) {
+                const int init = WIN_SIZE - curr < WIN_INIT ? WIN_SIZE - curr : WIN_INIT;
+                for (int i = 0; i < init; i++) win[curr + i] = 0;
+                high_water = curr + init;
+            } else if (high_water < curr + WIN_INIT) {
+                int init = curr + WIN_INIT - high_water;
+                if (init > WIN_SIZE - high_water) init = WIN_SIZE - high_water;
+                for (int i = 0; i < init; i++) win[high_water + i] = 0;
+                high_water += init;
+            }
+        }
+    };
     auto insert = [&](int str) -> int {
         ins_h = ((ins_h << HASH_SHIFT) ^ win[str + (MIN_MATCH - 1)]) & HASH_MASK;
         const int head = z.head[ins_h];
@@ -359,7 +442,11 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
         last_lit = 0;
     };
 
-    while (lookahead != 0) {
+    for (;;) {
+        if (lookahead < MIN_LOOKAHEAD) {
+            fill_window();
+            if (lookahead == 0) break;
+        }
         int hash_head = 0;
         if (lookahead >= MIN_MATCH) hash_head = insert(strstart);
         prev_length = match_length;
@@ -396,9 +483,11 @@ __host__ __device__ inline int compressed_len(const uint8_t* a, int na, const ui
     flush(true);
 
     // leave head[] all zero for the next stream
-    if (n >= MIN_MATCH) {
+    if (slid) {
+        for (int i = 0; i < HASH_SIZE; i++) z.head[i] = 0;
+    } else if (strstart >= MIN_MATCH) {  // never slid: the window holds all strstart input bytes
         uint32_t h = (((uint32_t)win[0] << HASH_SHIFT) ^ win[1]) & HASH_MASK;
-        for (int p = 0; p + MIN_MATCH - 1 < n; p++) {
+        for (int p = 0; p + MIN_MATCH - 1 < strstart; p++) {
             h = ((h << HASH_SHIFT) ^ win[p + 2]) & HASH_MASK;
             z.head[h] = 0;
         }

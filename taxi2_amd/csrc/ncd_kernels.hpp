@@ -6,7 +6,8 @@
 //
 // One thread per compressed stream: the lazy-match parse is a serial chain walk per byte, so the
 // work unit is the stream, not the byte.  Each thread owns a zeroed 64 KiB hash-head table and a
-// window / prev / tree scratch slab in HBM (the head table is cleaned per stream, never re-zeroed).
+// window / prev / tree scratch slab in HBM (the head table is cleaned per stream, never re-zeroed);
+// the 64 KiB window slides as zlib's does, so streams have no length limit.
 #pragma once
 #include "common.hpp"
 #include "deflate_len.hpp"
@@ -29,7 +30,7 @@ constexpr size_t ZS_HEAD = (size_t)zl::HASH_SIZE * 2;
 
 __global__ void __launch_bounds__(64, 4)
 k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, uint8_t* __restrict__ slabs,
-       int32_t* __restrict__ out) {
+       int32_t* __restrict__ out, int latin1) {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     uint8_t* slab = slabs + tid * ZS_SLAB;
@@ -37,7 +38,7 @@ k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, 
     zl::Trees* t = reinterpret_cast<zl::Trees*>(slab + ZS_WIN + ZS_PREV);
     for (int64_t s = tid; s < n; s += nthreads) {
         const ZStream d = st[s];
-        out[s] = zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t);
+        out[s] = zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t, latin1 != 0);
     }
 }
 

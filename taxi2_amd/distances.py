@@ -132,11 +132,14 @@ def engine_metric(metric: DistanceMetric) -> bool:
 
 
 def check_ncd_strings(strings) -> None:
-    """The engine compresses the stored bytes; the reference compresses ``str.upper().encode()``
-    (UTF-8).  Both agree on ASCII, so non-ASCII input is refused instead of silently differing."""
+    """The reference compresses ``str.upper().encode()`` (UTF-8).  The engine stores one latin-1
+    byte per character and compresses its UTF-8 upper case (``deflate_len.hpp upper_utf8``: "é" ->
+    "É" as two bytes, "ß" -> "SS", "ÿ" -> "Ÿ"), which is the same for every character up to
+    U+00FF; a character past latin-1 has no stored byte, so it is refused instead of silently
+    differing."""
     for s in strings:
-        if not s.isascii():
-            raise ValueError("NCD on the MI355X engine needs ASCII sequences")
+        if not s.isascii() and any(ord(c) > 0xFF for c in s):
+            raise ValueError("NCD on the MI355X engine needs latin-1 sequences (characters up to U+00FF)")
 
 
 def calculate_many(metrics: Iterable[DistanceMetric], xs: list[str], ys: list[str], *, engine=None) -> np.ndarray:

@@ -242,3 +242,52 @@ def test_zlib_lengths_wave_path_edges(engine):
     finally:
         os.environ.pop("TAXI2_ZLEN_SERIAL")
     st.free()
+
+
+def test_zlib_lengths_sliding_window(engine):
+    """Streams past one 64 KiB window (65 273 bytes): the one-thread parse slides the window as
+    zlib's fill_window does; single streams and concatenations up to 300 kB vs Python's zlib."""
+    rng = random.Random(31)
+    dna = "".join(rng.choice("ACGT") for _ in range(300000))
+    rep = (dna[:173] * 1800)[:300000]
+    seqs = [dna[:65274], dna[:65537], dna[:98305], dna[:131073], dna, rep[:200000], rep[:70001],
+            mutate([rep[:150000]], 3, rate=0.02)[0], "ACGT" * 10]
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    got1 = engine.zlib_lengths(st, np.arange(n))
+    assert got1.tolist() == [len(zlib.compress(s.upper().encode())) for s in seqs]
+    xs, ys = np.array([0, 1, 6, 8, 5]), np.array([6, 8, 2, 3, 7])
+    got2 = engine.zlib_lengths(st, xs, st, ys)
+    assert got2.tolist() == [len(zlib.compress((seqs[a] + seqs[b]).upper().encode())) for a, b in zip(xs, ys)]
+    st.free()
+
+
+def test_ncd_latin1_sequences(engine):
+    """Non-ASCII (latin-1) sequences: alfpy compresses str.upper().encode() -- two UTF-8 bytes per
+    accented letter, "ß" -> "SS" -- raw pairs (cached and per-pair paths) and aligned pairs."""
+    from oracle import restatement as R
+
+    rng = random.Random(37)
+    alpha = "ACGTNacgtéÉßµÿñ-"
+    seqs = ["".join(rng.choice(alpha) for _ in range(rng.randrange(0, 400))) for _ in range(14)] + ["ß", "ÿ" * 40]
+    st = engine.upload(seqs, align=False)
+    n = len(seqs)
+    assert engine.zlib_lengths(st, np.arange(n)).tolist() == [len(zlib.compress(s.upper().encode())) for s in seqs]
+    xs = np.repeat(np.arange(n), n)
+    ys = np.tile(np.arange(n), n)
+    got = engine.ncd_pairs(st, st, xs, ys, aligned=False, both=True)  # pairs >> sequences: cached C(x)
+    few = engine.ncd_pairs(st, st, xs[:5], ys[:5], aligned=False, both=True)  # per-pair streams
+    for k, (a, b) in enumerate(zip(xs, ys)):
+        assert got[k, 0] == R.ncd(seqs[a], seqs[b]) and got[k, 1] == R.ncd(seqs[b], seqs[a]), (a, b)
+    assert np.array_equal(few, got[:5])
+    st.free()
+    al = [s.replace("-", "") for s in seqs[:8]]
+    st = engine.upload(al, align=True)
+    xs = np.repeat(np.arange(8), 8)
+    ys = np.tile(np.arange(8), 8)
+    got = engine.ncd_pairs(st, st, xs, ys, DEFAULT, aligned=True, both=True)
+    for k, (a, b) in enumerate(zip(xs, ys)):
+        ax, ay, _ = R.align(al[a], al[b])
+        by, bx, _ = R.align(al[b], al[a])
+        assert got[k, 0] == R.ncd(ax, ay) and got[k, 1] == R.ncd(by, bx), (a, b)
+    st.free()

@@ -137,7 +137,7 @@ TASK = textwrap.dedent(
                 seqs[k] = Sequence("same", seqs[k].seq, seqs[k].extras)
             seqs[6] = Sequence("s5", seqs[6].seq, seqs[6].extras)
             t.input.sequences = Sequences(seqs)
-            t.params.format.float = "{:.5g}"
+            t.params.format.float = "{{:.5g}}"
             t.input.genera = Partition({{s.id: "g%d" % (k % 2) for k, s in enumerate(seqs)}})
         elif variant == "reductions":  # config-5 shape: pre-aligned, no N x N text, reductions only
             t.params.pairs.align = False

@@ -28,9 +28,9 @@ def zlen_host(tmp_path_factory):
     subprocess.run([gxx, "-O2", "-std=c++17", "-shared", "-fPIC", *os.environ.get("TAXI2_HOST_CFLAGS", "").split(), "-o", str(out),
                     str(ROOT / "tests/native/zlen_host.cpp")], check=True)
     lib = ctypes.CDLL(str(out))
-    lib.zlen_host.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    lib.zlen_host.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
     lib.zlen_host.restype = ctypes.c_int
-    return lambda a, b=b"": lib.zlen_host(a, len(a), b, len(b))
+    return lambda a, b=b"", latin1=False: lib.zlen_host(a, len(a), b, len(b), int(latin1))
 
 
 def _inputs(seed: int, n: int):
@@ -88,7 +88,51 @@ def test_deflate_len_multi_block(zlen_host):
     assert not bad, bad[:10]
     a = bytes(random.Random(5).choice(b"ACGT-") for _ in range(21000))
     assert zlen_host(a[:10500], a[10500:]) == len(zlib.compress(a))  # a 21 kB aligned-string concatenation
-    assert zlen_host(b"A" * 65274) == -1  # past one window: refused, not approximated
+
+
+def _long_inputs():
+    """Past one window (65 273 bytes): fill_window slides the window by 32 KiB whenever strstart
+    reaches 65 274 at a refill, with or without input left -- lengths around the first and later
+    slides, inputs ending just after a slide, and ~0.5 MB streams (many slides, many blocks)."""
+    rng = random.Random(23)
+    dna = bytes(rng.choice(b"ACGT") for _ in range(500000))
+    rnd = bytes(rng.randrange(256) for _ in range(140000))
+    rep = (dna[:211] * 2400)[:500000]
+    mut = bytearray(rep)
+    for i in range(0, len(mut), 41):
+        mut[i] = rng.choice(b"ACGT-")
+    low = bytes(rng.choice(b"AAAAAAAC") for _ in range(300000))
+    for src in (dna, rnd, bytes(mut), low):
+        for L in (65274, 65275, 65400, 65535, 65536, 65537, 65800, 98041, 98042, 98304, 98305, 131072, 131073,
+                  140000, 300000, 500000):
+            if L <= len(src):
+                yield src[:L]
+
+
+def test_deflate_len_sliding_window(zlen_host):
+    bad = [len(x) for x in _long_inputs() if zlen_host(x) != len(zlib.compress(x.upper()))]
+    assert not bad, bad[:10]
+    a = bytes(random.Random(8).choice(b"ACGTacgt-") for _ in range(150000))
+    assert zlen_host(a[:70000], a[70000:]) == len(zlib.compress(a.upper()))  # a concatenation across slides
+
+
+def test_upper_utf8_table(zlen_host):
+    """Every latin-1 character alone: the engine's upper_utf8 bytes are Python's c.upper().encode()."""
+    for c in range(256):
+        s = bytes([c]) * 5
+        assert zlen_host(s, latin1=True) == len(zlib.compress(s.decode("latin-1").upper().encode())), c
+
+
+def test_deflate_len_latin1_text(zlen_host):
+    """Non-ASCII sequences: what alfpy compresses is str.upper().encode() (UTF-8, "ß" -> "SS"), one
+    or two bytes per stored latin-1 byte; short and long (sliding) streams, concatenations."""
+    rng = random.Random(29)
+    alpha = "ACGTNacgtn-éÉßµÿ×÷ñ°"
+    for L in (0, 1, 2, 7, 100, 3000, 40000, 70000, 130000):
+        s = "".join(rng.choice(alpha) for _ in range(L))
+        t = "".join(rng.choice(alpha) for _ in range(L // 3))
+        a, b = s.encode("latin-1"), t.encode("latin-1")
+        assert zlen_host(a, b, latin1=True) == len(zlib.compress((s + t).upper().encode())), L
 
 
 def test_oracle_ncd_formula():
@@ -106,5 +150,6 @@ def test_ncd_label_is_an_engine_metric():
 
     assert "ncd" in ENGINE_LABELS
     assert isinstance(DistanceMetric.fromLabel("ncd"), DistanceMetric.NCD)
+    check_ncd_strings(["ACGT", "ACGé", "ßÿµ"])  # latin-1: compressed as Python's UTF-8 upper case
     with pytest.raises(ValueError):
-        check_ncd_strings(["ACGT", "ACGé"])
+        check_ncd_strings(["ACGT", "ACGŁ"])
