@@ -435,9 +435,16 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
                            hops, nx, ba.band, ba.esc_list, ba.esc_n, str);
 }
 
+// A2_OCC: waves per SIMD the one- and two-fill-wave shapes are compiled for (the VGPR budget:
+// 6 -> 80, 5 -> 96, 4 -> 128 registers per lane)
+#ifndef A2_OCC
+#define A2_OCC 6
+#endif
 const VariantT kAlignT2[] = {
-    T2_VARIANTT2(4, 1, true, 6),  T2_VARIANTT2(8, 1, true, 6),  T2_VARIANTT2(6, 2, true, 6),  T2_VARIANTT2(8, 2, true, 6),
-    T2_VARIANTT2(4, 1, false, 6), T2_VARIANTT2(8, 1, false, 6), T2_VARIANTT2(6, 2, false, 6), T2_VARIANTT2(8, 2, false, 6),
+    T2_VARIANTT2(4, 1, true, A2_OCC),  T2_VARIANTT2(8, 1, true, A2_OCC),
+    T2_VARIANTT2(6, 2, true, A2_OCC),  T2_VARIANTT2(8, 2, true, A2_OCC),
+    T2_VARIANTT2(4, 1, false, A2_OCC), T2_VARIANTT2(8, 1, false, A2_OCC),
+    T2_VARIANTT2(6, 2, false, A2_OCC), T2_VARIANTT2(8, 2, false, A2_OCC),
     // 1 025 - 2 048 columns: four fill waves + the walker (5 waves per workgroup)
     T2_VARIANTT2(6, 4, true, 5), T2_VARIANTT2(8, 4, true, 5), T2_VARIANTT2(6, 4, false, 5), T2_VARIANTT2(8, 4, false, 5),
 };

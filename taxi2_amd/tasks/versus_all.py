@@ -425,7 +425,8 @@ class VersusAll:
             if partition:
                 st = self.subset_stats[name] = aggregate(A, ids, partition)
                 write_subset_statistics(self.paths.subsets / name, st, self.params.distances.metrics,
-                                        self.params.format.float, self.params.format.stats_template)
+                                        self.params.format.float, self.params.format.stats_template,
+                                        eng=self._engine())
 
     # ------------------------------------------------------------------ streamed driver
     def _streaming(self, seqs: list) -> bool:
@@ -783,7 +784,6 @@ class _BlockWriters:
         self.ids = [s.id for s in seqs]
         n = len(seqs)
         self.diag = None
-        self.files = []
         ex0 = list(seqs[0].extras.keys())
         self.pre = ["\t".join([s.id, *[v if v is not None else self.missing for v in s.extras.values()]])
                     for s in seqs]
@@ -1029,4 +1029,4 @@ class _BlockWriters:
         for name, agg in self.aggs:
             st = self.task.subset_stats[name] = agg.result()
             write_subset_statistics(self.task.paths.subsets / name, st, self.metrics, p.format.float,
-                                    p.format.stats_template)
+                                    p.format.stats_template, eng=self.eng)
