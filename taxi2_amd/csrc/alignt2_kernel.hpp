@@ -69,9 +69,12 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 }
 
 // 1: a step whose wave has no lane inside the trace band skips the trace-code arithmetic
-// (bit-identical; 0 builds the always-encode variant for A/B runs)
+// (bit-identical).  Default 0 since round 3: with the raw-difference trace the skip's extra live
+// registers push the 80-VGPR shape into spilling (240 B scratch per lane, reloads that wait on the
+// trace stores), and the always-encode build measured 3.92e6 vs 3.57e6 pairs/s on the same box
+// (profiles/r3/ab_*.json; 128 / 96-VGPR builds of either form were slower still)
 #ifndef A2_SKIP_OUT_OF_BAND
-#define A2_SKIP_OUT_OF_BAND 1
+#define A2_SKIP_OUT_OF_BAND 0
 #endif
 // 1: the per-column substitution words come from ds_read_u16_d16 / _d16_hi pairs (LDS assembles
 // the (stream 0, stream 1) halves) instead of two ds_read_b128 and a v_perm per column

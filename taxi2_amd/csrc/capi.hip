@@ -1759,33 +1759,46 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     }
     if (nrows == 0) return 0;
     // exact parallel summation (subset_kernels.hpp), rows in sub-blocks whose row partials fit
-    // ~256 MB of scratch (and the groups' LDS sort), in ascending order on one stream
+    // ~256 MB of scratch (and the groups' LDS sort), in ascending order on one stream; each row's
+    // subsets in chunks of SUB_CH columns (tmax bounds the chunks per row: sum of ceil(size / CH))
     const int64_t per_row = (int64_t)ns * m;
-    const int64_t rows_per = std::max<int64_t>(1, std::min<int64_t>(SUB_MAX_ROWS, ((int64_t)256 << 20) /
-                                                                    (per_row * (int64_t)(sizeof(SubPart) + sizeof(SubWork)))));
+    const int64_t tmax64 = (int64_t)ns + (ncols + SUB_CH - 1) / SUB_CH;
+    if (tmax64 > INT32_MAX / 2) return fail(ctx, "taxi2_subset_aggregate_dev: too many subsets");
+    const int tmax = (int)tmax64;
+    const int64_t row_bytes = per_row * (int64_t)(sizeof(SubPart) + sizeof(SubWork)) + tmax64 * m * (int64_t)sizeof(SubPart);
+    const int64_t rows_per = std::max<int64_t>(1, std::min<int64_t>(SUB_MAX_ROWS, ((int64_t)256 << 20) / row_bytes));
     const int64_t rsub = std::min(rows_per, nrows);
     auto al = [](size_t v) { return (v + 255) / 256 * 256; };
     const size_t o_part = 0, o_work = al((size_t)rsub * per_row * sizeof(SubPart));
-    const size_t o_rows = o_work + al((size_t)rsub * per_row * sizeof(SubWork));
+    const size_t o_cpart = o_work + al((size_t)rsub * per_row * sizeof(SubWork));
+    const size_t o_cofs = o_cpart + al((size_t)rsub * tmax * m * sizeof(SubPart));
+    const size_t o_rows = o_cofs + al((size_t)(ns + 1) * 4);
     const size_t o_code = o_rows + al((size_t)rsub * 4), o_start = o_code + al((size_t)rsub * 4);
     const size_t o_n = o_start + al((size_t)(rsub + 1) * 4), total = o_n + 256;
     if (ensure(ctx, &ctx->d_sub, &ctx->d_sub_bytes, total)) return -1;
     char* base = (char*)ctx->d_sub;
     SubPart* part = (SubPart*)(base + o_part);
     SubWork* work = (SubWork*)(base + o_work);
+    SubPart* cpart = (SubPart*)(base + o_cpart);
+    int32_t* cofs = (int32_t*)(base + o_cofs);
     int32_t* grows = (int32_t*)(base + o_rows);
     int32_t* gcode = (int32_t*)(base + o_code);
     int32_t* gstart = (int32_t*)(base + o_start);
     int32_t* ngrp = (int32_t*)(base + o_n);
     unsigned int* wcount = (unsigned int*)(base + o_n + 64);
+    hipLaunchKernelGGL(k_subset_cofs, dim3(1), dim3(1024), 0, st, d_col_start, (int)ns, cofs);
+    HIP_TRY(ctx, hipGetLastError());
     for (int64_t r0 = 0; r0 < nrows; r0 += rsub) {
         const int64_t nr = std::min(rsub, nrows - r0);
         const double* v = d_vals + r0 * ncols * m;
         const int32_t* rc = d_row_code + r0;
         hipLaunchKernelGGL(k_subset_groups, dim3(1), dim3(1024), 0, st, rc, (int)nr, grows, gcode, gstart, ngrp);
         HIP_TRY(ctx, hipGetLastError());
-        hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * ns + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m, rc,
-                           d_col_start, d_col_idx, (int)ns, (const double*)d_sum, part);
+        hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * tmax + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m, rc,
+                           d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum, cpart);
+        HIP_TRY(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_subset_rowmerge, dim3((unsigned)((nr * per_row + 255) / 256)), dim3(256), 0, st, nr,
+                           (int)ns, m, (const int32_t*)cofs, tmax, (const SubPart*)cpart, part);
         HIP_TRY(ctx, hipGetLastError());
         HIP_TRY(ctx, hipMemsetAsync(wcount, 0, 4, st));
         hipLaunchKernelGGL(k_subset_combine, dim3((unsigned)((nr * per_row + 255) / 256)), dim3(256), 0, st, nr,
@@ -1794,7 +1807,7 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
         HIP_TRY(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_subset_fixup, dim3((unsigned)(ctx->num_cus * 8)), dim3(256), 0, st, v, ncols, m, (int)ns,
                            d_col_start, d_col_idx, (const int32_t*)gstart, (const int32_t*)grows,
-                           (const SubWork*)work, (const unsigned int*)wcount, d_sum);
+                           (const SubPart*)part, (const SubWork*)work, (const unsigned int*)wcount, d_sum);
         HIP_TRY(ctx, hipGetLastError());
     }
     return 0;

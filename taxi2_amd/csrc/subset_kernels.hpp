@@ -12,18 +12,27 @@
 // s).  So over a run of values with no tie, no negative value and no binade change, the
 // sequential result is s + (sum of the R) u, and the R are exact integers (< 2^53) whose sum is
 // the same in any order.  Per block of rows:
-//   k_subset_rows     one wave per (row x, column subset b): for each metric, R of every value of
-//                     the row's key (u from the key's sum at block start), the row's integer sum,
-//                     count, first minimum, maximum, and flags (tie / negative / no grid: s = 0)
+//   k_subset_cofs     chunk offsets: subset b's columns in chunks of SUB_CH (a 2-genus partition at
+//                     N = 200 000 is 98 chunks per row instead of 2 waves per row)
+//   k_subset_rows     one wave per (row x, chunk of column subset b): for each metric, R of every value of
+//                     the row's key at SUB_J grids -- u, 2u, 4u, 8u with u from the key's sum at
+//                     block start (binades e0 .. e0 + 3) -- the row's integer sums, count, first
+//                     minimum, maximum, and flags (tie at each grid / negative / no grid: s = 0)
+//   k_subset_rowmerge one thread per (row x, b, metric): the row's chunk partials in column order
+//                     (integer sums are exact in any order; the first minimum stays the first)
 //   k_subset_combine  one thread per (row group a, b, metric): walks the block's rows of subset a
 //                     in ascending x, adds the integer sums while S + sum <= 2^53 - 1 (the binade
 //                     holds) and nothing is flagged, merges count / min / max (in row order, so the
 //                     first minimum and the sign of a zero minimum are the sequential ones); at the
 //                     first row it cannot take, it queues the key with that row
-//   k_subset_fixup    one wave per queued key: the remaining rows in order, 64 values at a time --
-//                     the same integer step when the chunk qualifies, else 64 sequential f64 adds
-// Binade changes are rare (the sum of non-negative values doubles ~log2(N^2) times per key), so
-// the fixup runs on a key's first block and then on a few blocks only.  None (non-finite)
+//   k_subset_fixup    one wave per queued key: that row in order, 64 values at a time (the integer
+//                     step when the chunk qualifies, else 64 sequential f64 adds); each later row
+//                     from its partial at the binade the sum has reached (e0 .. e0 + 3) when that
+//                     partial qualifies, else again 64 values at a time
+// Binade changes are rare (the sum of non-negative values doubles ~log2(N^2) times per key), and
+// each costs one row walked value by value: the fixup's work no longer grows with the rows left in
+// the block after the change (round 3: a 2-genus partition at N = 50 000 spent 84 % of its kernel
+// time re-walking those rows).  None (non-finite)
 // values are skipped as SimpleAggregator.add does (in the sums they add +0.0, an exact no-op:
 // the running sum starts at +0.0 and never becomes -0.0).
 #pragma once
@@ -31,20 +40,26 @@
 
 namespace taxi2 {
 
-struct SubPart {    // one (block row, column subset b, metric k)
-    double rsum;    // sum of R over the row's values of the key (exact while < 2^53)
-    double mn, mx;  // first minimum (from +inf), maximum (from 0.0)
-    long long cnt;  // defined values
-    uint32_t flags; // SP_*: the integer step does not reproduce the sequential sum
+constexpr int SUB_J = 4;  // grids per row partial: binades e0 .. e0 + SUB_J - 1
+constexpr int SUB_NOE = -32768;  // no grid at block start (the key's sum was 0)
+struct SubPart {            // one (block row, column subset b, metric k)
+    double rsum[SUB_J];     // sum of R = rint(v / (2^j u)) over the row's values of the key (exact)
+    double mn, mx;          // first minimum (from +inf), maximum (from 0.0)
+    long long cnt;          // defined values
+    uint32_t flags;         // SP_*: where the integer step does not reproduce the sequential sum
     int32_t pad;
 };
+// SP_TIE << j: some value lies exactly halfway between two multiples of 2^j u
 enum : uint32_t { SP_NOGRID = 1, SP_NEG = 2, SP_TIE = 4 };
 struct SubWork {  // a key the combine could not finish: its rows from grp_rows[r0] on
     int64_t key;
     int32_t g, r0;
+    int32_t e0;   // binade of the key's sum at block start (the partials' grid), SUB_NOE: none
+    int32_t pad;
 };
 constexpr double SUB_TOP = 9007199254740991.0;  // 2^53 - 1: largest integer multiple of u below 2^E
 constexpr int SUB_MAX_ROWS = 8192;              // rows per k_subset_groups call (LDS sort)
+constexpr int SUB_CH = 2048;                    // columns per k_subset_rows wave (a subset's chunk)
 
 // The grid of running sum s: true with s in [2^(e-1), 2^e) when s is a positive normal number.
 __device__ __forceinline__ bool sub_grid(double s, int& e) {
@@ -126,25 +141,67 @@ __global__ void __launch_bounds__(1024) k_subset_groups(const int32_t* __restric
     }
 }
 
-// One wave per (block row x, column subset b), every metric.
+// cofs[b] = chunks of the subsets before b (subset b: max(1, ceil(size / SUB_CH)) chunks), cofs[ns]
+// = chunks per row.  One workgroup of 1024 threads: per-thread runs of subsets, then a scan.
+__global__ void __launch_bounds__(1024) k_subset_cofs(const int64_t* __restrict__ col_start, int ns,
+                                                      int32_t* __restrict__ cofs) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int per = (ns + 1023) / 1024;
+    const int b0 = min(ns, t * per), b1 = min(ns, b0 + per);
+    auto nch = [&](int b) {
+        const int64_t sz = col_start[b + 1] - col_start[b];
+        return sz <= SUB_CH ? 1 : (int)((sz + SUB_CH - 1) / SUB_CH);
+    };
+    int cnt = 0;
+    for (int b = b0; b < b1; ++b) cnt += nch(b);
+    part[t] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - cnt;
+    for (int b = b0; b < b1; ++b) {
+        cofs[b] = run;
+        run += nch(b);
+    }
+    if (t == 1023) cofs[ns] = part[1023];
+}
+
+// One wave per (block row x, chunk t of the row's chunks; tmax >= cofs[ns] bounds the grid), every
+// metric.  Chunk t belongs to subset b with cofs[b] <= t < cofs[b + 1].
 __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ vals, int64_t nrows, int64_t ncols,
                                                      int m, const int32_t* __restrict__ row_code,
                                                      const int64_t* __restrict__ col_start,
                                                      const int32_t* __restrict__ col_idx, int ns,
+                                                     const int32_t* __restrict__ cofs, int tmax,
                                                      const double* __restrict__ sum, SubPart* __restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w >= nrows * ns) return;
-    const int64_t x = w / ns;
-    const int b = (int)(w - x * ns);
+    if (w >= nrows * tmax) return;
+    const int64_t x = w / tmax;
+    const int t = (int)(w - x * tmax);
+    if (t >= cofs[ns]) return;
+    int lo = 0, hi = ns;  // the last b with cofs[b] <= t
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (cofs[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    const int b = lo;
     const int a = row_code[x];
-    const int64_t j0 = col_start[b], j1 = col_start[b + 1];
+    const int64_t j0 = col_start[b] + (int64_t)(t - cofs[b]) * SUB_CH;
+    const int64_t j1 = min(col_start[b + 1], j0 + SUB_CH);
     const double* row = vals + x * ncols * m;
     for (int k = 0; k < m; ++k) {
         int e;
         const bool grid = sub_grid(sum[((int64_t)a * ns + b) * m + k], e);
         const int sc = 53 - e;
-        double rs = 0.0, mn = __builtin_inf(), mx = 0.0;
+        double rs[SUB_J], mn = __builtin_inf(), mx = 0.0;
+        for (int q = 0; q < SUB_J; ++q) rs[q] = 0.0;
         long long c = 0, mnp = 0x7FFFFFFFFFFFFFFFll;
         uint32_t fl = grid ? 0u : SP_NOGRID;
         for (int64_t j = j0 + lane; j < j1; j += 64) {
@@ -158,14 +215,18 @@ __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ 
             if (v > mx) mx = v;
             if (grid) {
                 if (v < 0.0) fl |= SP_NEG;
-                const double r = ldexp(v, sc);
-                const double R = rint(r);
-                if (fabs(r - R) == 0.5) fl |= SP_TIE;
-                rs += R;
+#pragma unroll
+                for (int q = 0; q < SUB_J; ++q) {
+                    const double r = ldexp(v, sc - q);
+                    const double R = rint(r);
+                    if (fabs(r - R) == 0.5) fl |= (uint32_t)SP_TIE << q;
+                    rs[q] += R;
+                }
             }
         }
         for (int o = 32; o > 0; o >>= 1) {
-            rs += __shfl_xor(rs, o);
+#pragma unroll
+            for (int q = 0; q < SUB_J; ++q) rs[q] += __shfl_xor(rs[q], o);
             c += __shfl_xor(c, o);
             fl |= (uint32_t)__shfl_xor((int)fl, o);
             const double omx = __shfl_xor(mx, o);
@@ -177,8 +238,39 @@ __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ 
                 mnp = omp;
             }
         }
-        if (lane == 0) part[(x * ns + b) * m + k] = SubPart{rs, mn, mx, c, fl, 0};
+        if (lane == 0) {
+            SubPart P;
+            for (int q = 0; q < SUB_J; ++q) P.rsum[q] = rs[q];
+            P.mn = mn;
+            P.mx = mx;
+            P.cnt = c;
+            P.flags = fl;
+            P.pad = 0;
+            part[(x * tmax + t) * m + k] = P;
+        }
     }
+}
+
+// One thread per (block row x, subset b, metric k): the row's chunk partials merged in column order.
+__global__ void __launch_bounds__(256) k_subset_rowmerge(int64_t nrows, int ns, int m, const int32_t* __restrict__ cofs,
+                                                         int tmax, const SubPart* __restrict__ cpart,
+                                                         SubPart* __restrict__ part) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= nrows * ns * m) return;
+    const int k = (int)(i % m);
+    const int64_t xb = i / m;
+    const int b = (int)(xb % ns);
+    const int64_t x = xb / ns;
+    SubPart R = cpart[(x * tmax + cofs[b]) * m + k];
+    for (int t = cofs[b] + 1; t < cofs[b + 1]; ++t) {
+        const SubPart& P = cpart[(x * tmax + t) * m + k];
+        for (int q = 0; q < SUB_J; ++q) R.rsum[q] += P.rsum[q];  // integers: exact in any order
+        if (P.mn < R.mn) R.mn = P.mn;                            // strict: the earlier chunk's on ties
+        if (P.mx > R.mx) R.mx = P.mx;
+        R.cnt += P.cnt;
+        R.flags |= P.flags;
+    }
+    part[i] = R;
 }
 
 // One thread per (row group g, column subset b, metric k).
@@ -209,7 +301,7 @@ __global__ void __launch_bounds__(256) k_subset_combine(int64_t maxg, int ns, in
         if (P.mn < lo) lo = P.mn;
         if (P.mx > hi) hi = P.mx;
         if (resume < 0) {
-            if (grid && P.flags == 0u && S + P.rsum <= SUB_TOP) S += P.rsum;
+            if (grid && (P.flags & (SP_NOGRID | SP_NEG | SP_TIE)) == 0u && S + P.rsum[0] <= SUB_TOP) S += P.rsum[0];
             else resume = r;
         }
     }
@@ -218,15 +310,17 @@ __global__ void __launch_bounds__(256) k_subset_combine(int64_t maxg, int ns, in
     mn[key] = lo;
     mx[key] = hi;
     count[key] = c;
-    if (resume >= 0) work[atomicAdd(wcount, 1u)] = SubWork{key, g, resume};
+    if (resume >= 0) work[atomicAdd(wcount, 1u)] = SubWork{key, g, resume, grid ? e : SUB_NOE, 0};
 }
 
-// Persistent waves over the queued keys: the key's remaining rows of the block in order.
+// Persistent waves over the queued keys: row r0 of the key value by value (64 at a time), then each
+// later row from its partial at the grid of the binade the sum has reached, or value by value.
 __global__ void __launch_bounds__(256) k_subset_fixup(const double* __restrict__ vals, int64_t ncols, int m, int ns,
                                                       const int64_t* __restrict__ col_start,
                                                       const int32_t* __restrict__ col_idx,
                                                       const int32_t* __restrict__ grp_start,
                                                       const int32_t* __restrict__ grp_rows,
+                                                      const SubPart* __restrict__ part,
                                                       const SubWork* __restrict__ work,
                                                       const unsigned int* __restrict__ wcount,
                                                       double* __restrict__ sum) {
@@ -240,12 +334,22 @@ __global__ void __launch_bounds__(256) k_subset_fixup(const double* __restrict__
         const int64_t j0 = col_start[b], j1 = col_start[b + 1];
         double s = sum[it.key];
         for (int r = it.r0; r < grp_start[it.g + 1]; ++r) {
-            const double* row = vals + (int64_t)grp_rows[r] * ncols * m;
+            const int64_t x = grp_rows[r];
+            int e;
+            if (r > it.r0 && it.e0 != SUB_NOE && sub_grid(s, e) && e >= it.e0 && e < it.e0 + SUB_J) {
+                const SubPart& P = part[(x * ns + b) * m + k];
+                const int jq = e - it.e0;
+                const double S = ldexp(s, 53 - e);
+                if ((P.flags & (SP_NOGRID | SP_NEG | ((uint32_t)SP_TIE << jq))) == 0u && S + P.rsum[jq] <= SUB_TOP) {
+                    s = ldexp(S + P.rsum[jq], e - 53);  // the whole row in the binade: exact
+                    continue;
+                }
+            }
+            const double* row = vals + x * ncols * m;
             for (int64_t c0 = j0; c0 < j1; c0 += 64) {
                 const int64_t j = c0 + lane;
                 double v = j < j1 ? row[(int64_t)col_idx[j] * m + k] : 0.0;
                 if (!isfinite(v)) v = 0.0;  // None: skipped (+0.0 adds nothing)
-                int e;
                 if (sub_grid(s, e)) {  // the integer step, when the whole chunk qualifies
                     const double rr = ldexp(v, 53 - e);
                     const double R = rint(rr);

@@ -263,13 +263,24 @@ class SubsetAggregatorDev:
         self.torch = torch
 
     def add(self, D, x0: int, x1: int) -> None:
-        """D: (x1 - x0, n, m) float64 device tensor of the rows' adjusted values (NaN = None)."""
+        """D: (x1 - x0, n, m) float64 device tensor of the rows' adjusted values (NaN = None),
+        ordered after the work already queued on torch's current stream."""
+        torch = self.torch
         D = D.contiguous()
-        st = self.torch.cuda.current_stream(D.device).cuda_stream
+        cur = torch.cuda.current_stream(D.device)
+        side = None
+        if cur.cuda_stream == 0:
+            # the legacy default stream's handle is 0, which the engine reads as "its own stream":
+            # run on a side stream ordered after `cur`, and order `cur` after it
+            side = torch.cuda.Stream(D.device)
+            side.wait_stream(cur)
+        st = (side or cur).cuda_stream
         self.eng.subset_aggregate_dev(D.data_ptr(), x1 - x0, self.n, self.m, self.row_code[x0:x1].data_ptr(),
                                       self.col_start.data_ptr(), self.col_idx.data_ptr(), self.ns, False,
                                       self.sum.data_ptr(), self.min.data_ptr(), self.max.data_ptr(),
                                       self.count.data_ptr(), st)
+        if side is not None:
+            cur.wait_stream(side)
 
     def state(self) -> tuple:
         """The running state tensors (sum, min, max, count), passed rank to rank by the sharded

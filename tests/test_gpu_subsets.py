@@ -123,3 +123,49 @@ def test_subset_aggregate_long_chain(engine):
         got = run_dev(engine, A, code, 1, block)
         for g, e in zip(got, exp):
             assert_bits(g, e)
+
+
+def seq_aggregate_np(A: np.ndarray, code: np.ndarray, ns: int):
+    """seq_aggregate for large n: per key the x-major value sequence, summed by np.add.accumulate
+    (strictly left to right, as the reference's loop; None -> +0.0, an exact no-op on a sum that
+    starts at +0.0), the first minimum (sign of a zero minimum from the first zero), max from 0.0."""
+    n, _, m = A.shape
+    s = np.zeros((ns, ns, m))
+    lo = np.full((ns, ns, m), np.inf)
+    hi = np.zeros((ns, ns, m))
+    c = np.zeros((ns, ns, m), dtype=np.int64)
+    for a in range(ns):
+        xs = np.flatnonzero(code == a)
+        for b in range(ns):
+            ys = np.flatnonzero(code == b)
+            for k in range(m):
+                v = A[np.ix_(xs, ys)][:, :, k].ravel()  # x-major
+                fin = np.isfinite(v)
+                c[a, b, k] = int(fin.sum())
+                if not c[a, b, k]:
+                    continue
+                s[a, b, k] = np.add.accumulate(np.where(fin, v, 0.0))[-1]
+                d = v[fin]
+                mn = d.min()
+                if mn == 0.0:
+                    mn = d[np.flatnonzero(d == 0.0)[0]]
+                lo[a, b, k] = mn
+                pos = d[d > 0.0]
+                hi[a, b, k] = pos.max() if pos.size else 0.0
+    return s, lo, hi, c
+
+
+@pytest.mark.parametrize("kind", ["percent", "dyadic", "uniform"])
+@pytest.mark.parametrize("ns,block", [(1, 700), (2, 1999), (3, 5000)])
+def test_subset_aggregate_wide_subsets(engine, kind, ns, block):
+    """Subsets wider than one k_subset_rows chunk (2 048 columns): chunk partials merged per row in
+    column order, multi-grid row partials across binade changes."""
+    rng = np.random.default_rng(hash(("wide", kind, ns, block)) % 2**32)
+    n, m = 5000, 2
+    A = values(rng, n, m, kind)
+    code = rng.integers(0, ns, n).astype(np.int32)
+    code[:ns] = np.arange(ns)
+    exp = seq_aggregate_np(A, code, ns)
+    got = run_dev(engine, A, code, ns, block)
+    for g, e in zip(got, exp):
+        assert_bits(g, e)

@@ -6,11 +6,11 @@ the four default metrics, aligned_pairs.txt, linear.tsv, matricial/*.tsv and sum
 metrics, incl. D2H of the N x N x 4 matrix), aligned-pairs text (GPU formatter + file write), and
 each writer.
 
---null points the output files at /dev/null (symlinks made before start()): the text is still
+By default the output files point at /dev/null (symlinks made before start()): the text is still
 produced and written through the file API, only the disk is taken out (aligned_pairs.txt alone is
 ~2.2 KB per ordered pair: 55 GB at N = 5 000).
 
-usage: python tools/bench_task.py --n 2000 5000 [--null] > profiles/r3/bench_task.json
+usage: python tools/bench_task.py [--n 5000 10000] [--files] > profiles/r3/bench_task.json
 """
 
 from __future__ import annotations
@@ -57,9 +57,11 @@ def run(n: int, eng, null: bool) -> dict:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, nargs="+", default=[2000])
-    ap.add_argument("--null", action="store_true")
+    ap.add_argument("--n", type=int, nargs="+", default=[5000, 10000])
+    ap.add_argument("--files", action="store_true",
+                    help="write real files (default: /dev/null symlinks; N = 10 000 is ~240 GB of text)")
     args = ap.parse_args()
+    args.null = not args.files
     import torch  # noqa: F401  -- torch's HIP runtime first (Engine shares it)
 
     from taxi2_amd._native import Engine

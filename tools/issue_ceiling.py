@@ -155,12 +155,16 @@ def split_skip(body: list[str], kernel: list[str], a: int):
             stub.append(l2)
         else:
             return None
-        b = next(k for k, x in enumerate(body) if x.startswith(back + ":"))
+        b = next((k for k, x in enumerate(body) if x.startswith(back + ":")), None)
+        if b is None:  # an scc branch out of the loop that is not the skip's stub
+            continue
         mj = next((re.match(r"^\s+s_cbranch_execnz\s+(\.LBB\w+)", x) for x in reversed(body[i:b])
                    if re.match(r"^\s+s_cbranch_execnz", x)), None)
         if mj is None:
             return None
-        j = next(k for k, x in enumerate(body) if x.startswith(mj.group(1) + ":"))
+        j = next((k for k, x in enumerate(body) if x.startswith(mj.group(1) + ":")), None)
+        if j is None:
+            return None
         return body[:i], body[i + 1:b], stub + body[b:j], body[j:]
     return None
 
