@@ -429,13 +429,14 @@ class Engine:
     def format_pairs_dev(self, q: SeqSet, r: SeqSet, q0: int, q1: int, cap: int, sx_ptr: int, sy_ptr: int,
                          slen_ptr: int, row_ids, col_ids, *, first: bool, stream: int | None = None) -> bytes:
         """aligned_pairs.txt text of the slots of rows [q0, q1) (taxi2_format_pairs_dev).  row_ids /
-        col_ids: (bytes, offsets) from pack_strings."""
+        col_ids: (bytes, offsets) from pack_strings.  Returns a memoryview of the engine's pinned
+        text buffer, valid until the next call (write it out or copy it before then)."""
         rb, ro = row_ids
         cb, co = col_ids
         need = _I64()
         buf = getattr(self, "_pairs_buf", None)
         if buf is None:
-            buf = np.empty(1 << 20, dtype=np.uint8)
+            buf = self._pinned(1 << 20)
         for _ in range(2):
             with self._lock:
                 rc = self._lib.taxi2_format_pairs_dev(
@@ -444,12 +445,25 @@ class Engine:
                     1 if first else 0, buf.ctypes.data, buf.size, ctypes.byref(need),
                     ctypes.c_void_p(stream) if stream else None)
             if rc == 1:
-                buf = np.empty(max(int(need.value), 2 * buf.size), dtype=np.uint8)
+                self._pairs_buf = None
+                buf = self._pinned(max(int(need.value), 2 * buf.size))
                 continue
             self._check(rc, "taxi2_format_pairs_dev")
             self._pairs_buf = buf
-            return buf[: need.value].tobytes()
+            return memoryview(buf[: need.value])
         raise NativeError("taxi2_format_pairs_dev: output buffer sizing failed")
+
+    def _pinned(self, nbytes: int) -> np.ndarray:
+        """A page-locked host buffer (the D2H of a block's text runs at full PCIe rate into it, no
+        staging copy), kept alive by the engine; plain memory when torch cannot pin."""
+        try:
+            import torch
+
+            t = torch.empty(int(nbytes), dtype=torch.uint8, pin_memory=True)
+            self._pinned_keep = t
+            return t.numpy()
+        except Exception:
+            return np.empty(int(nbytes), dtype=np.uint8)
 
     def list_pairs(self, x: SeqSet, y: SeqSet, xs, ys, metrics, scores=None, *, with_scores=False):
         """Explicit pairs.  ALIGN: (count, 2, M) [(x,y), (y,x)]; else (count, M)."""

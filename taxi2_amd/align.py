@@ -52,6 +52,43 @@ class PairwiseAligner(Type):
     def align_pairs(self, pairs: Iterable[SequencePair]) -> SequencePairs:
         return SequencePairs(self._align_stream(pairs))
 
+    def align_product_rows(self, xs: list[Sequence], ys: list[Sequence], rows: range | None = None,
+                           max_pairs: int = 1 << 16, sets: tuple | None = None) -> Iterator[list[SequencePair]]:
+        """Row x of the x-major product xs x ys (``rows``: a range of x, default all), as the aligned
+        pairs (x, y) for every y -- what ``align_many([SequencePair(x, y) for y in ys])`` gives per
+        row, with both sides uploaded ONCE (not once per row; ``sets`` = (xs, ys) already uploaded
+        by the caller with ``upload_sets``, kept) and up to ``max_pairs`` pairs per engine call."""
+        rows = range(len(xs)) if rows is None else rows
+        if not len(rows):
+            return
+        eng = self.engine
+        own = sets is None
+        sx, sy = self.upload_sets(xs, ys) if own else sets
+        same = sx is sy
+        sc = Scores(**self.scores).as_tuple()
+        ny = len(ys)
+        per = max(1, max_pairs // max(1, ny))
+        try:
+            for r0 in range(rows.start, rows.stop, per):
+                r1 = min(rows.stop, r0 + per)
+                xi = np.repeat(np.arange(r0, r1), ny)
+                yi = np.tile(np.arange(ny), r1 - r0)
+                strings = eng.align_strings(sx, sy, xi, yi, sc) if ny else []
+                for i, x in enumerate(range(r0, r1)):
+                    X = xs[x]
+                    yield [SequencePair(Sequence(X.id, ax, X.extras), Sequence(Y.id, ay, Y.extras))
+                           for Y, (ax, ay) in zip(ys, strings[i * ny:(i + 1) * ny])]
+        finally:
+            if own:
+                sx.free()
+                if not same:
+                    sy.free()
+
+    def upload_sets(self, xs: list[Sequence], ys: list[Sequence]) -> tuple:
+        """The engine sets ``align_product_rows`` aligns from (one set when xs is ys)."""
+        sx = self.engine.upload([s.seq for s in xs], align=True)
+        return sx, (sx if xs is ys else self.engine.upload([s.seq for s in ys], align=True))
+
     def _align_stream(self, pairs: Iterable[SequencePair]) -> Iterator[SequencePair]:
         for pair in pairs:
             yield self.align(pair)

@@ -91,8 +91,8 @@ def write_rect_pairs(path: Path, data: list, refs: list, align: bool, scores, en
                     fh.write(SequencePair(x, y))
             return
         aligner = PairwiseAligner.Biopython(scores, engine=eng)
-        for x in data:
-            for pair in aligner.align_many([SequencePair(x, y) for y in refs]):
+        for row in aligner.align_product_rows(data, refs):
+            for pair in row:
                 fh.write(pair)
 
 

@@ -56,6 +56,20 @@ def walk_strings_ok(scores: tuple, seqs: list) -> bool:
     return lo + 2 * O + 2 * P + 16384 + 8 < 32767 and hi + 2 * O + 2 * P + 16384 + 8 < 32767
 
 
+
+WALK_LAUNCH_PAIRS = 1 << 19  # ordered pairs per string-emitting aligner launch (the bench's batch)
+WALK_BLOCK_BYTES = 8 << 30   # HBM for one block's string slots + metrics
+
+
+def walk_block_rows(n: int, per_pair: int, block_bytes: int, launch_pairs: int = WALK_LAUNCH_PAIRS) -> int:
+    """Rows per block of the string-emitting row-block path: at least what ``block_bytes`` allows,
+    and enough rows for ~``launch_pairs`` pairs per launch (a 12-row block of N = 5 000 left the
+    GPU mostly idle between syncs) as long as the block's slots fit WALK_BLOCK_BYTES."""
+    per_row = max(1, n * per_pair)
+    b_bytes = block_bytes // per_row
+    b_fill = min(-(-int(launch_pairs) // max(1, n)), WALK_BLOCK_BYTES // per_row)
+    return max(1, min(n, max(b_bytes, b_fill)))
+
 class VersusAll:
     def __init__(self):
         self.work_dir: Path = None
@@ -100,8 +114,11 @@ class VersusAll:
 
         # MI355X engine options (no reference counterpart).  stream: None = automatic (row-block
         # streaming when the dense N x N x M host matrix would exceed dense_limit bytes, or with
-        # more than one rank), True / False force it; block_bytes sizes the streamed row blocks.
+        # more than one rank), True / False force it; block_bytes sizes the streamed row blocks;
+        # launch_pairs: the string-emitting row blocks grow to about this many pairs per launch
+        # (0: block_bytes alone).
         self.params.engine = AttrDict()
+        self.params.engine.launch_pairs = WALK_LAUNCH_PAIRS
         self.params.engine.stream = None
         self.params.engine.dense_limit = 4 << 30
         self.params.engine.block_bytes = 256 << 20
@@ -268,7 +285,8 @@ class VersusAll:
 
         n = len(seqs)
         cap = 2 * max(len(s.seq) for s in seqs) + 1
-        B = max(1, min(n, int(self.params.engine.block_bytes) // max(1, n * (2 * cap + 8 * len(cidx) + 4))))
+        B = walk_block_rows(n, 2 * cap + 8 * len(cidx) + 4, int(self.params.engine.block_bytes),
+                            int(self.params.engine.launch_pairs or 0))
         ids = pack_strings([s.id for s in seqs])
         dev = torch.device("cuda", eng.device)
         stream = torch.cuda.Stream(dev)
@@ -402,8 +420,8 @@ class VersusAll:
                         fh.write(SequencePair(x, y))
                 return
             aligner = PairwiseAligner.Biopython(self.params.pairs.scores, engine=self._engine())
-            for x in seqs:  # row x: (x, y) for every y, x-major like fromProduct
-                for pair in aligner.align_many([SequencePair(x, y) for y in seqs]):
+            for row in aligner.align_product_rows(seqs, seqs):  # x-major like fromProduct
+                for pair in row:
                     fh.write(pair)
 
     def write_summary(self, seqs: list, A: np.ndarray):
@@ -550,7 +568,8 @@ class VersusAll:
         sink.diag = self._diag_info(seqs, eng, st, bool(p.pairs.align), scores, labels)
         scale = 100.0 if p.format.percentage_multiply else 1.0
         cap = 2 * max((len(s.seq) for s in seqs), default=0) + 1
-        B = block_rows(n, 8 * M + (2 * cap + 4 if walk else 0), int(p.engine.block_bytes))
+        B = (walk_block_rows(n, 8 * M + 2 * cap + 4, int(p.engine.block_bytes), int(p.engine.launch_pairs or 0)) if walk
+             else block_rows(n, 8 * M, int(p.engine.block_bytes)))
         hold = sharded and (r1 - r0) * n * M * 8 <= int(p.engine.hold_bytes)
         held = []
         total = M * n * n
@@ -850,6 +869,7 @@ class _BlockWriters:
         self.aggs = [(name, SubsetAggregatorDev(eng, self.ids, part, len(self.metrics)))
                      for part, name in ((genera, "genera"), (species, "species")) if part]
         self.pairs_fh = None
+        self._pair_sets = None
         if p.pairs.write and files:
             create_parents(task.paths.aligned_pairs)
             if walk:  # text from the metric kernel's walks, handed over per block (write_text)
@@ -936,12 +956,15 @@ class _BlockWriters:
         if self.walk and self.pairs_fh is not None:
             self.pairs_fh.write(pairs_text)
         elif self.pairs_fh is not None:
-            for x in seqs[x0:x1]:
-                if self.aligner is None:
+            if self.aligner is None:
+                for x in seqs[x0:x1]:
                     for y in seqs:
                         self.pairs_fh.write(SequencePair(x, y))
-                else:
-                    for pair in self.aligner.align_many([SequencePair(x, y) for y in seqs]):
+            else:
+                if self._pair_sets is None:  # uploaded once for every block
+                    self._pair_sets = self.aligner.upload_sets(seqs, seqs)
+                for row in self.aligner.align_product_rows(seqs, seqs, range(x0, x1), sets=self._pair_sets):
+                    for pair in row:
                         self.pairs_fh.write(pair)
         if self.dupids:
             self._write_text_handlers(x0, x1, A)
@@ -1024,6 +1047,9 @@ class _BlockWriters:
                              f"{fmt.format(float(d)) if np.isfinite(d) else missing}\n")
         if self.pairs_fh is not None:
             self.pairs_fh.close()
+        if self._pair_sets is not None:
+            self._pair_sets[0].free()
+            self._pair_sets = None
         p = self.task.params
         self.task.subset_stats = {}
         for name, agg in self.aggs:

@@ -118,6 +118,7 @@ TASK = textwrap.dedent(
         t.input.sequences = Sequences(seqs)
         t.params.engine.stream = stream
         t.params.engine.block_bytes = 3 * len(seqs) * 8 * 8  # ~3 rows per block
+        t.params.engine.launch_pairs = 0
         if variant == "full":
             t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.UncorrectedWithGaps(),
                                           DistanceMetric.JukesCantor(), DistanceMetric.Kimura2P(),
@@ -242,6 +243,7 @@ def test_streamed_reductions_only(tmp_path, engine):
         t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.Kimura2P()]
         t.params.engine.stream = stream
         t.params.engine.block_bytes = 4 * len(raw) * 8 * 8
+        t.params.engine.launch_pairs = 0
         if stream:
             t.params.engine.row_minima = "k2p"
             t.params.engine.write_summary = False

@@ -99,6 +99,7 @@ def test_task_pairs_from_walks_equal_round2_path(tmp_path, engine, variant, stre
             t.input.sequences = Sequences(seqs)
             t.params.engine.stream = stream
             t.params.engine.block_bytes = 7 * len(seqs) * 1000  # a few rows per block
+            t.params.engine.launch_pairs = 0
             if variant == "generic":
                 t.params.pairs.scores = dict(Scores(match_score=2, mismatch_score=-3, internal_open_gap_score=-5,
                                                     internal_extend_gap_score=-2, end_open_gap_score=-1,

@@ -43,7 +43,15 @@ def run(n: int, eng, null: bool) -> dict:
                 (out / f).parent.mkdir(parents=True, exist_ok=True)
                 os.symlink("/dev/null", out / f)
         t = VersusAll()
-        t.engine, t.progress_handler, t.work_dir = eng, None, out
+        last = [time.perf_counter()]
+
+        def progress(caption, index, total):  # a line every ~20 s (long runs must keep writing)
+            now = time.perf_counter()
+            if now - last[0] > 20.0:
+                last[0] = now
+                print(f"n={n}: {caption} {index}/{total}", file=sys.stderr, flush=True)
+
+        t.engine, t.progress_handler, t.work_dir = eng, progress, out
         t.input.sequences = Sequences(seqs)
         t0 = time.perf_counter()
         res = t.start()
