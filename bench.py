@@ -239,12 +239,16 @@ def compute_roofline(gcups: float) -> dict | None:
     clock = c["clock_ghz"] * 1e9                          # GRBM_GUI_ACTIVE / 8 / kernel time (PMC)
     achieved = gcups * 1e9 * instr_per_cell / (N_SIMDS * clock)  # wave-instructions per SIMD-cycle
     peak = c["ceiling_instr_per_simd_clk"]
+    full = 1.0 / c.get("full_rate_cycles", 2.28)  # every instruction at the full VOP2 rate
     return {
         "bound": "valu-issue",
         "unit": "wave64 VALU instructions per SIMD-cycle",
         "achieved": achieved,
         "peak": peak,
         "frac": achieved / peak,
+        "full_rate_peak": full,
+        "frac_of_full_rate": achieved / full,
+        "full_rate_share_of_mix": c.get("full_rate_share"),
         "gcups": gcups,
         "ops_per_cell": instr_per_cell * 64,
         "source": c["source"],

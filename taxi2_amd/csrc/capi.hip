@@ -1762,7 +1762,10 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     // ~256 MB of scratch (and the groups' LDS sort), in ascending order on one stream; each row's
     // subsets in chunks of SUB_CH columns (tmax bounds the chunks per row: sum of ceil(size / CH))
     const int64_t per_row = (int64_t)ns * m;
-    const int64_t tmax64 = (int64_t)ns + (ncols + SUB_CH - 1) / SUB_CH;
+    // few subsets: natural-order rows (k_subset_rows_nat), ns x nch chunk slots per row
+    const int64_t nch = std::max<int64_t>(1, (ncols + SUB_CH - 1) / SUB_CH);
+    const bool nat = ns <= 4 && !getenv("TAXI2_SUB_GATHER");
+    const int64_t tmax64 = nat ? (int64_t)ns * nch : (int64_t)ns + (ncols + SUB_CH - 1) / SUB_CH;
     if (tmax64 > INT32_MAX / 2) return fail(ctx, "taxi2_subset_aggregate_dev: too many subsets");
     const int tmax = (int)tmax64;
     const int64_t row_bytes = per_row * (int64_t)(sizeof(SubPart) + sizeof(SubWork)) + tmax64 * m * (int64_t)sizeof(SubPart);
@@ -1772,7 +1775,8 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     const size_t o_part = 0, o_work = al((size_t)rsub * per_row * sizeof(SubPart));
     const size_t o_cpart = o_work + al((size_t)rsub * per_row * sizeof(SubWork));
     const size_t o_cofs = o_cpart + al((size_t)rsub * tmax * m * sizeof(SubPart));
-    const size_t o_rows = o_cofs + al((size_t)(ns + 1) * 4);
+    const size_t o_ccode = o_cofs + al((size_t)(ns + 1) * 4);
+    const size_t o_rows = o_ccode + al((size_t)(nat ? ncols : 0) + 1);
     const size_t o_code = o_rows + al((size_t)rsub * 4), o_start = o_code + al((size_t)rsub * 4);
     const size_t o_n = o_start + al((size_t)(rsub + 1) * 4), total = o_n + 256;
     if (ensure(ctx, &ctx->d_sub, &ctx->d_sub_bytes, total)) return -1;
@@ -1786,7 +1790,19 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     int32_t* gstart = (int32_t*)(base + o_start);
     int32_t* ngrp = (int32_t*)(base + o_n);
     unsigned int* wcount = (unsigned int*)(base + o_n + 64);
-    hipLaunchKernelGGL(k_subset_cofs, dim3(1), dim3(1024), 0, st, d_col_start, (int)ns, cofs);
+    uint8_t* ccode = (uint8_t*)(base + o_ccode);
+    if (nat) {
+        std::vector<int32_t> hc(ns + 1);
+        for (int b = 0; b <= ns; ++b) hc[b] = (int32_t)(b * nch);
+        HIP_TRY(ctx, hipMemcpyAsync(cofs, hc.data(), (ns + 1) * 4, hipMemcpyHostToDevice, st));
+        if (ncols > 0)
+            hipLaunchKernelGGL(k_subset_colcode, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, st, d_col_start,
+                               d_col_idx, (int)ns, ncols, ccode);
+        // the host vector must outlive the async copy
+        HIP_TRY(ctx, hipStreamSynchronize(st));
+    } else {
+        hipLaunchKernelGGL(k_subset_cofs, dim3(1), dim3(1024), 0, st, d_col_start, (int)ns, cofs);
+    }
     HIP_TRY(ctx, hipGetLastError());
     for (int64_t r0 = 0; r0 < nrows; r0 += rsub) {
         const int64_t nr = std::min(rsub, nrows - r0);
@@ -1794,8 +1810,19 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
         const int32_t* rc = d_row_code + r0;
         hipLaunchKernelGGL(k_subset_groups, dim3(1), dim3(1024), 0, st, rc, (int)nr, grows, gcode, gstart, ngrp);
         HIP_TRY(ctx, hipGetLastError());
-        hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * tmax + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m, rc,
-                           d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum, cpart);
+        if (nat) {
+            const dim3 g((unsigned)((nr * nch + 3) / 4)), b(256);
+            if (ns <= 2)
+                hipLaunchKernelGGL(k_subset_rows_nat<2>, g, b, 0, st, v, nr, ncols, m, rc, (const uint8_t*)ccode, (int)ns,
+                                   (int)nch, (const double*)d_sum, cpart);
+            else
+                hipLaunchKernelGGL(k_subset_rows_nat<4>, g, b, 0, st, v, nr, ncols, m, rc, (const uint8_t*)ccode, (int)ns,
+                                   (int)nch, (const double*)d_sum, cpart);
+        } else {
+            hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * tmax + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m,
+                               rc, d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum,
+                               cpart);
+        }
         HIP_TRY(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_subset_rowmerge, dim3((unsigned)((nr * per_row + 255) / 256)), dim3(256), 0, st, nr,
                            (int)ns, m, (const int32_t*)cofs, tmax, (const SubPart*)cpart, part);

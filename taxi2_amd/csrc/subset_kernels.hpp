@@ -18,6 +18,9 @@
 //                     the row's key at SUB_J grids -- u, 2u, 4u, 8u with u from the key's sum at
 //                     block start (binades e0 .. e0 + 3) -- the row's integer sums, count, first
 //                     minimum, maximum, and flags (tie at each grid / negative / no grid: s = 0)
+//   (few subsets, ns <= 4: k_subset_rows_nat reads each row in natural column order instead, one
+//                     wave per (row, 2 048 consecutive columns), values routed to per-subset
+//                     accumulators in registers: no gather)
 //   k_subset_rowmerge one thread per (row x, b, metric): the row's chunk partials in column order
 //                     (integer sums are exact in any order; the first minimum stays the first)
 //   k_subset_combine  one thread per (row group a, b, metric): walks the block's rows of subset a
@@ -247,6 +250,114 @@ __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ 
             P.flags = fl;
             P.pad = 0;
             part[(x * tmax + t) * m + k] = P;
+        }
+    }
+}
+
+// Column codes from the sorted layout: code[col_idx[j]] = b for j in [col_start[b], col_start[b+1]).
+__global__ void __launch_bounds__(256) k_subset_colcode(const int64_t* __restrict__ col_start,
+                                                        const int32_t* __restrict__ col_idx, int ns, int64_t ncols,
+                                                        uint8_t* __restrict__ code) {
+    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j >= ncols) return;
+    int lo = 0, hi = ns;  // the last b with col_start[b] <= j
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (col_start[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    code[col_idx[j]] = (uint8_t)lo;
+}
+
+// Few subsets (ns <= NSB): one wave per (block row x, chunk of SUB_CH CONSECUTIVE columns), the
+// row read in natural order (coalesced, no gather) and every value routed to its subset's
+// accumulators in registers; the partial of (x, chunk c, subset b) goes to slot b * nch + c, so
+// k_subset_rowmerge (cofs[b] = b * nch) merges each subset's chunks in column order.  Same
+// partial contents as k_subset_rows: the subset's values of the chunk in ascending column order.
+template <int NSB>
+__global__ void __launch_bounds__(256) k_subset_rows_nat(const double* __restrict__ vals, int64_t nrows,
+                                                         int64_t ncols, int m, const int32_t* __restrict__ row_code,
+                                                         const uint8_t* __restrict__ col_code, int ns, int nch,
+                                                         const double* __restrict__ sum, SubPart* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nrows * nch) return;
+    const int64_t x = w / nch;
+    const int c = (int)(w - x * nch);
+    const int a = row_code[x];
+    const int64_t j0 = (int64_t)c * SUB_CH, j1 = min(ncols, j0 + SUB_CH);
+    const double* row = vals + x * ncols * m;
+    const int tmax = ns * nch;
+    for (int k = 0; k < m; ++k) {
+        int sc[NSB];
+        bool grid[NSB];
+        double rs[NSB][SUB_J], mn[NSB], mx[NSB];
+        long long cnt[NSB], mnp[NSB];
+        uint32_t fl[NSB];
+#pragma unroll
+        for (int b = 0; b < NSB; ++b) {
+            int e = 0;
+            grid[b] = b < ns && sub_grid(sum[((int64_t)a * ns + b) * m + k], e);
+            sc[b] = 53 - e;
+            for (int q = 0; q < SUB_J; ++q) rs[b][q] = 0.0;
+            mn[b] = __builtin_inf();
+            mx[b] = 0.0;
+            cnt[b] = 0;
+            mnp[b] = 0x7FFFFFFFFFFFFFFFll;
+            fl[b] = grid[b] ? 0u : SP_NOGRID;
+        }
+        for (int64_t j = j0 + lane; j < j1; j += 64) {
+            const double v = row[j * m + k];
+            const int cb = col_code[j];
+            if (!isfinite(v)) continue;
+#pragma unroll
+            for (int b = 0; b < NSB; ++b) {
+                if (cb != b) continue;
+                ++cnt[b];
+                if (v < mn[b]) {
+                    mn[b] = v;
+                    mnp[b] = j;
+                }
+                if (v > mx[b]) mx[b] = v;
+                if (grid[b]) {
+                    if (v < 0.0) fl[b] |= SP_NEG;
+#pragma unroll
+                    for (int q = 0; q < SUB_J; ++q) {
+                        const double r = ldexp(v, sc[b] - q);
+                        const double R = rint(r);
+                        if (fabs(r - R) == 0.5) fl[b] |= (uint32_t)SP_TIE << q;
+                        rs[b][q] += R;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < NSB; ++b) {
+            if (b >= ns) break;
+            for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+                for (int q = 0; q < SUB_J; ++q) rs[b][q] += __shfl_xor(rs[b][q], o);
+                cnt[b] += __shfl_xor(cnt[b], o);
+                fl[b] |= (uint32_t)__shfl_xor((int)fl[b], o);
+                const double omx = __shfl_xor(mx[b], o);
+                if (omx > mx[b]) mx[b] = omx;
+                const double omn = __shfl_xor(mn[b], o);
+                const long long omp = __shfl_xor(mnp[b], o);
+                if (omn < mn[b] || (omn == mn[b] && omp < mnp[b])) {
+                    mn[b] = omn;
+                    mnp[b] = omp;
+                }
+            }
+            if (lane == 0) {
+                SubPart P;
+                for (int q = 0; q < SUB_J; ++q) P.rsum[q] = rs[b][q];
+                P.mn = mn[b];
+                P.mx = mx[b];
+                P.cnt = cnt[b];
+                P.flags = fl[b];
+                P.pad = 0;
+                part[(x * tmax + (int64_t)b * nch + c) * m + k] = P;
+            }
         }
     }
 }

@@ -155,11 +155,15 @@ def seq_aggregate_np(A: np.ndarray, code: np.ndarray, ns: int):
     return s, lo, hi, c
 
 
-@pytest.mark.parametrize("kind", ["percent", "dyadic", "uniform"])
+@pytest.mark.parametrize("path", ["natural", "gather"])
+@pytest.mark.parametrize("kind", ["percent", "dyadic"])
 @pytest.mark.parametrize("ns,block", [(1, 700), (2, 1999), (3, 5000)])
-def test_subset_aggregate_wide_subsets(engine, kind, ns, block):
-    """Subsets wider than one k_subset_rows chunk (2 048 columns): chunk partials merged per row in
-    column order, multi-grid row partials across binade changes."""
+def test_subset_aggregate_wide_subsets(engine, monkeypatch, path, kind, ns, block):
+    """Subsets wider than one chunk (2 048 columns): chunk partials merged per row in column order,
+    multi-grid row partials across binade changes -- through the natural-order rows kernel that
+    few subsets take (k_subset_rows_nat) and through the sorted-gather one (TAXI2_SUB_GATHER=1)."""
+    if path == "gather":
+        monkeypatch.setenv("TAXI2_SUB_GATHER", "1")
     rng = np.random.default_rng(hash(("wide", kind, ns, block)) % 2**32)
     n, m = 5000, 2
     A = values(rng, n, m, kind)

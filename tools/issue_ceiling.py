@@ -275,6 +275,7 @@ def main() -> None:
         "ceiling_instr_per_simd_clk": 1.0 / mean_cyc,
         "pmc_frac_of_ceiling": achieved * mean_cyc,
         "full_rate_share": sum(c for op, c in hot_all.items() if price(op, costs, Counter()) < 3.0) / n_all,
+        "full_rate_cycles": costs.get("v_add_u32", 2.28),  # the full-rate (VOP2 32-bit) issue cost
         "trace_band": args.band,
         "trace_block_weight": f,
         "step_loops": loops,
