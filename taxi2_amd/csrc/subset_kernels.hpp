@@ -63,6 +63,7 @@ struct SubWork {  // a key the combine could not finish: its rows from grp_rows[
 constexpr double SUB_TOP = 9007199254740991.0;  // 2^53 - 1: largest integer multiple of u below 2^E
 constexpr int SUB_MAX_ROWS = 8192;              // rows per k_subset_groups call (LDS sort)
 constexpr int SUB_CH = 2048;                    // columns per k_subset_rows wave (a subset's chunk)
+constexpr int SUB_FU = 8;                       // fixup: 64-value groups per iteration
 
 // The grid of running sum s: true with s in [2^(e-1), 2^e) when s is a positive normal number.
 __device__ __forceinline__ bool sub_grid(double s, int& e) {
@@ -457,16 +458,28 @@ __global__ void __launch_bounds__(256) k_subset_fixup(const double* __restrict__
                 }
             }
             const double* row = vals + x * ncols * m;
-            for (int64_t c0 = j0; c0 < j1; c0 += 64) {
-                const int64_t j = c0 + lane;
-                double v = j < j1 ? row[(int64_t)col_idx[j] * m + k] : 0.0;
-                if (!isfinite(v)) v = 0.0;  // None: skipped (+0.0 adds nothing)
-                if (sub_grid(s, e)) {  // the integer step, when the whole chunk qualifies
-                    const double rr = ldexp(v, 53 - e);
-                    const double R = rint(rr);
-                    const bool bad = v < 0.0 || fabs(rr - R) == 0.5;
+            // SUB_FU x 64 values per iteration (SUB_FU loads per lane in flight): one integer step
+            // for all of them when they qualify, else 64 at a time, else one by one
+            for (int64_t c0 = j0; c0 < j1; c0 += 64 * SUB_FU) {
+                double v[SUB_FU];
+#pragma unroll
+                for (int u = 0; u < SUB_FU; ++u) {
+                    const int64_t j = c0 + 64 * u + lane;
+                    const double w = j < j1 ? row[(int64_t)col_idx[j] * m + k] : 0.0;
+                    v[u] = isfinite(w) ? w : 0.0;  // None: skipped (+0.0 adds nothing)
+                }
+                if (sub_grid(s, e)) {
+                    bool bad = false;
+                    double tot = 0.0;
+#pragma unroll
+                    for (int u = 0; u < SUB_FU; ++u) {
+                        const double rr = ldexp(v[u], 53 - e);
+                        const double R = rint(rr);
+                        bad |= v[u] < 0.0 || fabs(rr - R) == 0.5;
+                        tot += R;  // integers < 2^53: exact
+                    }
                     if (!__any(bad)) {
-                        const double tot = wave_sum_f64(R);
+                        tot = wave_sum_f64(tot);
                         const double S = ldexp(s, 53 - e);
                         if (S + tot <= SUB_TOP) {
                             s = ldexp(S + tot, e - 53);
@@ -474,8 +487,26 @@ __global__ void __launch_bounds__(256) k_subset_fixup(const double* __restrict__
                         }
                     }
                 }
-                const int n = (int)min((int64_t)64, j1 - c0);
-                for (int l = 0; l < n; ++l) s = s + __shfl(v, l);  // the reference's own additions
+#pragma unroll
+                for (int u = 0; u < SUB_FU; ++u) {
+                    const int64_t cu = c0 + 64 * u;
+                    if (cu >= j1) break;
+                    if (sub_grid(s, e)) {  // the integer step, when these 64 qualify
+                        const double rr = ldexp(v[u], 53 - e);
+                        const double R = rint(rr);
+                        const bool bad = v[u] < 0.0 || fabs(rr - R) == 0.5;
+                        if (!__any(bad)) {
+                            const double tot = wave_sum_f64(R);
+                            const double S = ldexp(s, 53 - e);
+                            if (S + tot <= SUB_TOP) {
+                                s = ldexp(S + tot, e - 53);
+                                continue;
+                            }
+                        }
+                    }
+                    const int n = (int)min((int64_t)64, j1 - cu);
+                    for (int l = 0; l < n; ++l) s = s + __shfl(v[u], l);  // the reference's own additions
+                }
             }
         }
         if (lane == 0) sum[it.key] = s;
