@@ -175,6 +175,18 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
                            const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* d_out,
                            int32_t cap, uint8_t* d_sx, uint8_t* d_sy, int32_t* d_slen, void* stream);
 
+/* Metrics and aligned strings of the unordered pairs [k0, k0 + count) of the versusAll triangle
+ * (pair k = (a, b), a < b, numbered as taxi2_all_pairs) from ONE fill each: the walkers walk both
+ * orientations, as the metric kernel does.  d_out[k][2][nmetrics] as taxi2_all_pairs (row (a, b),
+ * then row (b, a)); slot k*2 + 0 = the alignment of (a, b), slot k*2 + 1 = the alignment Biopython
+ * returns for (b, a) written in (a, b) column order (d_sx holds a's aligned string, d_sy b's), each
+ * right-aligned at byte len(a) + len(b) of its cap-byte slot, lengths d_slen[k*2 + o].  Replaces
+ * versus_all.py:746-750's two alignments of a pair (one per ordered pair) by one fill.  Same
+ * shape limits as taxi2_rect_strings_dev. */
+int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
+                          const int32_t* metrics, int nmetrics, double* d_out, int32_t cap, uint8_t* d_sx,
+                          uint8_t* d_sy, int32_t* d_slen, void* stream);
+
 /* aligned_pairs.txt text (pairs.py:51-97 SequencePairHandler.Formatted) of the rectangle rows
  * [q0, q1) x every r from taxi2_rect_strings_dev slots (device): per pair "idx / idy" LF, the
  * aligned x, the pattern ('|' equal non-gap, '-' gap, '.' mismatch), the aligned y, each LF-ended;
@@ -186,6 +198,15 @@ int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
                            const uint8_t* row_ids, const int64_t* row_offs, const uint8_t* col_ids,
                            const int64_t* col_offs, int first, uint8_t* out, int64_t out_cap,
                            int64_t* out_len, void* stream);
+
+/* Same text from per-pair string pointers: pair (r, c) of the nrows x ncols block (row-major k =
+ * r * ncols + c) shows the d_slen[k] bytes at device addresses d_px[k] (first line) and d_py[k]
+ * (third line) -- e.g. taxi2_tri_strings_dev slots of this block and strings kept from earlier
+ * blocks' fills (the (b, a) orientation of a pair filled with row a). */
+int taxi2_format_pairs_ptr_dev(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, const uint64_t* d_px,
+                               const uint64_t* d_py, const int32_t* d_slen, const uint8_t* row_ids,
+                               const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, int first,
+                               uint8_t* out, int64_t out_cap, int64_t* out_len, void* stream);
 
 /* ---- NCD (distances.py:351-358 NCD._calculate -> alfpy 1.0.6 ncd.Distance) ---------------- *
  * NCD(x, y) = (C(X+Y) - min(C(X), C(Y))) / max(C(X), C(Y)), X / Y = upper-cased strings,

@@ -40,6 +40,8 @@ EXPORTS = (
     "taxi2_rect_pairs",
     "taxi2_rect_pairs_dev",
     "taxi2_rect_strings_dev",
+    "taxi2_tri_strings_dev",
+    "taxi2_format_pairs_ptr_dev",
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
@@ -103,6 +105,10 @@ _SIGNATURES = {
                                       _P, _P]),
     "taxi2_format_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
                                       ctypes.POINTER(_I64), _P]),
+    "taxi2_tri_strings_dev": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _I32, _P, _P, _P,
+                                     _P]),
+    "taxi2_format_pairs_ptr_dev": (_INT, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
+                                          ctypes.POINTER(_I64), _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
@@ -425,6 +431,50 @@ class Engine:
                 ),
                 "taxi2_rect_strings_dev",
             )
+
+    def tri_strings_dev(self, s: SeqSet, k0: int, count: int, metrics, out_ptr: int | None, cap: int, sx_ptr: int,
+                        sy_ptr: int, slen_ptr: int, scores=None, stream: int | None = None) -> None:
+        """Metrics ([count][2][M], may be empty) and BOTH orientations' aligned strings of the
+        triangle pairs [k0, k0 + count), one fill per pair (device slots [k][2][cap]; see
+        taxi2_tri_strings_dev)."""
+        codes = metric_codes(metrics) if metrics else np.zeros(0, dtype=np.int32)
+        cs = to_cscores(scores)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_tri_strings_dev(
+                    self._ctx, s.id, int(k0), int(count), ctypes.byref(cs), codes.ctypes.data if len(codes) else None,
+                    len(codes), ctypes.c_void_p(out_ptr) if out_ptr else None, int(cap), ctypes.c_void_p(sx_ptr),
+                    ctypes.c_void_p(sy_ptr), ctypes.c_void_p(slen_ptr), ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_tri_strings_dev",
+            )
+
+    def format_pairs_ptr_dev(self, nrows: int, ncols: int, px_ptr: int, py_ptr: int, slen_ptr: int, row_ids, col_ids,
+                             *, first: bool, stream: int | None = None) -> memoryview:
+        """aligned_pairs.txt text of an nrows x ncols block from per-pair string pointers
+        (taxi2_format_pairs_ptr_dev); a memoryview of the pinned text buffer, valid until the next
+        text call."""
+        rb, ro = row_ids
+        cb, co = col_ids
+        need = _I64()
+        buf = getattr(self, "_pairs_buf", None)
+        if buf is None:
+            buf = self._pinned(1 << 20)
+        for _ in range(2):
+            with self._lock:
+                rc = self._lib.taxi2_format_pairs_ptr_dev(
+                    self._ctx, int(nrows), int(ncols), ctypes.c_void_p(px_ptr), ctypes.c_void_p(py_ptr),
+                    ctypes.c_void_p(slen_ptr), rb.ctypes.data, ro.ctypes.data, cb.ctypes.data, co.ctypes.data,
+                    1 if first else 0, buf.ctypes.data, buf.size, ctypes.byref(need),
+                    ctypes.c_void_p(stream) if stream else None)
+            if rc == 1:
+                self._pairs_buf = None
+                buf = self._pinned(max(int(need.value), 2 * buf.size))
+                continue
+            self._check(rc, "taxi2_format_pairs_ptr_dev")
+            self._pairs_buf = buf
+            return memoryview(buf[: need.value])
+        raise NativeError("taxi2_format_pairs_ptr_dev: output buffer sizing failed")
 
     def format_pairs_dev(self, q: SeqSet, r: SeqSet, q0: int, q1: int, cap: int, sx_ptr: int, sy_ptr: int,
                          slen_ptr: int, row_ids, col_ids, *, first: bool, stream: int | None = None) -> bytes:

@@ -1216,6 +1216,28 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
     return rc;
 }
 
+int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
+                          const int32_t* metrics, int nmetrics, double* d_out, int32_t cap, uint8_t* d_sx,
+                          uint8_t* d_sy, int32_t* d_slen, void* stream) {
+    if (!ctx) return -1;
+    DevSet* S = get_set(ctx, set);
+    if (!S) return fail(ctx, "unknown set");
+    if (S->mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need an ALIGN set");
+    if (!sc) return fail(ctx, "scores required");
+    MetricSpec ms{};
+    if (nmetrics > 0 && check_metrics(ctx, metrics, nmetrics, ms, true, S->max_len)) return -1;
+    const int64_t total = S->n * (S->n - 1) / 2;
+    if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
+    if (count > 0 && (!d_sx || !d_sy || !d_slen || (nmetrics > 0 && !d_out))) return fail(ctx, "null output");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairSrc ps{PAIRS_TRI, k0, count, S->n, 0, nullptr, nullptr};
+    const int rc = launch_packed_strings(ctx, *S, *S, ps, sc, ms, OUT_BOTH, d_out, nullptr, st,
+                                         StrOut{d_sx, d_sy, d_slen, cap, 2});
+    if (rc > 0) return fail(ctx, "walker strings need the packed aligner (Gotoh scores within int16, <= 2 048 bp)");
+    return rc;
+}
+
 int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const taxi2_scores* sc,
                          const int32_t* metrics, int nmetrics, double* d_out, int32_t* d_scores, void* stream) {
     if (!ctx) return -1;
@@ -1653,22 +1675,11 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
 
 extern "C" {
 
-int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, int32_t cap,
-                           const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, const uint8_t* row_ids,
-                           const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, int first,
-                           uint8_t* out, int64_t out_cap, int64_t* out_len, void* stream) {
-    if (!ctx) return -1;
-    DevSet* Q = get_set(ctx, set_q);
-    DevSet* R = get_set(ctx, set_r);
-    if (!Q || !R) return fail(ctx, "unknown set");
-    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
-    if (!out_len || !row_offs || !col_offs) return fail(ctx, "null argument");
-    const int64_t nrows = q1 - q0, ncols = R->n;
-    *out_len = 0;
-    if (nrows == 0 || ncols == 0) return 0;
-    if (!d_sx || !d_sy || !d_slen) return fail(ctx, "null string slots");
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+namespace {
+// Both pair-text entry points: ids to the device, per-row lengths, host prefix, the text, D2H.
+int format_pairs_impl(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, PairFmtArgs a, const uint8_t* row_ids,
+                      const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, uint8_t* out,
+                      int64_t out_cap, int64_t* out_len, hipStream_t st) {
     const int64_t rb = row_offs[nrows] - row_offs[0], cb = col_offs[ncols] - col_offs[0];
     auto al = [](size_t v) { return (v + 255) / 256 * 256; };
     const size_t o_ro = 0, o_co = o_ro + al((size_t)(nrows + 1) * 8), o_rid = o_co + al((size_t)(ncols + 1) * 8);
@@ -1683,8 +1694,11 @@ int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
     HIP_TRY(ctx, hipMemcpyAsync(b + o_co, co.data(), (ncols + 1) * 8, hipMemcpyHostToDevice, st));
     if (rb) HIP_TRY(ctx, hipMemcpyAsync(b + o_rid, row_ids + row_offs[0], rb, hipMemcpyHostToDevice, st));
     if (cb) HIP_TRY(ctx, hipMemcpyAsync(b + o_cid, col_ids + col_offs[0], cb, hipMemcpyHostToDevice, st));
-    PairFmtArgs a{d_sx, d_sy, d_slen, (int64_t)cap, Q->meta + q0, R->meta, ncols, (const uint8_t*)(b + o_rid),
-                  (const int64_t*)(b + o_ro), (const uint8_t*)(b + o_cid), (const int64_t*)(b + o_co), first ? 1 : 0};
+    a.ncols = ncols;
+    a.rid = (const uint8_t*)(b + o_rid);
+    a.roffs = (const int64_t*)(b + o_ro);
+    a.cid = (const uint8_t*)(b + o_cid);
+    a.coffs = (const int64_t*)(b + o_co);
     int64_t* d_rlen = (int64_t*)(b + o_len);
     int64_t* d_rbase = (int64_t*)(b + o_base);
     hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rlen);
@@ -1707,6 +1721,45 @@ int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
     HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, st));
     HIP_TRY(ctx, hipStreamSynchronize(st));
     return 0;
+}
+}  // namespace
+
+int taxi2_format_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, int32_t cap,
+                           const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, const uint8_t* row_ids,
+                           const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, int first,
+                           uint8_t* out, int64_t out_cap, int64_t* out_len, void* stream) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if (!out_len || !row_offs || !col_offs) return fail(ctx, "null argument");
+    const int64_t nrows = q1 - q0, ncols = R->n;
+    *out_len = 0;
+    if (nrows == 0 || ncols == 0) return 0;
+    if (!d_sx || !d_sy || !d_slen) return fail(ctx, "null string slots");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairFmtArgs a{d_sx, d_sy, d_slen, (int64_t)cap, Q->meta + q0, R->meta, ncols, nullptr, nullptr, nullptr, nullptr,
+                  first ? 1 : 0};
+    return format_pairs_impl(ctx, nrows, ncols, a, row_ids, row_offs, col_ids, col_offs, out, out_cap, out_len, st);
+}
+
+int taxi2_format_pairs_ptr_dev(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, const uint64_t* d_px,
+                               const uint64_t* d_py, const int32_t* d_slen, const uint8_t* row_ids,
+                               const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, int first,
+                               uint8_t* out, int64_t out_cap, int64_t* out_len, void* stream) {
+    if (!ctx) return -1;
+    if (nrows < 0 || ncols < 0) return fail(ctx, "negative size");
+    if (!out_len || !row_offs || !col_offs) return fail(ctx, "null argument");
+    *out_len = 0;
+    if (nrows == 0 || ncols == 0) return 0;
+    if (!d_px || !d_py || !d_slen) return fail(ctx, "null string pointers");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairFmtArgs a{nullptr, nullptr, d_slen, 0, nullptr, nullptr, ncols, nullptr, nullptr, nullptr, nullptr,
+                  first ? 1 : 0, d_px, d_py};
+    return format_pairs_impl(ctx, nrows, ncols, a, row_ids, row_offs, col_ids, col_offs, out, out_cap, out_len, st);
 }
 
 int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,

@@ -258,6 +258,10 @@ struct PairFmtArgs {
     const uint8_t* cid;
     const int64_t* coffs;
     int first;  // 1: the block's pair (0, 0) opens the file (no separator before it)
+    // pointer mode (px != nullptr): pair k's aligned strings start at px[k] / py[k] (slen[k] bytes
+    // each) instead of right-aligned slots -- strings kept from another block's fill
+    const uint64_t* px = nullptr;
+    const uint64_t* py = nullptr;
 };
 
 __device__ __forceinline__ int64_t pair_fmt_len(const PairFmtArgs& a, int64_t r, int64_t c) {
@@ -291,7 +295,7 @@ k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restri
     int64_t base = row_base[r];
     const int lx = (int)(a.roffs[r + 1] - a.roffs[r]);
     const uint8_t* idx = a.rid + a.roffs[r];
-    const int nx = a.qmeta[r].x;
+    const int nx = a.px ? 0 : a.qmeta[r].x;
     for (int64_t c0 = 0; c0 < a.ncols; c0 += FMT_BLOCK) {
         const int64_t c = c0 + threadIdx.x;
         const int64_t len = c < a.ncols ? pair_fmt_len(a, r, c) : 0;
@@ -313,9 +317,15 @@ k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restri
             const int ly = (int)(a.coffs[cc + 1] - a.coffs[cc]);
             const uint8_t* idy = a.cid + a.coffs[cc];
             const int L = a.slen[k];
-            const int64_t end = (int64_t)nx + a.rmeta[cc].x;
-            const uint8_t* X = a.sx + k * a.cap + end - L;
-            const uint8_t* Y = a.sy + k * a.cap + end - L;
+            const uint8_t *X, *Y;
+            if (a.px) {
+                X = (const uint8_t*)a.px[k];
+                Y = (const uint8_t*)a.py[k];
+            } else {
+                const int64_t end = (int64_t)nx + a.rmeta[cc].x;
+                X = a.sx + k * a.cap + end - L;
+                Y = a.sy + k * a.cap + end - L;
+            }
             const int h = sep + lx + 3 + ly + 1;  // header with its separator
             for (int64_t t = lane; t < plen; t += 64) {
                 char ch;

@@ -120,3 +120,49 @@ def test_task_pairs_from_walks_equal_round2_path(tmp_path, engine, variant, stre
     assert files
     for f in files:
         assert (tmp_path / "walk" / f).read_bytes() == (tmp_path / "r2" / f).read_bytes(), f
+
+
+@pytest.mark.parametrize("mode", ["one_block", "small_blocks", "switch"])
+@pytest.mark.parametrize("variant", ["default", "generic"])
+def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant):
+    """Dense aligned_pairs.txt from ONE fill per unordered pair (taxi2_tri_strings_dev: both
+    orientations walked, the (b, a) strings kept in HBM until row b, text through per-pair pointers)
+    == the rect path that aligns every ordered pair once (TAXI2_PAIRS_RECT=1), every output file
+    byte for byte: one block, many small blocks, and a keep budget that runs out mid-way (the
+    remaining rows switch to the rect path)."""
+    from taxi2_amd.align import Scores
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    raw = family_sequences(26, 500, 0x71, ancestors=3) + random_sequences(6, 1, 80, 72, "ACGTN") + ["A", ""]
+    seqs = [Sequence(f"q{k}", s, {"v": str(k % 4)}) for k, s in enumerate(raw)]
+    seqs.append(Sequence("q5", raw[5], {"v": "1"}))  # an identical full tuple (the diagonal rule)
+
+    def run(out, rect):
+        if rect:
+            os.environ["TAXI2_PAIRS_RECT"] = "1"
+        try:
+            t = VersusAll()
+            t.engine, t.progress_handler, t.work_dir = engine, None, out
+            t.input.sequences = Sequences(seqs)
+            t.params.engine.stream = False
+            if variant == "generic":
+                t.params.pairs.scores = dict(Scores(match_score=2, mismatch_score=-3, internal_open_gap_score=-5,
+                                                    internal_extend_gap_score=-2, end_open_gap_score=-1,
+                                                    end_extend_gap_score=-1))
+            if mode != "one_block":
+                t.params.engine.launch_pairs = 97  # a few rows per block
+            if mode == "switch":
+                t.params.engine.keep_bytes = 40_000  # runs out after the first blocks
+            t.start()
+            return t
+        finally:
+            os.environ.pop("TAXI2_PAIRS_RECT", None)
+
+    a = run(tmp_path / "tri", False)
+    b = run(tmp_path / "rect", True)
+    assert a.pairs_walked and b.pairs_walked
+    files = sorted(p.relative_to(tmp_path / "rect") for p in (tmp_path / "rect").rglob("*") if p.is_file())
+    assert files
+    for f in files:
+        assert (tmp_path / "tri" / f).read_bytes() == (tmp_path / "rect" / f).read_bytes(), f
