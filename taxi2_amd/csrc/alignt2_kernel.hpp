@@ -81,16 +81,6 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 #ifndef A2_D16_SUB
 #define A2_D16_SUB 0
 #endif
-// Experiments (timing only, not exact): A2_EXP_NOCOLC = 1 uses the internal gap-open constant for
-// every column (the end-gap column nB included) from a uniform register instead of the per-column
-// LDS constants -- the upper bound of removing those reads; A2_FILL_PRIO >= 0 raises the fill
-// waves' issue priority (s_setprio) over the walker's.
-#ifndef A2_EXP_NOCOLC
-#define A2_EXP_NOCOLC 0
-#endif
-#ifndef A2_FILL_PRIO
-#define A2_FILL_PRIO -1
-#endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
 #endif
@@ -715,7 +705,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                         const int s = ((j <= nB && c == (uint32_t)"ACGT"[r]) ? sc.ma : sc.mi) - 2 * dz;
                         ew[r][k / 2] |= ((uint32_t)s & 0xFFFFu) << (16 * (k & 1));
                     }
-                    const int oc = ((j == nB && !A2_EXP_NOCOLC) ? sc.eo : sc.io) - dz, ec = (j == nB) ? sc.ee : sc.ie;
+                    const int oc = ((j == nB) ? sc.eo : sc.io) - dz, ec = (j == nB) ? sc.ee : sc.ie;
                     colc[k][tid] = pk_int(pk2(oc, oc));
                     if (!DEF) colx[DEF ? 0 : k][tid] = pk_int(pk2(ec, ec));
                 }
@@ -910,11 +900,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     // default scores: both substitution halves are >= 0 (drift), so M is one
                                     // 32-bit add too; other scores may subtract: per-half add
                                     const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;
-#if A2_EXP_NOCOLC
-                                    const at_s2 cg = padd32(G1, pk_int(pk2(sc.io - dz, sc.io - dz)));
-#else
                                     const at_s2 cg = padd32(G1, colc[k][tq]);
-#endif
                                     const at_s2 cx = DEF ? X1 : padd32(X1, colx[DEF ? 0 : k][tq]);  // drift: + ie - dz = 0
                                     const at_s2 Xn1 = pmax(cg, cx);
                                     const at_s2 cf = padd32(F1, oy1i), cy = DEF ? Y : padd32(Y, eyi);
@@ -1036,10 +1022,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         }
     };
     if (walker) chain_loop(std::true_type{});
-    else {
-        if (A2_FILL_PRIO >= 0) __builtin_amdgcn_s_setprio(A2_FILL_PRIO < 0 ? 0 : A2_FILL_PRIO);
-        chain_loop(std::false_type{});
-    }
+    else chain_loop(std::false_type{});
 }
 
 // The band pass (every pair of the launch, trace strip of half-width `band`; 0 = full trace) ...
