@@ -440,11 +440,22 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
 #ifndef A2_OCC
 #define A2_OCC 6
 #endif
+#ifndef A2_K4W4
+#define A2_K4W4 0
+#endif
 const VariantT kAlignT2[] = {
     T2_VARIANTT2(4, 1, true, A2_OCC),  T2_VARIANTT2(8, 1, true, A2_OCC),
-    T2_VARIANTT2(6, 2, true, A2_OCC),  T2_VARIANTT2(8, 2, true, A2_OCC),
+    T2_VARIANTT2(6, 2, true, A2_OCC),
+#if A2_K4W4  // experiment: four fill waves of 4 columns per walker for 769-1 024 columns
+    T2_VARIANTT2(4, 4, true, 5),
+#endif
+    T2_VARIANTT2(8, 2, true, A2_OCC),
     T2_VARIANTT2(4, 1, false, A2_OCC), T2_VARIANTT2(8, 1, false, A2_OCC),
-    T2_VARIANTT2(6, 2, false, A2_OCC), T2_VARIANTT2(8, 2, false, A2_OCC),
+    T2_VARIANTT2(6, 2, false, A2_OCC),
+#if A2_K4W4
+    T2_VARIANTT2(4, 4, false, 5),
+#endif
+    T2_VARIANTT2(8, 2, false, A2_OCC),
     // 1 025 - 2 048 columns: four fill waves + the walker (5 waves per workgroup)
     T2_VARIANTT2(6, 4, true, 5), T2_VARIANTT2(8, 4, true, 5), T2_VARIANTT2(6, 4, false, 5), T2_VARIANTT2(8, 4, false, 5),
 };
