@@ -76,6 +76,20 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 #ifndef A2_SKIP_OUT_OF_BAND
 #define A2_SKIP_OUT_OF_BAND 0
 #endif
+// The same skip for the sign-digit trace (non-default scores, the 4-fill-wave shapes, the queued
+// pass): it keeps round 2's measured default there (2.73e6 vs 2.47e6 pairs/s on (8, 2))
+#ifndef A2_SKIP_SIGN
+#define A2_SKIP_SIGN 1
+#endif
+// Raw-difference trace (default scores) up to this many fill waves.  The 4-fill-wave shapes (1 025 -
+// 2 048 columns) keep the 2-byte sign-digit trace: on them the 4-byte raw trace measured 8 % slower
+// (1 200 / 1 500 / 2 000 bp: 8.1e5 / 6.5e5 / 4.7e5 vs 8.8e5 / 7.1e5 / 5.05e5 pairs/s,
+// profiles/r3/long_*.json)
+#ifndef A2_RAW_MAX_W
+#define A2_RAW_MAX_W 2
+#endif
+template <int W, bool DEF>
+constexpr bool a2_raw() { return DEF && W <= A2_RAW_MAX_W; }
 // 1: the per-column substitution words come from ds_read_u16_d16 / _d16_hi pairs (LDS assembles
 // the (stream 0, stream 1) halves) instead of two ds_read_b128 and a v_perm per column
 #ifndef A2_D16_SUB
@@ -934,7 +948,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     d1 = nd1;
                                 }
                                 };
-                                if (A2_SKIP_OUT_OF_BAND && !bmask) {
+                                if ((RAW ? A2_SKIP_OUT_OF_BAND : A2_SKIP_SIGN) && !bmask) {
                                     cells(std::false_type{});
                                 } else {
                                 cells(std::true_type{});
@@ -1032,7 +1046,7 @@ k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int c
           double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
           int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
           unsigned long long* __restrict__ esc_n, StrOut so) {
-    alignt2_body<K, W, DEF, DEF>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
+    alignt2_body<K, W, DEF, a2_raw<W, DEF>()>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
                                  hops, next, band, esc_list, esc_n, so);
 }
 // ... and the full-trace pass over the pairs it queued (ps.sel / ps.dcount): a kernel of its own

@@ -440,22 +440,11 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
 #ifndef A2_OCC
 #define A2_OCC 6
 #endif
-#ifndef A2_K4W4
-#define A2_K4W4 0
-#endif
 const VariantT kAlignT2[] = {
     T2_VARIANTT2(4, 1, true, A2_OCC),  T2_VARIANTT2(8, 1, true, A2_OCC),
-    T2_VARIANTT2(6, 2, true, A2_OCC),
-#if A2_K4W4  // experiment: four fill waves of 4 columns per walker for 769-1 024 columns
-    T2_VARIANTT2(4, 4, true, 5),
-#endif
-    T2_VARIANTT2(8, 2, true, A2_OCC),
+    T2_VARIANTT2(6, 2, true, A2_OCC),  T2_VARIANTT2(8, 2, true, A2_OCC),
     T2_VARIANTT2(4, 1, false, A2_OCC), T2_VARIANTT2(8, 1, false, A2_OCC),
-    T2_VARIANTT2(6, 2, false, A2_OCC),
-#if A2_K4W4
-    T2_VARIANTT2(4, 4, false, 5),
-#endif
-    T2_VARIANTT2(8, 2, false, A2_OCC),
+    T2_VARIANTT2(6, 2, false, A2_OCC), T2_VARIANTT2(8, 2, false, A2_OCC),
     // 1 025 - 2 048 columns: four fill waves + the walker (5 waves per workgroup)
     T2_VARIANTT2(6, 4, true, 5), T2_VARIANTT2(8, 4, true, 5), T2_VARIANTT2(6, 4, false, 5), T2_VARIANTT2(8, 4, false, 5),
 };
@@ -485,7 +474,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     // two trace buffers per resident workgroup: shrink the chunk (hence the chain rows) until they
     // fit the budget (TAXI2_AT_TRACE_GB, default 40 GB of the 288 GB HBM; 80 GB for the packed
     // default-score kernel, whose raw-difference trace takes 4 bytes per lane-column and step)
-    const bool raw = packed && v.def;  // alignt2_kernel.hpp: raw-difference trace in the band pass
+    const bool raw = packed && v.def && v.W <= A2_RAW_MAX_W;  // alignt2_kernel.hpp a2_raw: raw-difference trace
     double budget_gb = raw ? 80.0 : 40.0;
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     auto buf_bytes = [&](int64_t e) {
