@@ -800,6 +800,8 @@ class VersusAll:
         n, M = len(seqs), len(labels)
         cuda = stream.device
         store_dev = store.device
+        times = dict(compute_s=0.0, assemble_s=0.0, reduce_text_s=0.0)
+        t_c = perf_counter()
         try:
             # ---- 1. this rank's triangle rows
             # packed 16-bit counters (TAXI2_METRIC_COUNTS) up to 32 767 bp; past that, one f64 plane
@@ -827,6 +829,7 @@ class VersusAll:
                     npl[c0 : c0 + c] = torch.from_numpy(eng.ncd_pairs(st, st, a, b, scores, aligned=align, both=True))
                 report(self.progress_handler, "distance.x.id", min(total, 2 * M * (k + c) * world), total)
             torch.cuda.synchronize(cuda)
+            times["compute_s"] = perf_counter() - t_c
             # ---- 2. diagonal rule inputs (rank 0): identical full tuples -> None, unless the
             # alignment of the sequence with itself is not the identity (non-default scores)
             sink = _BlockWriters(self, seqs, eng) if rank == 0 else None
@@ -835,11 +838,17 @@ class VersusAll:
             # ---- 3. row blocks, x-major
             per_entry = 8 * (len(store.planes) + M)
             B = block_rows(n, per_entry, int(self.params.engine.block_bytes))
+            timed = bool(self.params.engine.timings)
             for x0 in range(0, n, B):
                 x1 = min(n, x0 + B)
+                t_a = perf_counter()
                 blk = store.assemble(x0, x1)
+                if timed:
+                    torch.cuda.synchronize(cuda)
+                    times["assemble_s"] += perf_counter() - t_a
                 if sink is None:
                     continue
+                t_r = perf_counter()
                 D = torch.empty((x1 - x0, n, M), dtype=torch.float64, device=cuda)
                 scale = 100.0 if self.params.format.percentage_multiply else 1.0
                 if cidx and "counts" not in blk:  # wide: the metric planes themselves
@@ -858,9 +867,13 @@ class VersusAll:
                         D[:, :, kk] = nv * scale if scale != 1.0 else nv
                 sink.consume(x0, x1, D, scale)
                 del D
+                if timed:
+                    torch.cuda.synchronize(cuda)
+                    times["reduce_text_s"] += perf_counter() - t_r
                 report(self.progress_handler, "distance.x.id", min(total, M * n * x1), total)
             if sink is not None:
                 sink.close()
+            self.timings = times
         finally:
             st.free()
 
