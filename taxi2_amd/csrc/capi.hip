@@ -440,11 +440,16 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
 #ifndef A2_OCC
 #define A2_OCC 6
 #endif
+// The same for other scores (the sign-digit trace + per-column extend constants): asked for 6 waves,
+// the compiler gave up at 144 VGPRs (3 waves per SIMD); 4 fits in 128 VGPRs with its spills in cold code
+#ifndef A2_OCC_GEN
+#define A2_OCC_GEN 4
+#endif
 const VariantT kAlignT2[] = {
     T2_VARIANTT2(4, 1, true, A2_OCC),  T2_VARIANTT2(8, 1, true, A2_OCC),
     T2_VARIANTT2(6, 2, true, A2_OCC),  T2_VARIANTT2(8, 2, true, A2_OCC),
-    T2_VARIANTT2(4, 1, false, A2_OCC), T2_VARIANTT2(8, 1, false, A2_OCC),
-    T2_VARIANTT2(6, 2, false, A2_OCC), T2_VARIANTT2(8, 2, false, A2_OCC),
+    T2_VARIANTT2(4, 1, false, A2_OCC_GEN), T2_VARIANTT2(8, 1, false, A2_OCC_GEN),
+    T2_VARIANTT2(6, 2, false, A2_OCC_GEN), T2_VARIANTT2(8, 2, false, A2_OCC_GEN),
     // 1 025 - 2 048 columns: four fill waves + the walker (5 waves per workgroup)
     T2_VARIANTT2(6, 4, true, 5), T2_VARIANTT2(8, 4, true, 5), T2_VARIANTT2(6, 4, false, 5), T2_VARIANTT2(8, 4, false, 5),
 };
