@@ -182,10 +182,12 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
  * returns for (b, a) written in (a, b) column order (d_sx holds a's aligned string, d_sy b's), each
  * right-aligned at byte len(a) + len(b) of its cap-byte slot, lengths d_slen[k*2 + o].  Replaces
  * versus_all.py:746-750's two alignments of a pair (one per ordered pair) by one fill.  Same
- * shape limits as taxi2_rect_strings_dev. */
+ * shape limits as taxi2_rect_strings_dev.  reserve_cus: the persistent aligner grid leaves that many
+ * CUs' worth of workgroups unlaunched, so work the caller queues on another stream (the previous
+ * block's text) finds room to run beside it; 0 = the whole GPU. */
 int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
                           const int32_t* metrics, int nmetrics, double* d_out, int32_t cap, uint8_t* d_sx,
-                          uint8_t* d_sy, int32_t* d_slen, void* stream);
+                          uint8_t* d_sy, int32_t* d_slen, int reserve_cus, void* stream);
 
 /* aligned_pairs.txt text (pairs.py:51-97 SequencePairHandler.Formatted) of the rectangle rows
  * [q0, q1) x every r from taxi2_rect_strings_dev slots (device): per pair "idx / idy" LF, the
@@ -219,6 +221,18 @@ int taxi2_format_pairs_ptr_dev(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, con
  * (deflate_len.hpp); bytes are compressed as given (the Python layer hands UTF-8). */
 int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,
                     int64_t count, const taxi2_scores* sc, int both, double* out);
+
+/* Asynchronous form of taxi2_format_pairs_ptr_dev for pipelines: every input is a device array
+ * (ids as concatenated bytes with offsets relative to those bytes), the text goes to the device
+ * buffer d_text, and d_total[0] = its length, d_total[1] = 1 if it fit text_cap (else nothing is
+ * written: call again with a larger buffer); d_scratch: 2 nrows int64 of device scratch.  Nothing
+ * synchronises the host or the device: the caller copies d_text[0, d_total[0]) out when the stream
+ * reaches it. */
+int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, const uint64_t* d_px,
+                                 const uint64_t* d_py, const int32_t* d_slen, const uint8_t* d_row_ids,
+                                 const int64_t* d_row_offs, const uint8_t* d_col_ids, const int64_t* d_col_offs,
+                                 int first, uint8_t* d_text, int64_t text_cap, int64_t* d_total,
+                                 int64_t* d_scratch, void* stream);
 
 /* ---- compressed length (alfpy ncd.complexity) --------------------------------------------- *
  * out[k] = len(zlib.compress(upper(x[xs[k]]) + upper(y[ys[k]]))), zlib 1.2.11 level 6;

@@ -42,6 +42,7 @@ EXPORTS = (
     "taxi2_rect_strings_dev",
     "taxi2_tri_strings_dev",
     "taxi2_format_pairs_ptr_dev",
+    "taxi2_format_pairs_ptr_async",
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
@@ -106,7 +107,9 @@ _SIGNATURES = {
     "taxi2_format_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
                                       ctypes.POINTER(_I64), _P]),
     "taxi2_tri_strings_dev": (_INT, [_P, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _I32, _P, _P, _P,
-                                     _P]),
+                                     _INT, _P]),
+    "taxi2_format_pairs_ptr_async": (_INT, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64, _P, _P,
+                                            _P]),
     "taxi2_format_pairs_ptr_dev": (_INT, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
                                           ctypes.POINTER(_I64), _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
@@ -433,7 +436,7 @@ class Engine:
             )
 
     def tri_strings_dev(self, s: SeqSet, k0: int, count: int, metrics, out_ptr: int | None, cap: int, sx_ptr: int,
-                        sy_ptr: int, slen_ptr: int, scores=None, stream: int | None = None) -> None:
+                        sy_ptr: int, slen_ptr: int, scores=None, stream: int | None = None, reserve_cus: int = 0) -> None:
         """Metrics ([count][2][M], may be empty) and BOTH orientations' aligned strings of the
         triangle pairs [k0, k0 + count), one fill per pair (device slots [k][2][cap]; see
         taxi2_tri_strings_dev)."""
@@ -444,9 +447,27 @@ class Engine:
                 self._lib.taxi2_tri_strings_dev(
                     self._ctx, s.id, int(k0), int(count), ctypes.byref(cs), codes.ctypes.data if len(codes) else None,
                     len(codes), ctypes.c_void_p(out_ptr) if out_ptr else None, int(cap), ctypes.c_void_p(sx_ptr),
-                    ctypes.c_void_p(sy_ptr), ctypes.c_void_p(slen_ptr), ctypes.c_void_p(stream) if stream else None,
+                    ctypes.c_void_p(sy_ptr), ctypes.c_void_p(slen_ptr), int(reserve_cus),
+                    ctypes.c_void_p(stream) if stream else None,
                 ),
                 "taxi2_tri_strings_dev",
+            )
+
+    def format_pairs_ptr_async(self, nrows: int, ncols: int, px_ptr: int, py_ptr: int, slen_ptr: int, rid_ptr: int,
+                               roffs_ptr: int, cid_ptr: int, coffs_ptr: int, *, first: bool, text_ptr: int, cap: int,
+                               total_ptr: int, scratch_ptr: int, stream: int) -> None:
+        """Queue the aligned_pairs.txt text of an nrows x ncols block on ``stream``, every argument
+        a device pointer (taxi2_format_pairs_ptr_async): text into ``text_ptr`` (``cap`` bytes),
+        total_ptr[0] = its length, total_ptr[1] = 1 if it fit.  No host synchronisation."""
+        with self._lock:
+            self._check(
+                self._lib.taxi2_format_pairs_ptr_async(
+                    self._ctx, int(nrows), int(ncols), ctypes.c_void_p(px_ptr), ctypes.c_void_p(py_ptr),
+                    ctypes.c_void_p(slen_ptr), ctypes.c_void_p(rid_ptr), ctypes.c_void_p(roffs_ptr),
+                    ctypes.c_void_p(cid_ptr), ctypes.c_void_p(coffs_ptr), 1 if first else 0,
+                    ctypes.c_void_p(text_ptr), int(cap), ctypes.c_void_p(total_ptr), ctypes.c_void_p(scratch_ptr),
+                    ctypes.c_void_p(stream)),
+                "taxi2_format_pairs_ptr_async",
             )
 
     def format_pairs_ptr_dev(self, nrows: int, ncols: int, px_ptr: int, py_ptr: int, slen_ptr: int, row_ids, col_ids,
@@ -502,6 +523,15 @@ class Engine:
             self._pairs_buf = buf
             return memoryview(buf[: need.value])
         raise NativeError("taxi2_format_pairs_dev: output buffer sizing failed")
+
+    def _pinned_view(self, nbytes: int) -> np.ndarray:
+        """The first ``nbytes`` of the engine's pinned text buffer (grown as needed; valid until the
+        next text call)."""
+        buf = getattr(self, "_pairs_buf", None)
+        if buf is None or buf.size < nbytes:
+            self._pairs_buf = None
+            buf = self._pairs_buf = self._pinned(max(int(nbytes), 1 << 20))
+        return buf[: int(nbytes)]
 
     def _pinned(self, nbytes: int) -> np.ndarray:
         """A page-locked host buffer (the D2H of a block's text runs at full PCIe rate into it, no

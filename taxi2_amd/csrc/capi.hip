@@ -52,6 +52,7 @@ struct DevSet {
 struct taxi2_ctx {
     int device = 0;
     int num_cus = 0;
+    int reserve_cus = 0;  // packed aligner launches leave this many CUs' worth of workgroups free
     hipStream_t stream = nullptr;
     std::string err;
     std::vector<DevSet> sets;
@@ -465,10 +466,13 @@ const VariantT* pick_variantt2(const KScores& k, int max_len) {
 int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
                         hipStream_t st, int max_len, bool packed, StrOut str = StrOut{}) {
-    // resident workgroups of the kernel (VGPR and LDS limits), persistent grid
+    // resident workgroups of the kernel (VGPR and LDS limits), persistent grid; a caller overlapping
+    // other work with this launch leaves ctx->reserve_cus CUs' worth of workgroups unlaunched
     int per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 64 * (v.W + 1), 0));
-    const int64_t resident = (int64_t)ctx->num_cus * std::max(1, per_cu);
+    const int64_t resident =
+        (int64_t)std::max(1, ctx->num_cus - std::max(0, std::min(ctx->reserve_cus, ctx->num_cus - 1))) *
+        std::max(1, per_cu);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ps.count, resident));
     // chunk (pairs per cursor step): TAXI2_AT_CHUNK forces 1..AT_CHUNK, else the kernel's automatic
     // rule (at least ~8 chunks per workgroup); it bounds the rows of a chain, hence the buffers
@@ -1223,7 +1227,7 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
 
 int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
                           const int32_t* metrics, int nmetrics, double* d_out, int32_t cap, uint8_t* d_sx,
-                          uint8_t* d_sy, int32_t* d_slen, void* stream) {
+                          uint8_t* d_sy, int32_t* d_slen, int reserve_cus, void* stream) {
     if (!ctx) return -1;
     DevSet* S = get_set(ctx, set);
     if (!S) return fail(ctx, "unknown set");
@@ -1237,8 +1241,10 @@ int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, co
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     PairSrc ps{PAIRS_TRI, k0, count, S->n, 0, nullptr, nullptr};
+    ctx->reserve_cus = std::max(0, reserve_cus);
     const int rc = launch_packed_strings(ctx, *S, *S, ps, sc, ms, OUT_BOTH, d_out, nullptr, st,
                                          StrOut{d_sx, d_sy, d_slen, cap, 2});
+    ctx->reserve_cus = 0;
     if (rc > 0) return fail(ctx, "walker strings need the packed aligner (Gotoh scores within int16, <= 2 048 bp)");
     return rc;
 }
@@ -1765,6 +1771,41 @@ int taxi2_format_pairs_ptr_dev(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, con
     PairFmtArgs a{nullptr, nullptr, d_slen, 0, nullptr, nullptr, ncols, nullptr, nullptr, nullptr, nullptr,
                   first ? 1 : 0, d_px, d_py};
     return format_pairs_impl(ctx, nrows, ncols, a, row_ids, row_offs, col_ids, col_offs, out, out_cap, out_len, st);
+}
+
+int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, const uint64_t* d_px,
+                                 const uint64_t* d_py, const int32_t* d_slen, const uint8_t* d_row_ids,
+                                 const int64_t* d_row_offs, const uint8_t* d_col_ids, const int64_t* d_col_offs,
+                                 int first, uint8_t* d_text, int64_t text_cap, int64_t* d_total,
+                                 int64_t* d_scratch, void* stream) {
+    if (!ctx) return -1;
+    if (nrows < 0 || ncols < 0) return fail(ctx, "negative size");
+    if (!d_total || !d_scratch) return fail(ctx, "null total / scratch");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    if (nrows == 0 || ncols == 0) {
+        HIP_TRY(ctx, hipMemsetAsync(d_total, 0, 8, st));
+        return 0;
+    }
+    if (!d_px || !d_py || !d_slen || !d_row_ids || !d_row_offs || !d_col_ids || !d_col_offs || !d_text)
+        return fail(ctx, "null device argument");
+    // row lengths and bases in the caller's scratch (2 nrows int64: no context buffer that could be
+    // regrown -- hipFree synchronises the whole device -- while another stream runs); ids and
+    // offsets are device arrays the caller keeps: row offsets relative to d_row_ids, column
+    // offsets to d_col_ids
+    int64_t* d_rlen = d_scratch;
+    int64_t* d_rbase = d_rlen + nrows;
+    PairFmtArgs a{nullptr, nullptr, d_slen, 0, nullptr, nullptr, ncols, d_row_ids, d_row_offs, d_col_ids, d_col_offs,
+                  first ? 1 : 0, d_px, d_py};
+    hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rlen);
+    HIP_TRY(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_pairs_row_base, dim3(1), dim3(FMT_BLOCK), 0, st, (const int64_t*)d_rlen, nrows, text_cap,
+                       d_rbase, d_total);
+    HIP_TRY(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, (const int64_t*)d_rbase,
+                       (char*)d_text, (const int64_t*)d_total);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
 }
 
 int taxi2_format_rows(taxi2_ctx* ctx, int mode, const double* vals, int64_t nrows, int64_t ncols, int nm,

@@ -285,11 +285,41 @@ __global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_len(PairFmtArgs a, int6
     if (threadIdx.x == 0) row_len[r] = red[0];
 }
 
+// Asynchronous form: exclusive prefix of the row lengths on the device (one workgroup; rows in
+// chunks of FMT_BLOCK), total in *total; cap_ok = total <= cap (else k_pairs_text writes nothing).
+__global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_base(const int64_t* __restrict__ row_len, int64_t nrows,
+                                                              int64_t cap, int64_t* __restrict__ row_base,
+                                                              int64_t* __restrict__ total) {
+    __shared__ int64_t scan[FMT_BLOCK];
+    int64_t run = 0;
+    for (int64_t r0 = 0; r0 < nrows; r0 += FMT_BLOCK) {
+        const int64_t r = r0 + threadIdx.x;
+        const int64_t v = r < nrows ? row_len[r] : 0;
+        scan[threadIdx.x] = v;
+        __syncthreads();
+        for (int w = 1; w < FMT_BLOCK; w <<= 1) {
+            const int64_t add = threadIdx.x >= w ? scan[threadIdx.x - w] : 0;
+            __syncthreads();
+            scan[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (r < nrows) row_base[r] = run + scan[threadIdx.x] - v;
+        run += scan[FMT_BLOCK - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        total[0] = run;
+        total[1] = run <= cap ? 1 : 0;
+    }
+}
+
 // Pass 2: one workgroup per row; the pair offsets of 256 columns at a time by an LDS scan, then
 // each wave writes whole pairs, its lanes striding over the pair's bytes (coalesced stores).
 __global__ void __launch_bounds__(FMT_BLOCK)
-k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out) {
+k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out,
+             const int64_t* __restrict__ cap_ok = nullptr) {
     __shared__ int64_t scan[FMT_BLOCK];
+    if (cap_ok && cap_ok[1] == 0) return;  // asynchronous form: the text would not fit the buffer
     const int64_t r = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int64_t base = row_base[r];
