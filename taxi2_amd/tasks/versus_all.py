@@ -232,7 +232,8 @@ class VersusAll:
 
             walked = False
             if pairs_fh is not None and cidx:
-                walked = (self._tri_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh)
+                tri = self._tri_with_pairs_seq if os.environ.get("TAXI2_PAIRS_SEQ") else self._tri_with_pairs
+                walked = (tri(seqs, eng, st, D, cidx, clabels, scores, pairs_fh)
                           or self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh))
             if walked:  # counter metrics and aligned_pairs.txt done; NCD (if any) from the triangle
                 if nidx:
@@ -469,6 +470,136 @@ class VersusAll:
             sc_.synchronize()
             state["kept"].clear()
         return True
+
+    def _tri_with_pairs_seq(self, seqs, eng, st, D, cidx, clabels, scores, fh) -> bool:
+        """Round-3 sequential form of _tri_with_pairs (one stream, text after each block's
+        alignment), kept for A/B against the two-stream pipeline (TAXI2_PAIRS_SEQ=1)."""
+        import torch
+
+        from .._native import NativeError, pack_strings
+
+        n = len(seqs)
+        lens_h = np.array([len(s.seq) for s in seqs], dtype=np.int64)
+        if os.environ.get("TAXI2_PAIRS_RECT") or n < 2:
+            return False
+        keep_limit = int(self.params.engine.keep_bytes)
+        kept_bytes = 0
+        dev = torch.device("cuda", eng.device)
+        cap = 2 * int(lens_h.max()) + 1
+        Mc = len(cidx)
+        npairs = n * (n - 1) // 2
+        ids = pack_strings([s.id for s in seqs])
+        total = len(self.params.distances.metrics) * n * n
+        launch = int(self.params.engine.launch_pairs or 0)
+        slot_budget = max(int(self.params.engine.block_bytes), WALK_BLOCK_BYTES if launch else 0)
+        per_pair = 4 * cap + 16 * Mc + 8
+        target = max(1, min(launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
+        stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(stream):
+            lens = torch.as_tensor(lens_h, device=dev)
+            # self alignments (x, x) for the diagonal pairs' text
+            strings = eng.align_strings(st, st, np.arange(n), np.arange(n), scores)
+            sa = [a.encode("latin-1") for a, _ in strings]
+            sb = [b.encode("latin-1") for _, b in strings]
+            slen_self = torch.as_tensor(np.array([len(a) for a in sa], dtype=np.int32), device=dev)
+            soff = np.zeros(n, dtype=np.int64)
+            soff[1:] = np.cumsum([len(a) for a in sa])[:-1]
+            self_x = torch.as_tensor(np.frombuffer(b"".join(sa) + b"\0", dtype=np.uint8).copy(), device=dev)
+            self_y = torch.as_tensor(np.frombuffer(b"".join(sb) + b"\0", dtype=np.uint8).copy(), device=dev)
+            soff_d = torch.as_tensor(soff, device=dev)
+            px_self = self_x.data_ptr() + soff_d
+            py_self = self_y.data_ptr() + soff_d
+            # (b, a) strings of every pair, kept until row b: pointers per triangle pair
+            kpx = torch.zeros(npairs, dtype=torch.int64, device=dev)
+            kpy = torch.zeros(npairs, dtype=torch.int64, device=dev)
+            klen = torch.zeros(npairs, dtype=torch.int32, device=dev)
+            kept = []
+            ar = torch.arange(cap, device=dev)
+            x0 = 0
+            while x0 < n:
+                # rows [x0, x1): about `target` triangle pairs, at most 2 * target ordered pairs of text
+                x1, cnt = x0, 0
+                while x1 < n and (x1 == x0 or (cnt + (n - 1 - x1) <= target and (x1 + 1 - x0) * n <= 2 * target)):
+                    cnt += n - 1 - x1
+                    x1 += 1
+                k0 = x0 * (2 * n - x0 - 1) // 2
+                blk = None
+                if cnt:
+                    d = torch.empty((cnt, 2, Mc), dtype=torch.float64, device=dev)
+                    sx = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
+                    sy = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
+                    sl = torch.empty((cnt, 2), dtype=torch.int32, device=dev)
+                    try:
+                        eng.tri_strings_dev(st, k0, cnt, clabels, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
+                                            sl.data_ptr(), scores, stream.cuda_stream)
+                    except NativeError as e:
+                        if x0 == 0 and "walker strings need" in str(e):
+                            return False
+                        raise
+                    # pair (a, b) of the block: a in [x0, x1), b > a
+                    ra = torch.repeat_interleave(torch.arange(x0, x1, device=dev), n - 1 - torch.arange(x0, x1, device=dev))
+                    first = torch.cumsum(n - 1 - torch.arange(x0, x1, device=dev), 0) - (n - 1 - torch.arange(x0, x1, device=dev))
+                    rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(first, n - 1 - torch.arange(x0, x1, device=dev))
+                    end = (lens[ra] + lens[rb]).to(torch.int64)
+                    # keep the (b, a) orientation compacted (mask of each slot's right-aligned bytes)
+                    L1 = sl[:, 1].to(torch.int64)
+                    m1 = (ar[None, :] >= (end - L1)[:, None]) & (ar[None, :] < end[:, None])
+                    kx, ky = sx[:, 1, :][m1], sy[:, 1, :][m1]
+                    off = torch.cumsum(L1, 0) - L1
+                    kpx[k0:k0 + cnt] = kx.data_ptr() + off
+                    kpy[k0:k0 + cnt] = ky.data_ptr() + off
+                    klen[k0:k0 + cnt] = sl[:, 1]
+                    kept.append((kx, ky))
+                    kept_bytes += 2 * kx.numel()
+                    del m1
+                    blk = (sx, sy, sl, end, d, ra, rb)
+                    dd = d.cpu().numpy()
+                    a_h, b_h = ra.cpu().numpy(), rb.cpu().numpy()
+                    for q, kk in enumerate(cidx):
+                        D[a_h, b_h, kk] = dd[:, 0, q]
+                        D[b_h, a_h, kk] = dd[:, 1, q]
+                # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
+                # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
+                # and (x, x) from the self alignments
+                xs_ = torch.arange(x0, x1, device=dev)[:, None]
+                ys_ = torch.arange(n, device=dev)[None, :]
+                up = ys_ > xs_
+                lo = ys_ < xs_
+                pu = xs_ * (2 * n - xs_ - 1) // 2 + (ys_ - xs_ - 1)   # pair (x, y) for y > x
+                pl = ys_ * (2 * n - ys_ - 1) // 2 + (xs_ - ys_ - 1)   # pair (y, x) for y < x
+                px = torch.where(lo, kpy[pl.clamp(0, npairs - 1)], px_self[xs_.expand(-1, n)])
+                py = torch.where(lo, kpx[pl.clamp(0, npairs - 1)], py_self[xs_.expand(-1, n)])
+                ln = torch.where(lo, klen[pl.clamp(0, npairs - 1)], slen_self[xs_.expand(-1, n)])
+                if blk is not None:
+                    sx, sy, sl, end, _, _, _ = blk
+                    q = (pu - k0).clamp(0, max(0, cnt - 1))
+                    L0 = sl[:, 0].to(torch.int64)
+                    start0 = q * 2 * cap + end[q] - L0[q]
+                    px = torch.where(up, sx.data_ptr() + start0, px)
+                    py = torch.where(up, sy.data_ptr() + start0, py)
+                    ln = torch.where(up, sl[:, 0][q], ln)
+                px, py, ln = px.contiguous(), py.contiguous(), ln.to(torch.int32).contiguous()
+                stream.synchronize()  # the alignment kernel counts as compute, not text
+                t0 = perf_counter()
+                fh.write(eng.format_pairs_ptr_dev(x1 - x0, n, px.data_ptr(), py.data_ptr(), ln.data_ptr(),
+                                                  (ids[0], ids[1][x0:x1 + 1]), ids, first=x0 == 0,
+                                                  stream=stream.cuda_stream))
+                if isinstance(self.timings, dict):
+                    self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
+                del blk, px, py, ln
+                report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
+                       total)
+                x0 = x1
+                if x0 < n and kept_bytes > keep_limit:
+                    # the kept strings outgrew their budget: the remaining rows align every ordered
+                    # pair once (row blocks of the rect path), nothing kept
+                    stream.synchronize()
+                    del kept, kpx, kpy, klen
+                    return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
+            stream.synchronize()
+            del kept
+        return True
+
 
     def _rows_with_pairs(self, seqs, eng, st, D, cidx, clabels, scores, fh, x_start: int = 0) -> bool:
         """versus_all.py:746-750 as the reference runs it: each ORDERED pair aligned once, its aligned
