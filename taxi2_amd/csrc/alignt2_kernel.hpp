@@ -186,22 +186,20 @@ __device__ __forceinline__ uint32_t a2_load_trace32(const uint8_t* p) { return *
 
 // Raw-difference trace (default scores, the band pass).  Instead of forming sign digits per cell
 // (3 subtracts, 3 clamps and 3 multiply-adds per column pair: ~45 % of the fill's issue cycles),
-// the fill stores two exact differences of the cell's own states per pair,
-//   D = Gn - Xn1   (G = max(M, Iy) tagged, Ix odd)   and   E = Fn1 - Yn   (F = max(M, Ix) odd),
+// the fill stores two exact differences of the cell's own states per pair.  Since round 3 the fill
+// is the best-open form (alignt2_body, cells): plain scores, states M, Ix, Iy and their maximum B,
+// and the bytes are
+//   D1 = M - Ix   and   D2 = M - Iy
 // as int8: one 32-bit subtract each over both halves and one v_perm per column gather the four
-// bytes (D lo, D hi, E lo, E hi).  Between the states of one cell these differences are bounded by
-// the scores (default scores: D in [-18, 34], E in [-17, 35] over every cell of the CPU model,
-// tools/proto_rawdiff.c), so the int8 is exact.  The high half's bytes carry the low half's borrow
+// bytes (D1 lo, D1 hi, D2 lo, D2 hi).  Between the states of one cell these differences are bounded
+// by the scores (default scores: both in [-9, 17] over every cell of the CPU model,
+// tools/proto_bopen.c), so the int8 is exact.  The high half's bytes carry the low half's borrow
 // (the subtract is 32-bit): the walker adds back (lo byte < 0).
-// What the walker derives from the NEXT cell's (D, E):
-//   tag      = D even  (Gn odd iff M won; Xn1 odd)          -- parity survives any wrap
-//   class    = clamp(D, -2, 1) with tag, as the sign-digit code's sa
-//   Ix(i, j) formed from (i-1, j):  sign(cg - cx) = sign(D + (1 - tag) + colc_j)
-//   Iy(i, j) formed from (i, j-1):  sign(cf - cy) = sign(E + oy1_i)
-// (colc_j = ox_j - dz, oy1_i = oy_i - dz - 1 as in the fill).  The walker also sums the score of
-// its moves; a walk whose sum differs from the fill's optimum (impossible while the differences
-// fit int8: any wrong decision leaves the optimal path strictly) queues its pair for the
-// sign-digit full-trace pass, like a walk that leaves the band.
+// From (D1, D2) of a cell the walker has all three state values relative to each other, so it
+// decides the first path's ties exactly (walk_run).  The walker also sums the score of its moves; a
+// walk whose sum differs from the fill's optimum (impossible while the differences fit int8: any
+// wrong decision leaves the optimal path strictly) queues its pair for the sign-digit full-trace
+// pass, like a walk that leaves the band.
 __device__ __forceinline__ void a2_raw_de(uint32_t w, int sm, int& d, int& e) {
     if (sm == 0) {
         d = (int)(int8_t)(uint8_t)w;
@@ -308,7 +306,9 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
     constexpr int XR = a1c_xr(W);
     constexpr int KW = K / 2;
     const KScores sc0 = DEF ? KScores{1, -1, -8, -1, -1, -1} : scin;  // align.py:20-27 defaults
-    const KScores sc = doubled(sc0);
+    // RAW (best-open fill, below): plain scores; otherwise doubled scores with tie tags in bit 0
+    const KScores sc = RAW ? sc0 : doubled(sc0);
+    constexpr uint32_t ODD = RAW ? 0u : 0x00010001u;  // Ix / F kept odd (tagged forms only)
     // Drift (default scores, where every gap extend is ie): cells store V(i, j) - (i + j) dz, so
     // Ix(i, j) = max(G(i-1, j) + o, Ix(i-1, j) + e) becomes max(G + (o - dz), Ix) and likewise for
     // Iy: both extend additions vanish; M absorbs -2 dz in its substitution table.
@@ -445,7 +445,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 if (ni == 0 && nj == 0) {  // the gap run (if any) opened at the start: end-gap open
                     if (st != AT_M) sc2 += sc.eo;
                     // the walked score must be the fill's optimum, else a decision was wrong
-                    if (sc2 != ((fin[pb][pi] + (nA_ + nB_) * dz) & ~1)) {
+                    if (sc2 != fin[pb][pi] + (nA_ + nB_) * dz) {  // best-open form: plain scores
                         st = AT_ESC;
                         continue;
                     }
@@ -461,7 +461,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 for (int m = 0; m < nm; ++m)
                     o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
                 if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK && fin[pb][pi] != (int)AT_POISON_LDS, AG_FIN))  // undo the drift of cell (nA, nB)
-                    sout[p] = (fin[pb][pi] + (cp.nA + chs[pb].nB) * dz) >> 1;
+                    sout[p] = RAW ? fin[pb][pi] + (cp.nA + chs[pb].nB) * dz : (fin[pb][pi] + (cp.nA + chs[pb].nB) * dz) >> 1;
                 if (so.slen) so.slen[p * so.nslot + ((prio ^ cp.swp) & (so.nslot - 1))] = ncol;
                 st = AT_DONE;
                 continue;
@@ -495,27 +495,32 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             xa = (ni >= 1 && AT_OK(ni - 1 < cp.nA, AG_ROWSEQ)) ? a2_load_byte(rs + ni - 1) : 0u;
             yb = (nj >= 1 && AT_OK(nj - 1 < ch.nB, AG_COLSEQ)) ? a2_load_byte(cs + nj - 1) : 0u;
             if constexpr (RAW) {
-                int dv, ev;
-                a2_raw_de(nb, sm, dv, ev);
-                const bool tg = !(dv & 1);  // Gn odd iff M won, Xn1 odd
-                const int sa = dv < -2 ? -2 : dv > 1 ? 1 : dv;
-                const bool clsM = sa == 0 || (sa == 1 && tg);
-                int nst;
-                if (ni == 0) {
-                    nst = AT_IY;
-                } else if (nj == 0) {
-                    nst = AT_IX;
-                } else if (st == AT_M) {  // best state of (ni, nj)
-                    nst = clsM ? AT_M : sa == 1 ? AT_IY : sa == -1 ? (prio ? AT_IY : AT_IX) : AT_IX;
-                } else if (st == AT_IX) {  // Ix(i, j) from (i-1, j): sign of (G | 1) + ox_j - X1 there
-                    const int sb = dv + (tg ? 0 : 1) + (j == nB_ ? sc.eo : sc.io) - dz;
-                    const bool gp = sb > 0 || (sb == 0 && (tg || prio));
-                    nst = gp ? (tg ? AT_M : AT_IY) : AT_IX;
-                } else {  // Iy(i, j) from (i, j-1): sign of F1 + oy1_i - Y there (tagF = class M, see below)
-                    const int scv = ev + (i == nA_ ? sc.eo : sc.io) - dz - 1;
-                    const bool fp = scv > 0 || (scv == 0 && (clsM || !prio));
-                    nst = fp ? (clsM ? AT_M : AT_IX) : AT_IY;
+                // best-open trace: D1 = M - X and D2 = M - Y of (ni, nj) give the three state values
+                // relative to each other; the candidates of the move into (i, j) are taken at (ni, nj)
+                // relative to the one that extends, and the first in priority order (A: M, Ix, Iy;
+                // B: M, Iy, Ix) among those at the maximum is the next state
+                int d1v, d2v;
+                a2_raw_de(nb, sm, d1v, d2v);
+                int vM, vX, vY;
+                if (st == AT_M) {  // best state of (ni, nj), relative to Ix
+                    vM = d1v;
+                    vX = 0;
+                    vY = d1v - d2v;
+                } else if (st == AT_IX) {  // Ix(i, j) from (i-1, j): M + co, Ix (extend), Iy + co
+                    const int co = (j == nB_ ? sc.eo : sc.io) - dz;
+                    vM = d1v + co;
+                    vX = 0;
+                    vY = d1v - d2v + co;
+                } else {  // Iy(i, j) from (i, j-1): M + oy, Ix + oy, Iy (extend)
+                    const int oy = (i == nA_ ? sc.eo : sc.io) - dz;
+                    vM = d2v + oy;
+                    vX = d2v - d1v + oy;
+                    vY = 0;
                 }
+                const int vm = max(vM, max(vX, vY));
+                int nst = vM == vm ? AT_M : prio ? (vY == vm ? AT_IY : AT_IX) : (vX == vm ? AT_IX : AT_IY);
+                if (ni == 0) nst = AT_IY;
+                else if (nj == 0) nst = AT_IX;
                 if (st == AT_IX) {  // gap moves: extend when the run continues, end scores on the edges
                     const bool en = j == nB_ || j == 0;
                     sc2 += nst == AT_IX ? (en ? sc.ee : sc.ie) : (en ? sc.eo : sc.io);
@@ -737,12 +742,13 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             for (int k = 0; k < K; ++k) {
                 const int g0 = sc.eo + sc.ee * (j0 + k - 1) - (j0 + k) * dz;
                 stG[k] = pk2b(g0, g0);
-                stX[k] = NEG16X2 | 0x00010001u;  // Ix kept odd
+                stX[k] = NEG16X2 | ODD;  // Ix kept odd (tagged forms)
             }
-            uint32_t payF = NEG16X2 | 0x00010001u, payY = NEG16X2;
+            uint32_t payF = NEG16X2 | ODD, payY = NEG16X2;
             // column-0 boundary of wave 0's lane 0 (row g = s): odd F = 2 Ix(i, 0) + 1 - i dz with
             // Ix(i, 0) = eo + ee (i - 1); default scores (ee = dz) make it one constant
-            const uint32_t bnd1 = pk2b(sc.eo - dz + 1, sc.eo - dz + 1);
+            // (best-open form: B(i, 0) = Ix(i, 0), plain)
+            const uint32_t bnd1 = pk2b(sc.eo - dz + (RAW ? 0 : 1), sc.eo - dz + (RAW ? 0 : 1));
             uint32_t bnd = bnd1;
             uint32_t carry = 0u;
             const uint2* ring_in = (w > 0 && !IS_W) ? ring + (size_t)(w - 1) * RING : nullptr;
@@ -800,10 +806,12 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     for (int k = 0; k < K; ++k) {
                                         const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
                                         stG[k] = (pk2b(g0, g0) & m) | (stG[k] & ~m);
-                                        stX[k] = ((NEG16X2 | 0x00010001u) & m) | (stX[k] & ~m);
+                                        stX[k] = ((NEG16X2 | ODD) & m) | (stX[k] & ~m);
                                     }
                                     // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
-                                    const int c0 = jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1) - jb * dz) | 1;
+                                    // (best-open form: B(0, jb), plain)
+                                    const int c0 = RAW ? (jb == 0 ? 0 : sc.eo + sc.ee * (jb - 1) - jb * dz)
+                                                       : jb == 0 ? 1 : (sc.eo + sc.ee * (jb - 1) - jb * dz) | 1;
                                     carry = (pk2b(c0, c0) & m) | (carry & ~m);
                                 }
                                 // substitution words of both rows
@@ -878,10 +886,10 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 }
 #endif
                                 // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
-                                // minus 1 because the F payload is kept odd (below)
+                                // minus 1 because the F payload is kept odd (below; not in the best-open form)
                                 const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
                                 const uint32_t oy1 = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
-                                                            (at_s2){(short)(sc.io - dz - 1), (short)(sc.io - dz - 1)});
+                                                            (at_s2){(short)(sc.io - dz - (RAW ? 0 : 1)), (short)(sc.io - dz - (RAW ? 0 : 1))});
                                 const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
                                                         : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
                                                                  (at_s2){(short)sc.ie, (short)sc.ie});
@@ -899,6 +907,46 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 // outside both streams' bands), so the trace codes are not formed at all --
                                 // the same cells, ~13 fewer VALU instructions per cell pair
                                 auto cells = [&](auto TR) {
+                                if constexpr (RAW) {
+                                    // Best-open form (default scores, raw-difference trace).  Opens are no
+                                    // cheaper than extends (co, oy <= 0 in drift units), so Ix may open from
+                                    // B = max(M, Ix, Iy) instead of max(M, Iy) (Ix + o <= Ix + e), Iy likewise,
+                                    // and the diagonal input of the next column is B itself: per cell
+                                    //   M = B(i-1, j-1) + s,  X = max(B_up + co_j, X_up),
+                                    //   Y = max(B_left + oy_i, Y_left),  B = max(max(M, X), Y)
+                                    // -- four maxima and no tag fix-ups.  The values of M, Ix and Iy are
+                                    // Biopython's, so the walker decides every tie of the first path from
+                                    // D1 = M - X and D2 = M - Y (stored as int8; [-9, 17] over every cell of
+                                    // the CPU model, tools/proto_bopen.c).  Registers: stG = B, stX = X of
+                                    // the previous row, F1 = B and Y of the left column, d1 = diagonal B.
+    #pragma unroll
+                                    for (int k = 0; k < K; ++k) {
+                                        const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
+                                        const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
+#if A2_D16_SUB
+                                        (void)sel;
+                                        const at_s2 sM = as_s2(sw[k]);
+#else
+                                        const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
+#endif
+                                        const at_s2 M = padd32(d1, as_u32(sM));
+                                        const at_s2 Xn = pmax(padd32(Bu, colc[k][tq]), Xu);
+                                        const at_s2 Yn = pmax(padd32(F1, oy1i), Y);
+                                        const at_s2 Bn = pmax(pmax(M, Xn), Yn);
+                                        if constexpr (decltype(TR)::value) {
+                                            // D1 = M - X, D2 = M - Y over both halves with 32-bit subtracts
+                                            // (the high half carries the low half's borrow: a2_raw_de)
+                                            const uint32_t dD = as_u32(M) - as_u32(Xn);
+                                            const uint32_t dE = as_u32(M) - as_u32(Yn);
+                                            acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
+                                        }
+                                        d1 = Bu;
+                                        stG[k] = as_u32(Bn);
+                                        stX[k] = as_u32(Xn);
+                                        F1 = Bn;
+                                        Y = Yn;
+                                    }
+                                } else {
     #pragma unroll
                                 for (int k = 0; k < K; ++k) {
                                     const at_s2 G = as_s2(stG[k]), X1 = as_s2(stX[k]);
@@ -947,6 +995,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     Y = Yn;
                                     d1 = nd1;
                                 }
+                                }
                                 };
                                 if ((RAW ? A2_SKIP_OUT_OF_BAND : A2_SKIP_SIGN) && !bmask) {
                                     cells(std::false_type{});
@@ -991,7 +1040,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         eG = (stG[k] & m) | (eG & ~m);
                                         eX = (stX[k] & m) | (eX & ~m);
                                     }
-                                    const at_s2 e = pmax(as_s2(eG), as_s2(eX));
+                                    const at_s2 e = RAW ? as_s2(eG) : pmax(as_s2(eG), as_s2(eX));  // best of (nA, nB)
                                     if (rw & (A2_LAST | (A2_LAST << 16))) AT_DIAG(3, 1);
                                     const uint32_t eu = as_u32(e);  // unbias the final cells
                                     if ((rw & A2_LAST) && AT_OK(2 * fin_n[0] < AT2_CHUNK, AG_FIN))
@@ -1000,7 +1049,9 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         fin[cur][2 * fin_n[1]++ + 1] = (int)(eu >> 16) - BIAS16;
                                 }
                             }
-                            carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;  // best of (i, j0 - 1), | 1
+                            // best of (i, j0 - 1) (| 1 in the tagged forms): the next row's diagonal
+                            if constexpr (RAW) carry = inF;
+                            else carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;
             };
 
             const int rmax = max(rows0, rows1);
