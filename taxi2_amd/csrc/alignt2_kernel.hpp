@@ -90,10 +90,23 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 #endif
 template <int W, bool DEF>
 constexpr bool a2_raw() { return DEF && W <= A2_RAW_MAX_W; }
-// 1: the per-column substitution words come from ds_read_u16_d16 / _d16_hi pairs (LDS assembles
-// the (stream 0, stream 1) halves) instead of two ds_read_b128 and a v_perm per column
-#ifndef A2_D16_SUB
-#define A2_D16_SUB 0
+// 1: in the best-open fill Iy opens from B of the left column too (the lane hand-off is then B, Iy);
+// 0: from F = max(M, Ix), Biopython's recurrence (hand-off F, Iy): a shorter left-to-right
+// dependency chain, but measured 4.02e6 vs 4.26e6 pairs/s on the same box (profiles/r3/ab_bopen_y)
+#ifndef A2_BOPEN_Y
+#define A2_BOPEN_Y 1
+#endif
+// 1: the best-open fill updates the Ix column state at the top of the step, while the row record
+// and the ring entry are in flight (it needs neither); measured 3 % slower (profiles/r3/ab_early_x)
+#ifndef A2_EARLY_X
+#define A2_EARLY_X 0
+#endif
+// 1: when column nB is the last slot of its lane (e.g. 1 000 bp with K = 8), the best-open fill adds
+// one uniform internal-open constant to columns 0..K-2 and reads only the last slot's constant from
+// LDS (K per-lane reads otherwise).  Measured: 4.11e6 vs 4.28e6 pairs/s in the cell loop, 4.25e6 vs
+// 4.16e6 on top of A2_EARLY_X (profiles/r3/ab_early_x, ab_uni_co): off
+#ifndef A2_UNI_CO
+#define A2_UNI_CO 0
 #endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
@@ -690,6 +703,11 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 break;
             }
             const int nB = chs[cur].nB;
+            // column nB's slot in its lane (chain-uniform) and the internal Ix open as one add constant
+            const int knb = __builtin_amdgcn_readfirstlane((nB - 1) % K);
+            const uint32_t coi = pk_int(pk2(sc.io - dz, sc.io - dz));
+            (void)knb;
+            (void)coi;
 #ifdef TAXI2_GUARD
             {  // poison the row ring, the wave ring and this chain's trace buffer (see AT_OK)
                 at_poison_lds(xinfo, sizeof xinfo);
@@ -759,7 +777,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             // One systolic step of a fill wave, specialised on the wave's role: FW = wave 0 (column-0
             // boundary from the row record, no ring read), HO = writes the ring to the next wave.  Per-step
             // uniform branches on w cost spilled SGPR masks (v_readlane) on every step.
-            auto step = [&](auto FW, auto HO, const int s) {
+            auto step = [&](auto FW, auto HO, auto UNI, const int s) {
                             // lane id recomputed (two v_mbcnt) rather than kept live across the chain
                             // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
                             int ln;
@@ -769,6 +787,31 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                             // across the loop (it was spilled and reloaded in the first-row path)
                             const int tq = w * 64 + ln;
                             const uint2 rec = xinfo[g & (XR - 1)];
+                            uint2 o_ring = make_uint2(0u, 0u);
+                            if constexpr (!decltype(FW)::value) o_ring = ring_in[(s + 1) & (RING - 1)];
+#if A2_EARLY_X
+                            if constexpr (RAW) {
+                                // best-open form: Ix(i, j) = max(B(i-1, j) + co_j, Ix(i-1, j)) needs no row
+                                // data, so the column updates run here while the row record and the ring
+                                // entry are in flight (in place: stX holds Ix of THIS row from now on; a
+                                // pair's first row sets it from the row-0 boundary itself, below)
+                                if constexpr (decltype(UNI)::value) {
+                                    // column nB is the lane's last (knb == K - 1, e.g. 1 000 bp with K = 8):
+                                    // columns 0..K-2 open with the internal score from one constant, the
+                                    // last from the per-lane LDS constant (the end-gap score on column nB)
+                                    const uint32_t cend = colc[K - 1][tq];
+    #pragma unroll
+                                    for (int k = 0; k < K - 1; ++k) stX[k] = as_u32(pmax(padd32(as_s2(stG[k]), coi), as_s2(stX[k])));
+                                    stX[K - 1] = as_u32(pmax(padd32(as_s2(stG[K - 1]), cend), as_s2(stX[K - 1])));
+                                } else {
+    #pragma unroll
+                                for (int k = 0; k < K; ++k) stX[k] = as_u32(pmax(padd32(as_s2(stG[k]), colc[k][tq]), as_s2(stX[k])));
+                                }
+                            }
+#endif
+                            uint32_t cend = 0u;
+                            if constexpr (RAW && decltype(UNI)::value && !A2_EARLY_X) cend = colc[K - 1][tq];
+                            (void)cend;
                             // trace band (a2_row_record): store iff (u16)(block - lo) <= hi - lo (covers
                             // j0 <= nB).  The lane mask is formed here, a whole cell block ahead of the
                             // store, so the exec-mask update there never waits on the compare.
@@ -786,7 +829,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 inF = shr_old(payF, bnd);
                                 inY = shr_old(payY, NEG16X2);
                             } else {
-                                const uint2 o = ring_in[(s + 1) & (RING - 1)];
+                                const uint2 o = o_ring;
                                 // lane 0 reads row s; rows past the chain's last are never read back
                                 (void)AT_OK(s >= max(rows0, rows1) || o.x != AT_POISON_LDS, AG_RING_POISON);
                                 inF = shr_old(payF, o.x);
@@ -806,7 +849,11 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     for (int k = 0; k < K; ++k) {
                                         const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
                                         stG[k] = (pk2b(g0, g0) & m) | (stG[k] & ~m);
-                                        stX[k] = ((NEG16X2 | ODD) & m) | (stX[k] & ~m);
+                                        // (early-X best-open form: stX already holds this row's Ix, which
+                                        // on a first row is B(0, j) + co_j)
+                                        const uint32_t x0 = (RAW && A2_EARLY_X) ? as_u32(padd32(as_s2(pk2b(g0, g0)), colc[k][tq]))
+                                                                                 : (NEG16X2 | ODD);
+                                        stX[k] = (x0 & m) | (stX[k] & ~m);
                                     }
                                     // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
                                     // (best-open form: B(0, jb), plain)
@@ -815,44 +862,6 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     carry = (pk2b(c0, c0) & m) | (carry & ~m);
                                 }
                                 // substitution words of both rows
-#if A2_D16_SUB
-                                // substitution words of both rows, one per column, assembled by the LDS
-                                // itself: ds_read_u16_d16 fills the low half (stream 0's row base),
-                                // ds_read_u16_d16_hi the high half (stream 1's) -- no v_perm per column
-                                uint32_t sw[K];
-                                {
-                                    const uint32_t a0 = (uint32_t)(uintptr_t)&eqt[(rw >> 11) & 3u][tq][0];
-                                    const uint32_t a1 = (uint32_t)(uintptr_t)&eqt[(rw >> 27) & 3u][tq][0];
-    #pragma unroll
-                                    for (int k = 0; k < K; ++k)
-                                        asm volatile("ds_read_u16_d16 %0, %1 offset:%3\n\tds_read_u16_d16_hi %0, %2 offset:%3"
-                                                     : "=&v"(sw[k]) : "v"(a0), "v"(a1), "i"(2 * k));
-                                    // the words are defined only after this wait (the compiler does not
-                                    // track inline-asm LDS loads): redefine them here
-                                    static_assert(K == 8 || K == 6 || K == 4, "d16 substitution: K in {4, 6, 8}");
-                                    if constexpr (K == 8)
-                                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sw[0]), "+v"(sw[1]), "+v"(sw[2]), "+v"(sw[3]),
-                                                     "+v"(sw[4]), "+v"(sw[5]), "+v"(sw[6]), "+v"(sw[7]));
-                                    else if constexpr (K == 6)
-                                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sw[0]), "+v"(sw[1]), "+v"(sw[2]), "+v"(sw[3]),
-                                                     "+v"(sw[4]), "+v"(sw[5]));
-                                    else
-                                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sw[0]), "+v"(sw[1]), "+v"(sw[2]), "+v"(sw[3]));
-                                }
-                                if (rw & (A2_OTHER | (A2_OTHER << 16))) {  // a row byte other than A/C/G/T
-                                    const uint8_t* cseq = chs[cur].cseq;
-                                    const uint32_t b0 = rw & 0xFFu, b1 = (rw >> 16) & 0xFFu;
-    #pragma unroll
-                                    for (int k = 0; k < K; ++k) {
-                                        const int jc = j0 + k;
-                                        const uint32_t cb_ = jc <= nB ? (uint32_t)cseq[jc - 1] : 0u;
-                                        const int s0_ = ((cb_ != 0u && cb_ == b0) ? sc.ma : sc.mi) - 2 * dz;
-                                        const int s1_ = ((cb_ != 0u && cb_ == b1) ? sc.ma : sc.mi) - 2 * dz;
-                                        if (rw & A2_OTHER) sw[k] = (sw[k] & 0xFFFF0000u) | ((uint32_t)s0_ & 0xFFFFu);
-                                        if (rw & (A2_OTHER << 16)) sw[k] = (sw[k] & 0xFFFFu) | ((uint32_t)s1_ << 16);
-                                    }
-                                }
-#else
                                 uint32_t eq0[KW], eq1[KW];
                                 {
                                     // the per-thread table address is recomputed here (one op) rather
@@ -884,7 +893,6 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         if (rw & (A2_OTHER << 16)) eq1[q] = v1;
                                     }
                                 }
-#endif
                                 // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
                                 // minus 1 because the F payload is kept odd (below; not in the best-open form)
                                 const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
@@ -912,27 +920,37 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     // cheaper than extends (co, oy <= 0 in drift units), so Ix may open from
                                     // B = max(M, Ix, Iy) instead of max(M, Iy) (Ix + o <= Ix + e), Iy likewise,
                                     // and the diagonal input of the next column is B itself: per cell
-                                    //   M = B(i-1, j-1) + s,  X = max(B_up + co_j, X_up),
-                                    //   Y = max(B_left + oy_i, Y_left),  B = max(max(M, X), Y)
-                                    // -- four maxima and no tag fix-ups.  The values of M, Ix and Iy are
+                                    //   M = B(i-1, j-1) + s,  X = max(B_up + co_j, X_up),  F = max(M, X),
+                                    //   Y = max(F_left + oy_i, Y_left),  B = max(F, Y)
+                                    // -- four maxima and no tag fix-ups (Iy keeps Biopython's open from
+                                    // M and Ix, F: the left-to-right chain is one maximum per column).  The values of M, Ix and Iy are
                                     // Biopython's, so the walker decides every tie of the first path from
                                     // D1 = M - X and D2 = M - Y (stored as int8; [-9, 17] over every cell of
                                     // the CPU model, tools/proto_bopen.c).  Registers: stG = B, stX = X of
-                                    // the previous row, F1 = B and Y of the left column, d1 = diagonal B.
+                                    // the previous row, F1 = F and Y of the left column, d1 = diagonal B.
     #pragma unroll
                                     for (int k = 0; k < K; ++k) {
                                         const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
                                         const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
-#if A2_D16_SUB
-                                        (void)sel;
-                                        const at_s2 sM = as_s2(sw[k]);
-#else
                                         const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-#endif
                                         const at_s2 M = padd32(d1, as_u32(sM));
-                                        const at_s2 Xn = pmax(padd32(Bu, colc[k][tq]), Xu);
+#if A2_EARLY_X
+                                        const at_s2 Xn = Xu;  // updated at the top of the step
+#else
+                                        // Ix open of column j: one uniform constant except on column nB (UNI:
+                                        // the lane's last slot, its constant read once per step)
+                                        const at_s2 Xn = pmax(padd32(Bu, decltype(UNI)::value ? (k < K - 1 ? coi : cend) : colc[k][tq]), Xu);
+#endif
+                                        const at_s2 Fn = pmax(M, Xn);
+#if A2_BOPEN_Y
+                                        const at_s2 Yn = pmax(padd32(F1, oy1i), Y);  // Iy opens from B
+#else
+                                        // Iy opens from F = max(M, Ix) of the left column (Biopython's own
+                                        // recurrence, same values): the left-to-right dependency chain is then
+                                        // one maximum per column instead of add + two maxima through B
                                         const at_s2 Yn = pmax(padd32(F1, oy1i), Y);
-                                        const at_s2 Bn = pmax(pmax(M, Xn), Yn);
+#endif
+                                        const at_s2 Bn = pmax(Fn, Yn);
                                         if constexpr (decltype(TR)::value) {
                                             // D1 = M - X, D2 = M - Y over both halves with 32-bit subtracts
                                             // (the high half carries the low half's borrow: a2_raw_de)
@@ -943,7 +961,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         d1 = Bu;
                                         stG[k] = as_u32(Bn);
                                         stX[k] = as_u32(Xn);
-                                        F1 = Bn;
+                                        F1 = A2_BOPEN_Y ? Bn : Fn;
                                         Y = Yn;
                                     }
                                 } else {
@@ -953,12 +971,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     const at_s2 G1 = as_s2(as_u32(G) | 0x00010001u);
                                     const at_s2 nd1 = pmax(G1, X1);
                                     const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
-#if A2_D16_SUB
-                                    (void)sel;
-                                    const at_s2 sM = as_s2(sw[k]);
-#else
                                     const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-#endif
                                     // default scores: both substitution halves are >= 0 (drift), so M is one
                                     // 32-bit add too; other scores may subtract: per-half add
                                     const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;
@@ -1050,7 +1063,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 }
                             }
                             // best of (i, j0 - 1) (| 1 in the tagged forms): the next row's diagonal
-                            if constexpr (RAW) carry = inF;
+                            if constexpr (RAW) carry = A2_BOPEN_Y ? inF : as_u32(pmax(as_s2(inF), as_s2(inY)));
                             else carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;
             };
 
@@ -1066,13 +1079,20 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                     if (blk >= 0 && blk < nblk) {
                         const int s0 = blk * INTERVAL;
                         const int s1 = min(s0 + INTERVAL, nsteps);
-                        if (w == 0) {
-                            for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
-                        } else if (w == W - 1) {
-                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
-                        } else {
-                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, s);
-                        }
+                        // uniform Ix-open constant when column nB is each lane's last slot (early-X
+                        // best-open form only; one step variant per wave role and layout)
+                        const bool uni = RAW && A2_UNI_CO && knb == K - 1;
+                        auto run = [&](auto UNI) {
+                            if (w == 0) {
+                                for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, UNI, s);
+                            } else if (w == W - 1) {
+                                for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, UNI, s);
+                            } else {
+                                for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, UNI, s);
+                            }
+                        };
+                        if (uni) run(std::true_type{});
+                        else run(std::false_type{});
                     }
                 }
                 const int gpre = (it + 1) * INTERVAL + tid;

@@ -5,10 +5,10 @@
  * Default scores open no cheaper than they extend (io <= ie, eo <= ee), so the gap recurrences
  * may open from the cell's best state B = max(M, Ix, Iy) instead of max(M, Iy) / max(M, Ix):
  *   Ix(i, j) = max(M + o, Iy + o, Ix + e)(i-1, j) = max(B(i-1, j) + o, Ix(i-1, j) + e)   (Ix + o <= Ix + e)
- *   Iy(i, j) = max(B(i, j-1) + o, Iy(i, j-1) + e)                                      (likewise)
+ *   (Iy may likewise open from B(i, j-1); the kernel keeps Biopython's F = max(M, Ix) there)
  * and the diagonal input of the next column is B itself, so per cell the fill is
- *   M = B(i-1, j-1) + s,  X = max(B_up + co_j, X_up),  Y = max(B_left + ro_i, Y_left),
- *   B = max(max(M, X), Y)
+ *   M = B(i-1, j-1) + s,  X = max(B_up + co_j, X_up),  F = max(M, X),
+ *   Y = max(F_left + ro_i, Y_left),  B = max(F, Y)
  * (drift coordinates V - (i + j) ie: both extends vanish, co_j / ro_i = open - ie; plain, untagged
  * scores).  The values of M, Ix and Iy are Biopython's, so the first path is decided exactly from
  * D1 = M - X and D2 = M - Y of each cell (int8: the trace bytes), whatever tie set a cell holds.
@@ -66,7 +66,7 @@ int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4]
     int fin = 0;
     for (int i = 1; i <= nA; i++) {
         const int ro = (i == nA ? eo : io) - dz;
-        int Bl = eo + ee * (i - 1) - i * dz; /* Ix(i, 0) */
+        int Fl = eo + ee * (i - 1) - i * dz; /* Ix(i, 0) = F(i, 0) */
         int Yl = NEG;
         int d = (i == 1) ? 0 : eo + ee * (i - 2) - (i - 1) * dz; /* B(i - 1, 0) */
         for (int j = 1; j <= nB; j++) {
@@ -74,8 +74,9 @@ int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4]
             const int co = (j == nB ? eo : io) - dz;
             const int M = d + ((x[i - 1] == y[j - 1]) ? ma : mi) - 2 * dz;
             const int Xn = max2(Bu + co, Xu);
-            const int Yn = max2(Bl + ro, Yl);
-            const int Bn = max2(max2(M, Xn), Yn);
+            const int Fn = max2(M, Xn);
+            const int Yn = max2(Fl + ro, Yl); /* Iy opens from F = max(M, Ix) (Biopython's recurrence) */
+            const int Bn = max2(Fn, Yn);
             const size_t c = (size_t)i * (nB + 1) + j;
             t1[c] = M - Xn;
             t2[c] = M - Yn;
@@ -88,7 +89,7 @@ int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4]
             d = Bu;
             B[j] = Bn;
             X[j] = Xn;
-            Bl = Bn;
+            Fl = Fn;
             Yl = Yn;
             if (i == nA && j == nB) fin = Bn;
         }
