@@ -108,6 +108,10 @@ constexpr bool a2_raw() { return DEF && W <= A2_RAW_MAX_W; }
 #ifndef A2_UNI_CO
 #define A2_UNI_CO 0
 #endif
+// 1: the best-open (RAW) walks run the branch-free hop (walk_run_raw)
+#ifndef A2_WALK_BF
+#define A2_WALK_BF 1
+#endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
 #endif
@@ -221,6 +225,14 @@ __device__ __forceinline__ void a2_raw_de(uint32_t w, int sm, int& d, int& e) {
         d = (int)(int8_t)(uint8_t)((w >> 8) + ((w >> 7) & 1u));
         e = (int)(int8_t)(uint8_t)((w >> 24) + ((w >> 23) & 1u));
     }
+}
+
+// Walker base code without a branch tree: A 0, C 1, T 2, G 3 (bits 1-2 of the byte, either case),
+// 4 for any other byte.  Transitions (A<->G, C<->T) differ in both bits, transversions in one.
+__device__ __forceinline__ uint32_t a2_wcode(uint32_t c) {
+    const uint32_t d = (c & 0xDFu) - 0x41u;  // 'A' -> 0, 'C' -> 2, 'G' -> 6, 'T' -> 19
+    const bool ok = d < 20u && ((0x80045u >> d) & 1u);
+    return ok ? ((c >> 1) & 3u) : 4u;
 }
 
 // Row records.  One 8-byte LDS entry per step row g holds both streams: .x = two 16-bit row
@@ -605,6 +617,131 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         W_.ncol = ncol;
     };
 
+    // Best-open walker (RAW), written branch-free: the three state cases of the move out of (i, j)
+    // are selects over one straight-line hop instead of three divergent branches (the walker wave
+    // shares its SIMD with the fill waves, so its VALU count is the cost).  Same decisions, counters,
+    // strings, score check and escapes as walk_run.  The candidates of the move into (i, j) are taken
+    // at (ni, nj) relative to Ix there plus a per-case offset:
+    //   diagonal arrival: (M, Ix, Iy) - Ix           = (D1,      0, D1 - D2)
+    //   Ix arrival:       (M + co, Ix, Iy + co) - Ix = (D1 + co, 0, D1 - D2 + co)
+    //   Iy arrival:       (M + oy, Ix + oy, Iy) - (Ix + oy) = (D1, 0, D1 - D2 - oy)
+    auto walk_run_raw = [&](int pb, int budget, int target) {
+        AtWalk& W_ = wks[lane < 2 * AT2_CHUNK ? lane : 0];
+        int st = lane < 2 * AT2_CHUNK ? W_.st : AT_DONE;
+        if (!AT_OK(st != (int)AT_POISON_LDS && W_.pi != (int)AT_POISON_LDS, AG_WALK_POISON)) st = AT_DONE;
+        if (!__any(st != AT_DONE)) return;
+        const int pi = W_.pi;
+        const ChainPair& cp = tab[pb][AT_OK(st == AT_DONE || (pi >= 0 && pi < chs[pb].n), AG_PI) ? pi : 0];
+        const AtChain& ch = chs[pb];
+        const int fx = cp.fx, lx = cp.lx, fy = ch.fy, ly = ch.ly, r0 = cp.r0, sm = cp.pad;
+        const int prio = W_.prio;
+        const int bdl = min(0, ch.nB - cp.nA) - band;
+        const uint32_t bwd = (uint32_t)(abs(ch.nB - cp.nA) + 2 * band);
+        const uint8_t* rs = cp.rseq;
+        const uint8_t* cs = ch.cseq;
+        const uint8_t* trb = bufs + (size_t)pb * (size_t)buf_bytes;
+        int i = W_.i, j = W_.j, first = W_.first;
+        uint32_t xa = W_.xa, yb = W_.yb;
+        int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
+        int sc2 = W_.sc2, ncol = W_.ncol;
+        const int nA_ = cp.nA, nB_ = ch.nB;
+        const int co_i = sc.io - dz, co_e = sc.eo - dz;  // opens relative to the (drift-free) extend
+        const int bsh = sm ? 8 : 0;                       // this stream's byte of each 16-bit half
+        for (int h = 0; budget < 0 || h < budget; ++h) {
+            if (!__any(st < AT_DONE)) break;
+            if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+            if (st < AT_DONE) {
+                const bool isM = st == AT_M, isX = st == AT_IX, isY = st == AT_IY;
+                // counters and score of the move out of (i, j) (xa, yb: its row / column bytes)
+                const uint32_t bx = a2_wcode(xa), by = a2_wcode(yb);
+                const uint32_t dd = bx ^ by;
+                const bool cnt = isM && !first && (bx | by) < 4u;
+                valid += cnt;
+                ts += cnt && dd == 3u;                 // a2_wcode: A<->G, C<->T differ in both bits
+                tv += cnt && (dd == 1u || dd == 2u);
+                gap += (isX && bx < 4 && j - 1 >= fy && j <= ly) || (isY && by < 4 && i - 1 >= fx && i <= lx);
+                sc2 += (isM && !first) ? (xa == yb ? sc.ma : sc.mi) : 0;
+                const int ni = isY ? i : i - 1, nj = isX ? j : j - 1;
+                if (so.sx && !first) {  // this column of the alignment, right to left, in (a, b) order
+                    const uint32_t rc = isY ? (uint32_t)'-' : xa, cc = isX ? (uint32_t)'-' : yb;
+                    const size_t o = ((size_t)cp.p * so.nslot + ((prio ^ cp.swp) & (so.nslot - 1))) * (size_t)so.cap +
+                                     (size_t)(nA_ + nB_ - 1 - ncol);
+                    so.sx[o] = (uint8_t)(cp.swp ? cc : rc);
+                    so.sy[o] = (uint8_t)(cp.swp ? rc : cc);
+                    ++ncol;
+                }
+                first = 0;
+                if (ni == 0 && nj == 0) {  // the walk is complete (once per walk)
+                    if (!isM) sc2 += sc.eo;  // the gap run (if any) opened at the start: end-gap open
+                    if (sc2 != fin[pb][pi] + (nA_ + nB_) * dz) {  // a wrong decision: queue the pair
+                        st = AT_ESC;
+                    } else {
+                        const int64_t p = cp.p;
+                        double* o = out_mode == OUT_BOTH ? out + (p * 2 + ((prio ^ cp.swp) ? 1 : 0)) * nm : out + p * nm;
+                        AT_DIAG(4, 1);
+                        if (AT_OK(p >= 0 && p < ps.count, AG_OUT))
+                            for (int m = 0; m < nm; ++m)
+                                o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
+                        if (sout && (out_mode != OUT_BOTH || !prio) && AT_OK(pi >= 0 && pi < AT2_CHUNK && fin[pb][pi] != (int)AT_POISON_LDS, AG_FIN))
+                            sout[p] = fin[pb][pi] + (nA_ + nB_) * dz;
+                        if (so.slen) so.slen[p * so.nslot + ((prio ^ cp.swp) & (so.nslot - 1))] = ncol;
+                        st = AT_DONE;
+                    }
+                } else {
+                    const bool in = ni >= 1 && nj >= 1;
+                    const bool esc = in && band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
+                    // trace word and bytes of (ni, nj) (row / column 0: clamped, the value unused)
+                    const int cj = max(nj, 1) - 1, ci = max(ni, 1) - 1;
+                    const uint32_t t = (uint32_t)cj / K, k = (uint32_t)cj - t * K;
+                    const uint32_t off = (((uint32_t)(r0 + ci) + (t & 63u)) * (uint32_t)NT + t) * (uint32_t)TB + 4u * k;
+                    const uint32_t xa_ = a2_load_byte(rs + ci), yb_ = a2_load_byte(cs + cj);
+                    uint32_t nb = 0u;
+                    if (AT_OK(off + 4 <= (size_t)buf_bytes, AG_LOAD)) nb = a2_load_trace32(trb + off);
+                    xa = ni >= 1 ? xa_ : 0u;
+                    yb = nj >= 1 ? yb_ : 0u;
+                    // D1, D2 of this stream: bytes 0 / 2 (stream 0) or 1 / 3 plus the low half's borrow
+                    const int d1v = (int)(int8_t)(uint8_t)((nb >> bsh) + (sm ? ((nb >> 7) & 1u) : 0u));
+                    const int d2v = (int)(int8_t)(uint8_t)((nb >> (16 + bsh)) + (sm ? ((nb >> 23) & 1u) : 0u));
+                    (void)AT_OK(esc || !in || (d1v >= -64 && d1v <= 63 && d2v >= -64 && d2v <= 63), AG_TRACE_POISON);
+                    const int co = j == nB_ ? co_e : co_i, oy = i == nA_ ? co_e : co_i;
+                    const int vM = d1v + (isX ? co : 0);
+                    const int vY = d1v - d2v + (isX ? co : isY ? -oy : 0);
+                    const int vm = max(max(vM, vY), 0);
+                    int nst = vM == vm ? AT_M : prio ? (vY == vm ? AT_IY : AT_IX) : (vm == 0 ? AT_IX : AT_IY);
+                    nst = ni == 0 ? AT_IY : nj == 0 ? AT_IX : nst;
+                    // gap moves: extend when the run continues, end scores on the edges
+                    const bool ext = isX ? nst == AT_IX : nst == AT_IY;
+                    const bool en = isX ? (j == nB_ || j == 0) : (i == nA_ || i == 0);
+                    sc2 += isM ? 0 : ext ? (en ? sc.ee : sc.ie) : (en ? sc.eo : sc.io);
+                    i = ni;
+                    j = nj;
+                    st = esc ? AT_ESC : nst;
+                }
+            }
+        }
+        if (st == AT_ESC) {  // queue the pair (once, whichever orientation stopped) for the full-trace pass
+            if (atomicOr(&escf[pb][pi], 1) == 0 && AT_OK(esc_list != nullptr, AG_OUT)) esc_list[atomicAdd(esc_n, 1ull)] = cp.p;
+            st = AT_DONE;
+        }
+        if (lane >= 2 * AT2_CHUNK) return;
+        W_.i = i;
+        W_.j = j;
+        W_.st = st;
+        W_.first = first;
+        W_.xa = xa;
+        W_.yb = yb;
+        W_.valid = valid;
+        W_.ts = ts;
+        W_.tv = tv;
+        W_.gap = gap;
+        W_.sc2 = sc2;
+        W_.ncol = ncol;
+    };
+    auto walk = [&](int pb, int budget, int target) {
+        if constexpr (RAW && A2_WALK_BF) walk_run_raw(pb, budget, target);
+        else walk_run(pb, budget, target);
+    };
+
     // The fill waves and the walker wave run separate copies of the chain loop (same barrier
     // sequence): the fill state (columns, carries) is then not live across the walker code,
     // which kept it in registers for the whole loop and spilled both to scratch.
@@ -699,7 +836,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             const int pb = cur ^ 1;
             if constexpr (IS_W) walk_init(pb, prev_n);
             if (n == 0) {
-                if constexpr (IS_W) walk_run(pb, -1, 0);
+                if constexpr (IS_W) walk(pb, -1, 0);
                 break;
             }
             const int nB = chs[cur].nB;
@@ -1073,7 +1210,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             const int nint = nblk + WAVE_LAG * (W - 1);
             for (int it = 0; it < nint; ++it) {
                 if constexpr (IS_W) {
-                    walk_run(pb, hops, W * (it + 1));
+                    walk(pb, hops, W * (it + 1));
                 } else {
                     const int blk = it - WAVE_LAG * w;
                     if (blk >= 0 && blk < nblk) {
@@ -1101,7 +1238,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);  // this fill wave is done with interval it
                 __syncthreads();
             }
-            if constexpr (IS_W) walk_run(pb, -1, 0);
+            if constexpr (IS_W) walk(pb, -1, 0);
             prev_n = n;
             cur ^= 1;
         }
