@@ -325,7 +325,6 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
              int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
              unsigned long long* __restrict__ esc_n, StrOut so) {
     static_assert(K % 2 == 0 && K <= 16, "16-bit score fields: K / 2 words per stream and base");
-    static_assert(!RAW || DEF, "the raw-difference bounds are those of the default scores");
     constexpr int TB = RAW ? 4 * K : 2 * K;  // trace bytes per lane and step
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
@@ -337,7 +336,9 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
     // Drift (default scores, where every gap extend is ie): cells store V(i, j) - (i + j) dz, so
     // Ix(i, j) = max(G(i-1, j) + o, Ix(i-1, j) + e) becomes max(G + (o - dz), Ix) and likewise for
     // Iy: both extend additions vanish; M absorbs -2 dz in its substitution table.
-    const int dz = DEF ? sc.ie : 0;
+    // (the best-open form of other scores needs one extend for internal and end gaps, pick_variantt2,
+    // so it drifts too: its state differences are then bounded by the scores)
+    const int dz = (DEF || RAW) ? sc.ie : 0;
     __shared__ uint2 xinfo[XR];  // row records (a2_row_record)
     __shared__ ChainPair tab[2][AT2_CHUNK];
     __shared__ int fin[2][AT2_CHUNK];
@@ -645,7 +646,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap;
         int sc2 = W_.sc2, ncol = W_.ncol;
         const int nA_ = cp.nA, nB_ = ch.nB;
-        const int co_i = sc.io - dz, co_e = sc.eo - dz;  // opens relative to the (drift-free) extend
+        const int co_i = sc.io - sc.ie, co_e = sc.eo - sc.ee;  // opens relative to their extends
         const int bsh = sm ? 8 : 0;                       // this stream's byte of each 16-bit half
         for (int h = 0; budget < 0 || h < budget; ++h) {
             if (!__any(st < AT_DONE)) break;
@@ -959,7 +960,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                             (void)AT_OK(rw != AT_POISON_LDS, AG_ROW_POISON);
                             uint32_t inF, inY;
                             if constexpr (decltype(FW)::value) {  // column 0: Ix(i, 0) = eo + ee (i - 1), Iy = -inf
-                                if constexpr (!DEF) {  // one row on per step; a first row restarts its half
+                                if constexpr (!DEF && !RAW) {  // one row on per step; a first row restarts its half
                                     const uint32_t mf = ((rw & A2_FIRST) ? 0xFFFFu : 0u) | ((rw & (A2_FIRST << 16)) ? 0xFFFF0000u : 0u);
                                     bnd = (bnd1 & mf) | (as_u32(as_s2(bnd) + (at_s2){(short)sc.ee, (short)sc.ee}) & ~mf);
                                 }
@@ -1070,7 +1071,8 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
                                         const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
                                         const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-                                        const at_s2 M = padd32(d1, as_u32(sM));
+                                        // (other scores: a per-half add, the drifted substitution may be negative)
+                                        const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;
 #if A2_EARLY_X
                                         const at_s2 Xn = Xu;  // updated at the top of the step
 #else
@@ -1248,13 +1250,15 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
 }
 
 // The band pass (every pair of the launch, trace strip of half-width `band`; 0 = full trace) ...
-template <int K, int W, bool DEF, int OCC>
+// RAWT: the best-open fill with the raw-difference trace (default scores on W <= 2; other scores whose
+// opens are no better than their extends, capi.hip pick_variantt2), else the tagged fill with sign digits
+template <int K, int W, bool DEF, int OCC, bool RAWT = a2_raw<W, DEF>()>
 __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
           double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
           int cap_rows, int hops, unsigned long long* __restrict__ next, int band, int64_t* __restrict__ esc_list,
           unsigned long long* __restrict__ esc_n, StrOut so) {
-    alignt2_body<K, W, DEF, a2_raw<W, DEF>()>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
+    alignt2_body<K, W, DEF, RAWT>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
                                  hops, next, band, esc_list, esc_n, so);
 }
 // ... and the full-trace pass over the pairs it queued (ps.sel / ps.dcount): a kernel of its own

@@ -394,6 +394,7 @@ struct VariantT {
     const void* fn;
     void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, PairSrc, KScores, MetricSpec, int, int, double*,
                    int32_t*, uint8_t*, int64_t, int, int, unsigned long long*, BandArgs, StrOut);
+    bool raw = false;  // packed kernels: best-open fill + raw-difference trace (4 K bytes per lane-step)
 };
 
 template <int K, int W, bool DEF, int OCC>
@@ -422,9 +423,12 @@ const VariantT* pick_variantt(const KScores& k, int max_len) {
 
 // Packed variants (two pairs per lane in 16-bit halves, alignt2_kernel.hpp); same launch shape.
 #define T2_VARIANTT2(K, W, DEF, OCC) \
-    VariantT{K, W, OCC, DEF, (const void*)&k_alignt2<K, W, DEF, OCC>, &launch_alignt2<K, W, DEF, OCC>}
+    VariantT{K, W, OCC, DEF, (const void*)&k_alignt2<K, W, DEF, OCC>, &launch_alignt2<K, W, DEF, OCC>, a2_raw<W, DEF>()}
+// other scores on the best-open fill (opens no better than extends: bopen_ok)
+#define T2_VARIANTT2R(K, W, OCC) \
+    VariantT{K, W, OCC, false, (const void*)&k_alignt2<K, W, false, OCC, true>, &launch_alignt2<K, W, false, OCC, true>, true}
 
-template <int K, int W, bool DEF, int OCC>
+template <int K, int W, bool DEF, int OCC, bool RAWT = a2_raw<W, DEF>()>
 void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSrc ps, KScores sc, MetricSpec ms,
                     int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb, int cap, int hops,
                     unsigned long long* nx, BandArgs ba, StrOut str) {
@@ -432,7 +436,7 @@ void launch_alignt2(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, PairSr
         hipLaunchKernelGGL((k_alignt2_queued<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr,
                            bb, cap, hops, nx, str);
     else
-        hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
+        hipLaunchKernelGGL((k_alignt2<K, W, DEF, OCC, RAWT>), g, b, 0, st, x, y, ps, sc, ms, chunk, om, out, so, tr, bb, cap,
                            hops, nx, ba.band, ba.esc_list, ba.esc_n, str);
 }
 
@@ -454,9 +458,31 @@ const VariantT kAlignT2[] = {
     // 1 025 - 2 048 columns: four fill waves + the walker (5 waves per workgroup)
     T2_VARIANTT2(6, 4, true, 5), T2_VARIANTT2(8, 4, true, 5), T2_VARIANTT2(6, 4, false, 5), T2_VARIANTT2(8, 4, false, 5),
 };
+// other scores, best-open fill (at 6 waves per SIMD the compiler ends at 4 with 117 VGPRs)
+const VariantT kAlignT2R[] = {
+    T2_VARIANTT2R(4, 1, A2_OCC_GEN), T2_VARIANTT2R(8, 1, A2_OCC_GEN),
+    T2_VARIANTT2R(6, 2, A2_OCC_GEN), T2_VARIANTT2R(8, 2, A2_OCC_GEN),
+};
+
+// The best-open recurrences (alignt2_kernel.hpp) need every open no better than its extend (an Ix / Iy
+// open from its own state is then never better than the extend); the raw trace keeps the cell's
+// state differences as int8 (CPU model: within [-16, 25] for scores up to 10 with one extend; the
+// walkers' score check is a second net, but it cannot see a wrapped difference that flips a tie
+// between two optimal moves, so the bound itself must hold)
+// The kernel drifts by the extend (cells store V - (i + j) ie), which needs ONE extend for internal and
+// end gaps: then neighbouring cells differ by amounts bounded by the scores and the int8 differences
+// are exact (with ie != ee they grow with the length of end gaps: tools/proto_bopen.c).
+bool bopen_ok(const KScores& k) {
+    auto ab = [](int v) { return v < 0 ? -v : v; };
+    const int big = std::max({ab(k.ma), ab(k.mi), ab(k.io), ab(k.ie), ab(k.eo), ab(k.ee)});
+    return k.ie == k.ee && k.io <= k.ie && k.eo <= k.ee && big <= 12 && !getenv("TAXI2_NO_BOPEN");
+}
 
 const VariantT* pick_variantt2(const KScores& k, int max_len) {
     const bool def = is_default(k);
+    if (!def && bopen_ok(k))
+        for (const auto& v : kAlignT2R)
+            if (64 * v.K * v.W >= max_len) return &v;
     for (const auto& v : kAlignT2)
         if (v.def == def && 64 * v.K * v.W >= max_len) return &v;
     return nullptr;
@@ -483,7 +509,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     // two trace buffers per resident workgroup: shrink the chunk (hence the chain rows) until they
     // fit the budget (TAXI2_AT_TRACE_GB, default 40 GB of the 288 GB HBM; 80 GB for the packed
     // default-score kernel, whose raw-difference trace takes 4 bytes per lane-column and step)
-    const bool raw = packed && v.def && v.W <= A2_RAW_MAX_W;  // alignt2_kernel.hpp a2_raw: raw-difference trace
+    const bool raw = packed && v.raw;  // best-open fill + raw-difference trace (alignt2_kernel.hpp)
     double budget_gb = raw ? 80.0 : 40.0;
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     auto buf_bytes = [&](int64_t e) {

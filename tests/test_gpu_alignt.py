@@ -64,7 +64,7 @@ def test_alignt_triangle(engine, oracle_c, env):
     st = engine.upload(seqs, align=True)
     a, b = tri_pairs(len(seqs))
     nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
-    for name in ("default", "generic"):
+    for name in ("default", "generic", "generic1"):
         sc = SCORE_SETS[name]
         got, gsc = _with_env(env, lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
         old, osc = _with_env({"TAXI2_NO_ALIGNT": "1"},

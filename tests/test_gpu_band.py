@@ -81,7 +81,7 @@ def test_band_rectangle_and_list(engine, oracle_c, band):
     allseq = q + r
     pa = np.repeat(np.arange(len(q)), len(r))
     pb = np.tile(np.arange(len(r)), len(q)) + len(q)
-    for name in ("default", "generic"):
+    for name in ("default", "generic", "generic1"):
         sc = SCORE_SETS[name]
         got = _with_env(env, lambda: engine.rect_pairs(qs, rs, 0, len(q), METRICS, sc))
         exp, _ = oracle_c.batch(allseq, pa, pb, align=True, scores=sc)

@@ -22,6 +22,8 @@ TOL_LOG = 1e-12  # jc / k2p (f64 log on GPU vs glibc)
 SCORE_SETS = {
     "default": (1, -1, -8, -1, -1, -1),
     "generic": (2, -3, -5, -2, -1, -1),
+    # one extend for internal and end gaps: the packed aligner's best-open fill (capi.hip bopen_ok)
+    "generic1": (2, -3, -5, -2, -3, -2),
     "linear": (1, -1, -2, -2, -1, -1),
 }
 
@@ -272,7 +274,7 @@ def test_single_orientation_divergent_pairs(engine, oracle_c):
     st = engine.upload(seqs, align=True)
     n = len(seqs)
     a, b = tri_pairs(n)
-    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"]):
+    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"], SCORE_SETS["generic1"]):
         got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
         two, tsc = _with_env("TAXI2_NO_ALIGN1", "1",
                              lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
@@ -339,7 +341,7 @@ def test_chained_pairs(engine, oracle_c, chunk):
     seqs[11] = seqs[10]  # identical neighbours: a full-tie pair inside a chain
     st = engine.upload(seqs, align=True)
     a, b = tri_pairs(len(seqs))
-    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"]):
+    for sc in (SCORE_SETS["default"], SCORE_SETS["generic"], SCORE_SETS["generic1"]):
         got, gsc = _with_env("TAXI2_A1_CHUNK", str(chunk),
                              lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
         one = _with_env("TAXI2_A1_NOCHAIN", "1", lambda: engine.all_pairs(st, 0, len(a), METRICS, sc))
@@ -372,7 +374,7 @@ def test_chained_pairs(engine, oracle_c, chunk):
         s.free()
 
 
-@pytest.mark.parametrize("scores", ["default", "generic"])
+@pytest.mark.parametrize("scores", ["default", "generic", "generic1"])
 @pytest.mark.parametrize("chunk", [16, 5])
 def test_chained_long_ragged_rect(engine, oracle_c, chunk, scores):
     """2 100-2 600 bp (past the packed kernel's 2 048 columns, so k_align1c with three-word

@@ -108,7 +108,7 @@ def test_packed_w4_rectangle_after_other_kernels(engine, oracle_c):
     allseq = q + r
     pa = np.repeat(np.arange(len(q)), len(r))
     pb = np.tile(np.arange(len(r)), len(q)) + len(q)
-    for name in ("default", "generic"):
+    for name in ("default", "generic", "generic1"):
         sc = SCORE_SETS[name]
         exp, _ = oracle_c.batch(allseq, pa, pb, align=True, scores=sc)
         for env in ({}, {"TAXI2_AT_CHUNK": "5"}):

@@ -21,6 +21,7 @@ sys.path.insert(0, str(ROOT))
 SETS = {
     "default": (1, -1, -8, -1, -1, -1),
     "generic": (2, -3, -5, -2, -1, -1),
+    "generic1": (2, -3, -5, -2, -3, -2),  # one extend: the best-open fill
     "linear": (1, -1, -2, -2, -2, -2),
 }
 

@@ -50,8 +50,13 @@ static int pick(int vM, int vX, int vY, int prio) {
 }
 
 /* stats: [0] min D1, [1] max D1, [2] min D2, [3] max D2, [4] score-check failures, [5] hops */
-int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4] */, int* stats, int wrap) {
-    const int ma = 1, mi = -1, io = -8, ie = -1, eo = -1, ee = -1, dz = ie;
+int proto_align_sc(const char* x, int nA, const char* y, int nB, int* out /* [2][4] */, int* stats, int wrap,
+                   const int* scv /* ma, mi, io, ie, eo, ee; NULL = TaxI2 defaults */) {
+    static const int def[6] = {1, -1, -8, -1, -1, -1};
+    if (!scv) scv = def;
+    const int ma = scv[0], mi = scv[1], io = scv[2], ie = scv[3], eo = scv[4], ee = scv[5];
+    /* drift only when every extend is the same (the default scores); otherwise plain values */
+    const int dz = (ie == ee) ? ie : 0;  /* as the kernel: drift whenever one extend serves both (best-open sets) */
     const int NEG = -16384;
     int8_t* D1 = (int8_t*)calloc((size_t)(nA + 1) * (nB + 1), 1);
     int8_t* D2 = (int8_t*)calloc((size_t)(nA + 1) * (nB + 1), 1);
@@ -65,17 +70,17 @@ int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4]
     }
     int fin = 0;
     for (int i = 1; i <= nA; i++) {
-        const int ro = (i == nA ? eo : io) - dz;
+        const int ro = (i == nA ? eo : io) - dz, re = (i == nA ? ee : ie) - dz;
         int Fl = eo + ee * (i - 1) - i * dz; /* Ix(i, 0) = F(i, 0) */
         int Yl = NEG;
         int d = (i == 1) ? 0 : eo + ee * (i - 2) - (i - 1) * dz; /* B(i - 1, 0) */
         for (int j = 1; j <= nB; j++) {
             const int Bu = B[j], Xu = X[j];
-            const int co = (j == nB ? eo : io) - dz;
+            const int co = (j == nB ? eo : io) - dz, ce = (j == nB ? ee : ie) - dz;
             const int M = d + ((x[i - 1] == y[j - 1]) ? ma : mi) - 2 * dz;
-            const int Xn = max2(Bu + co, Xu);
+            const int Xn = max2(Bu + co, Xu + ce);
             const int Fn = max2(M, Xn);
-            const int Yn = max2(Fl + ro, Yl); /* Iy opens from F = max(M, Ix) (Biopython's recurrence) */
+            const int Yn = max2(Fl + ro, Yl + re); /* Iy opens from F = max(M, Ix) (Biopython's recurrence) */
             const int Bn = max2(Fn, Yn);
             const size_t c = (size_t)i * (nB + 1) + j;
             t1[c] = M - Xn;
@@ -137,10 +142,10 @@ int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4]
                 if (st == ST_M) {          /* best state of (ni, nj); relative to X */
                     nst = pick(a, 0, a - b, prio);
                 } else if (st == ST_IX) {  /* candidates of Ix(i, j) at (i - 1, j), relative to X + e */
-                    const int co = (j == nB ? eo : io) - dz;
+                    const int co = j == nB ? eo - ee : io - ie;
                     nst = pick(a + co, 0, a - b + co, prio);
                 } else {                   /* candidates of Iy(i, j) at (i, j - 1), relative to Y + e */
-                    const int ro = (i == nA ? eo : io) - dz;
+                    const int ro = i == nA ? eo - ee : io - ie;
                     nst = pick(b + ro, b - a + ro, 0, prio);
                 }
             }
@@ -170,4 +175,8 @@ int proto_align(const char* x, int nA, const char* y, int nB, int* out /* [2][4]
     }
     free(D1); free(D2); free(t1); free(t2); free(B); free(X);
     return best;
+}
+
+int proto_align(const char* x, int nA, const char* y, int nB, int* out, int* stats, int wrap) {
+    return proto_align_sc(x, nA, y, nB, out, stats, wrap, 0);
 }
