@@ -112,6 +112,19 @@ constexpr bool a2_raw() { return DEF && W <= A2_RAW_MAX_W; }
 #ifndef A2_WALK_BF
 #define A2_WALK_BF 1
 #endif
+// 1: the best-open fill forms column k+1's M from B(i-1, k) before column k's new B exists, so the
+// old B dies first and the new one takes its register: 3 instead of 9 v_mov per step at the loop's
+// back edge (2: on the column-0 fill wave only).  A2_MNEXT_WAIT: drain vector memory before each
+// fill wave's step loop -- with the new register assignment a scratch reload into a register the
+// last wave's loop writes was left in flight, and the wait for it (vmcnt(0), i.e. on the trace
+// stores too) sat inside every step.  Same-box A/B (profiles/r3/ab_mnext/): 4.47e6 (0) -> 4.51e6 (2)
+// -> 4.55e6 pairs/s (1 + wait); 1 without the wait 2.4 % slower than 0
+#ifndef A2_MNEXT
+#define A2_MNEXT 1
+#endif
+#ifndef A2_MNEXT_WAIT
+#define A2_MNEXT_WAIT 1
+#endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
 #endif
@@ -918,6 +931,8 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             auto step = [&](auto FW, auto HO, auto UNI, const int s) {
                             // lane id recomputed (two v_mbcnt) rather than kept live across the chain
                             // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
+                            // (still so after the next-column M ordering: kept live, the step loop
+                            // reloads three dwords from scratch per step in the ISA)
                             int ln;
                             asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
                             const int g = s - ln;
@@ -1033,13 +1048,16 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 }
                                 // end-gap Iy scores on each stream's last row: io + last * (eo - io) per half,
                                 // minus 1 because the F payload is kept odd (below; not in the best-open form)
-                                const at_s2 lastb = as_s2((rw >> 9) & 0x00010001u);
-                                const uint32_t oy1 = as_u32(lastb * (at_s2){(short)(sc.eo - sc.io), (short)(sc.eo - sc.io)} +
-                                                            (at_s2){(short)(sc.io - dz - (RAW ? 0 : 1)), (short)(sc.io - dz - (RAW ? 0 : 1))});
-                                const uint32_t ey = DEF ? pk2(sc.ie, sc.ie)
-                                                        : as_u32(lastb * (at_s2){(short)(sc.ee - sc.ie), (short)(sc.ee - sc.ie)} +
-                                                                 (at_s2){(short)sc.ie, (short)sc.ie});
-                                const uint32_t oy1i = pk_int(oy1), eyi = pk_int(ey);
+                                // Formed directly as pk_int words: with l = 1 in each half of a last row,
+                                // pk_int(l * d + c per half) = l * d + c * 0x10001 (mod 2^32) -- one 24-bit
+                                // multiply-add (d sign-extended from 16 bits) instead of a packed
+                                // multiply-add and the three-op pk_int borrow fix-up
+                                const uint32_t lastw = (rw >> 9) & 0x00010001u;
+                                const uint32_t oy1i = (uint32_t)((int)lastw * (int)(short)(sc.eo - sc.io)) +
+                                                      (uint32_t)(sc.io - dz - (RAW ? 0 : 1)) * 0x00010001u;
+                                const uint32_t eyi = DEF ? pk_int(pk2(sc.ie, sc.ie))
+                                                         : (uint32_t)((int)lastw * (int)(short)(sc.ee - sc.ie)) +
+                                                               (uint32_t)sc.ie * 0x00010001u;
                                 // Representation (doubled scores): G = max(M, Iy) tagged (M odd, Iy even);
                                 // Ix and F = max(M, Ix) kept ODD (2v + 1, no tag): then the diagonal
                                 // max(G, Ix) | 1 = max(G | 1, X1) needs no fix-up, Ix candidates built on G | 1
@@ -1066,13 +1084,26 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     // D1 = M - X and D2 = M - Y (stored as int8; [-9, 17] over every cell of
                                     // the CPU model, tools/proto_bopen.c).  Registers: stG = B, stX = X of
                                     // the previous row, F1 = F and Y of the left column, d1 = diagonal B.
+                                    // M of column k from the diagonal B and the substitution halves of column k
+                                    // (other scores: a per-half add, the drifted substitution may be negative)
+                                    auto mcell = [&](at_s2 diag, int k) {
+                                        const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
+                                        const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
+                                        return DEF ? padd32(diag, as_u32(sM)) : diag + sM;
+                                    };
+                                    at_s2 Mk = mcell(d1, 0);
     #pragma unroll
                                     for (int k = 0; k < K; ++k) {
                                         const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
-                                        const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;
-                                        const at_s2 sM = as_s2(__builtin_amdgcn_perm(eq1[k / 2], eq0[k / 2], sel));
-                                        // (other scores: a per-half add, the drifted substitution may be negative)
-                                        const at_s2 M = DEF ? padd32(d1, as_u32(sM)) : d1 + sM;
+                                        at_s2 M;
+                                        if constexpr (A2_MNEXT == 1 || (A2_MNEXT == 2 && decltype(FW)::value)) {
+                                            // the next column's M first: B(i-1, k) dies here, so column k's
+                                            // new B can take its register
+                                            M = Mk;
+                                            if (k + 1 < K) Mk = mcell(Bu, k + 1);
+                                        } else {
+                                            M = mcell(d1, k);
+                                        }
 #if A2_EARLY_X
                                         const at_s2 Xn = Xu;  // updated at the top of the step
 #else
@@ -1222,9 +1253,17 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                         // best-open form only; one step variant per wave role and layout)
                         const bool uni = RAW && A2_UNI_CO && knb == K - 1;
                         auto run = [&](auto UNI) {
+                            // no vector memory in flight into the last wave's step loop (a scratch reload
+                            // of a register it writes would cost a vmcnt(0) inside every step; gfx9
+                            // encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  Only there: the same wait before
+                            // every role's loop changes the register assignment and brings it back.
+                            auto drain = [] {
+                                if constexpr (A2_MNEXT_WAIT != 0) __builtin_amdgcn_s_waitcnt(0x0F70);
+                            };
                             if (w == 0) {
                                 for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, UNI, s);
                             } else if (w == W - 1) {
+                                drain();
                                 for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, UNI, s);
                             } else {
                                 for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, UNI, s);
