@@ -136,9 +136,18 @@ constexpr int NEG16 = -16384;
 // ONE 32-bit v_add_u32 of the integer c_hi * 65536 + c_lo: no half leaves [0, 65535], so no carry
 // crosses between the halves.  v_add_u32 issues in 2.28 SIMD cycles, v_pk_add_u16 in 4.09
 // (profiles/r2/valu_peak.txt).
-constexpr int BIAS16 = 32768;
+// A2_MAX3 (default-score best-open fill): the bias is 20480 instead, so that every value the fill
+// can hold there -- the -16384 sentinel less a few opens up to the 1 024-column maximum, [4 000,
+// 24 000] biased -- is a positive NORMAL f16 bit pattern ([0x0400, 0x7BFF]), whose order as a float is
+// its order as an unsigned integer: the cell's best state is then ONE v_pk_maximum3_f16 (gfx950) of
+// (M, Ix, Iy) instead of two v_pk_max_u16.  Every other packed form keeps the same bias (the
+// range at_fits16 admits, [-16384 - small, 16383], still maps into [0, 65535]).
+#ifndef A2_MAX3
+#define A2_MAX3 1
+#endif
+constexpr int BIAS16 = A2_MAX3 ? 20480 : 32768;
 constexpr int AT_ESC = AT_DONE + 1;  // walk state: stepped outside the stored trace band
-constexpr uint32_t NEG16X2 = 0x40004000u;  // -16384 + 32768 in both halves
+constexpr uint32_t NEG16X2 = (uint32_t)(NEG16 + BIAS16) * 0x00010001u;  // -16384 biased, both halves
 
 __device__ __forceinline__ at_s2 as_s2(uint32_t v) { return __builtin_bit_cast(at_s2, v); }
 __device__ __forceinline__ uint32_t as_u32(at_s2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -1120,7 +1129,15 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         // one maximum per column instead of add + two maxima through B
                                         const at_s2 Yn = pmax(padd32(F1, oy1i), Y);
 #endif
-                                        const at_s2 Bn = pmax(Fn, Yn);
+                                        at_s2 Bn;
+                                        if constexpr (A2_MAX3 && DEF && A2_BOPEN_Y) {
+                                            // max of three normal positive f16 patterns = their unsigned max
+                                            uint32_t b3;
+                                            asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(b3) : "v"(as_u32(M)), "v"(as_u32(Xn)), "v"(as_u32(Yn)));
+                                            Bn = as_s2(b3);
+                                        } else {
+                                            Bn = pmax(Fn, Yn);
+                                        }
                                         if constexpr (decltype(TR)::value) {
                                             // D1 = M - X, D2 = M - Y over both halves with 32-bit subtracts
                                             // (the high half carries the low half's borrow: a2_raw_de)
