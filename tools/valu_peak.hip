@@ -73,7 +73,7 @@ constexpr int UNROLL = 32;  // asm blocks per loop iteration (256 measured instr
     X(30, "v_bfe_u32", 3) X(31, "v_lshl_add_u32", 3) X(32, "v_and_or_b32", 3) X(33, "v_pk_mad_u16", 3)          \
     X(34, "v_pk_fma_f16", 3) X(35, "v_mad_u32_u24", 3) X(36, "v_pk_add_f32", 6) X(37, "v_pk_mul_f32", 6)       \
     X(38, "v_max_u16", 2) X(39, "v_add_u16", 2) X(40, "v_max_f16", 2) X(41, "v_cvt_f32_i32", 1)               \
-    X(42, "v_add_u32_sdwa", s)
+    X(42, "v_add_u32_sdwa", s) X(43, "v_pk_maximum3_f16", 3) X(44, "v_pk_max_u16", 2)
 #define FORM_2(INS) CH8(INS)
 #define FORM_3(INS) CH8_3(INS)
 #define FORM_1(INS) CH8_1(INS)
