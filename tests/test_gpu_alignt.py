@@ -124,3 +124,29 @@ def test_alignt_bench_shape(engine, oracle_c, packed):
     assert np.array_equal(gsc, esc)
     assert_metrics_equal(got, exp)
     st.free()
+
+
+def test_alignt2_value_range_extremes(engine, oracle_c):
+    """The default-score best-open fill stores its cells as f16 bit patterns (bias 20480, one
+    v_pk_maximum3_f16 per cell pair, alignt2_kernel.hpp A2_MAX3): exact only while every value is a
+    positive normal f16 pattern.  The extremes of that range at the packed shape's 1 024-column
+    capacity: identical full-length sequences (the largest drifted values), full-length all-mismatch
+    pairs, full-length against 1-base sequences (the longest end gaps), long internal runs, non-ACGT
+    rows and empty sequences -- every pair in both orientations against the oracle."""
+    from taxi2_amd._native import tri_pairs
+
+    L = 1024
+    seqs = ["A" * L, "A" * L, "C" * L, "T" * L, "A" * (L // 2) + "C" * (L // 2), "ACGT" * (L // 4),
+            "A", "C", "AC" * 8, "A" * (L - 24) + "N" * 24, "G" * 3 + "A" * (L - 6) + "G" * 3, "", "N" * L]
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
+    sc = SCORE_SETS["default"]
+    got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
+    assert np.array_equal(gsc[nonempty], esc[nonempty])
+    assert_metrics_equal(got, exp)
+    # the identical full-length pair scores its length (the largest value the fill holds)
+    k = int(np.flatnonzero((a == 0) & (b == 1))[0])
+    assert int(gsc[k]) == L
+    st.free()
