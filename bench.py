@@ -88,6 +88,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores (max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    ap.add_argument("--secondary", default="allmetrics,config4,task,config5",
+                    help="secondary legs after the headline (one GPU only; bench_secondary.py); '' = none")
     return ap.parse_args()
 
 
@@ -175,6 +177,17 @@ def main() -> None:
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, buf, offs, eng, seqset)
+    secondary = None
+    legs = [x for x in args.secondary.split(",") if x]
+    if rank == 0 and world == 1 and legs:  # after the timed region, outside the headline
+        import bench_secondary
+
+        del out, scores
+        torch.cuda.empty_cache()
+        secondary = bench_secondary.run_all(eng, seqset, N_SEQS, legs)
+    from taxi2_amd._native import build_info
+
+    build = build_info()
 
     if rank == 0:
         line = {
@@ -212,7 +225,10 @@ def main() -> None:
                 "kernel_ms": kern_ms,
             },
             "compute_roofline": compute,
+            "ceilings": ceilings(value / world, traffic, B, compute),
             "cpu_baseline": cpu,
+            "secondary": secondary,
+            "build": build,
             "assumptions": [
                 "Biopython 1.85's tie order among equal-scoring alignments is restated (end state M>Ix>Iy, "
                 "each backward step the first tied predecessor; (y, x) = Ix/Iy swapped), not pinned: every "
@@ -224,6 +240,30 @@ def main() -> None:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+NORTH_STAR_PER_GPU = 1e8 / 8          # BASELINE.json north_star: >= 1e8 aligned pairs/s on 8 x MI355X
+HBM_MEASURED_GBS = 6290.0             # measured achievable HBM bandwidth (MI355X_MICROARCH.md)
+
+
+def ceilings(per_gpu: float, traffic: float | None, batch: int, compute: dict | None) -> dict:
+    """What the kernel's own limits imply in the metric's unit (pairs/s per GPU): the VALU issue
+    ceilings at today's measured instructions per cell (the kernel's mix, and every instruction at
+    the full VOP2 rate), the HBM cap of today's measured bytes per pair (trace stream + walker
+    fetches, PMC) at the measured achievable bandwidth, and the share of north_star's per-GPU rate."""
+    out = {"north_star_per_gpu": NORTH_STAR_PER_GPU, "share_of_north_star_per_gpu": per_gpu / NORTH_STAR_PER_GPU}
+    if compute:
+        c = json.loads(COMPUTE_CEILING_JSON.read_text())
+        cells = float(SEQ_LEN) * SEQ_LEN
+        rate = N_SIMDS * c["clock_ghz"] * 1e9 / (c["valu_instr_per_cell"] * cells)  # pairs/s per instr/SIMD-clk
+        out["valu_mix_ceiling_pairs_per_s"] = c["ceiling_instr_per_simd_clk"] * rate
+        out["valu_full_rate_ceiling_pairs_per_s"] = rate / c.get("full_rate_cycles", 2.28)
+        out["valu_instr_per_cell"] = c["valu_instr_per_cell"]
+    if traffic:
+        bpp = traffic / batch
+        out["hbm_bytes_per_pair"] = bpp
+        out["hbm_cap_pairs_per_s"] = HBM_MEASURED_GBS * 1e9 / bpp
+    return out
 
 
 def compute_roofline(gcups: float) -> dict | None:

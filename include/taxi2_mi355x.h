@@ -78,7 +78,8 @@ int taxi2_device_count(void);
 int taxi2_ctx_create(int device, taxi2_ctx** out);
 void taxi2_ctx_destroy(taxi2_ctx* ctx);
 const char* taxi2_last_error(const taxi2_ctx* ctx);
-/* Replaces nothing in the reference; reports the build (kernel variants, arch). */
+/* Replaces nothing in the reference; reports the build (kernel variants, arch) and ends in
+ * "src:<16 hex>", the hash of the sources it was built from (taxi2_amd/srchash.py). */
 const char* taxi2_version(void);
 
 /* ---- sequence sets ------------------------------------------------------------------ *

@@ -165,6 +165,18 @@ def version() -> str:
     return load_library().taxi2_version().decode()
 
 
+def build_info() -> dict:
+    """The loaded library's source hash (baked in at build time) beside the hash of the sources in
+    this tree (taxi2_amd/srchash.py): equal when the binary was built from these sources."""
+    from .srchash import src_hash
+
+    v = version()
+    lib_hash = v.rsplit("src:", 1)[1] if "src:" in v else None
+    tree = src_hash()
+    return {"lib_src_hash": lib_hash, "tree_src_hash": tree, "lib_matches_tree": lib_hash == tree,
+            "lib": str(LIB_PATH.relative_to(LIB_PATH.parent.parent.parent))}
+
+
 def to_cscores(scores) -> CScores:
     """``align.Scores`` / mapping / 6-tuple -> C struct (field order = Scores.defaults)."""
     if scores is None:

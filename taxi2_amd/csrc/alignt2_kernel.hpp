@@ -68,16 +68,16 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
     for (size_t k = threadIdx.x; k < bytes / 4; k += blockDim.x) w[k] = AT_POISON_LDS;
 }
 
-// 1: a step whose wave has no lane inside the trace band skips the trace-code arithmetic
-// (bit-identical).  Default 0 since round 3: with the raw-difference trace the skip's extra live
-// registers push the 80-VGPR shape into spilling (240 B scratch per lane, reloads that wait on the
-// trace stores), and the always-encode build measured 3.92e6 vs 3.57e6 pairs/s on the same box
-// (profiles/r3/ab_*.json; 128 / 96-VGPR builds of either form were slower still)
-#ifndef A2_SKIP_OUT_OF_BAND
-#define A2_SKIP_OUT_OF_BAND 0
-#endif
-// The same skip for the sign-digit trace (non-default scores, the 4-fill-wave shapes, the queued
-// pass): it keeps round 2's measured default there (2.73e6 vs 2.47e6 pairs/s on (8, 2))
+// Measured and settled (the experiment knobs are gone from the tree):
+// * the raw-difference trace always forms its bytes (a wave-uniform skip of out-of-band steps
+//   spilled at 80 VGPRs: 3.57e6 vs 3.92e6 pairs/s); the sign-digit trace (non-default scores, the
+//   4-fill-wave shapes, the queued pass) keeps round 2's skip (A2_SKIP_SIGN: 2.73e6 vs 2.47e6);
+// * Iy opens from the left column's best state B (Biopython's F = max(M, Ix): 4.02e6 vs 4.26e6);
+// * the Ix column updates stay in the cell loop (at the top of the step: 4.16e6 vs 4.29e6), with the
+//   per-column open constants from LDS (one uniform constant + column nB's: 4.11e6 vs 4.28e6);
+// * column k+1's M is formed before column k's new B (3 instead of 9 back-edge moves) and vector
+//   memory is drained before the last fill wave's step loop (4.47e6 -> 4.55e6);
+// * the best state is one v_pk_maximum3_f16 (BIAS16 below: 4.53e6 -> 4.74e6).
 #ifndef A2_SKIP_SIGN
 #define A2_SKIP_SIGN 1
 #endif
@@ -85,46 +85,9 @@ __device__ __forceinline__ void at_poison_lds(void* p, size_t bytes) {
 // 2 048 columns) keep the 2-byte sign-digit trace: on them the 4-byte raw trace measured 8 % slower
 // (1 200 / 1 500 / 2 000 bp: 8.1e5 / 6.5e5 / 4.7e5 vs 8.8e5 / 7.1e5 / 5.05e5 pairs/s,
 // profiles/r3/long_*.json)
-#ifndef A2_RAW_MAX_W
-#define A2_RAW_MAX_W 2
-#endif
+constexpr int A2_RAW_MAX_W = 2;
 template <int W, bool DEF>
 constexpr bool a2_raw() { return DEF && W <= A2_RAW_MAX_W; }
-// 1: in the best-open fill Iy opens from B of the left column too (the lane hand-off is then B, Iy);
-// 0: from F = max(M, Ix), Biopython's recurrence (hand-off F, Iy): a shorter left-to-right
-// dependency chain, but measured 4.02e6 vs 4.26e6 pairs/s on the same box (profiles/r3/ab_bopen_y)
-#ifndef A2_BOPEN_Y
-#define A2_BOPEN_Y 1
-#endif
-// 1: the best-open fill updates the Ix column state at the top of the step, while the row record
-// and the ring entry are in flight (it needs neither); measured 3 % slower (profiles/r3/ab_early_x)
-#ifndef A2_EARLY_X
-#define A2_EARLY_X 0
-#endif
-// 1: when column nB is the last slot of its lane (e.g. 1 000 bp with K = 8), the best-open fill adds
-// one uniform internal-open constant to columns 0..K-2 and reads only the last slot's constant from
-// LDS (K per-lane reads otherwise).  Measured: 4.11e6 vs 4.28e6 pairs/s in the cell loop, 4.25e6 vs
-// 4.16e6 on top of A2_EARLY_X (profiles/r3/ab_early_x, ab_uni_co): off
-#ifndef A2_UNI_CO
-#define A2_UNI_CO 0
-#endif
-// 1: the best-open (RAW) walks run the branch-free hop (walk_run_raw)
-#ifndef A2_WALK_BF
-#define A2_WALK_BF 1
-#endif
-// 1: the best-open fill forms column k+1's M from B(i-1, k) before column k's new B exists, so the
-// old B dies first and the new one takes its register: 3 instead of 9 v_mov per step at the loop's
-// back edge (2: on the column-0 fill wave only).  A2_MNEXT_WAIT: drain vector memory before each
-// fill wave's step loop -- with the new register assignment a scratch reload into a register the
-// last wave's loop writes was left in flight, and the wait for it (vmcnt(0), i.e. on the trace
-// stores too) sat inside every step.  Same-box A/B (profiles/r3/ab_mnext/): 4.47e6 (0) -> 4.51e6 (2)
-// -> 4.55e6 pairs/s (1 + wait); 1 without the wait 2.4 % slower than 0
-#ifndef A2_MNEXT
-#define A2_MNEXT 1
-#endif
-#ifndef A2_MNEXT_WAIT
-#define A2_MNEXT_WAIT 1
-#endif
 #ifndef TAXI2_AT2_CHUNK
 #define TAXI2_AT2_CHUNK 8
 #endif
@@ -136,16 +99,13 @@ constexpr int NEG16 = -16384;
 // ONE 32-bit v_add_u32 of the integer c_hi * 65536 + c_lo: no half leaves [0, 65535], so no carry
 // crosses between the halves.  v_add_u32 issues in 2.28 SIMD cycles, v_pk_add_u16 in 4.09
 // (profiles/r2/valu_peak.txt).
-// A2_MAX3 (default-score best-open fill): the bias is 20480 instead, so that every value the fill
+// The default-score best-open fill uses a bias of 20480 instead, so that every value the fill
 // can hold there -- the -16384 sentinel less a few opens up to the 1 024-column maximum, [4 000,
 // 24 000] biased -- is a positive NORMAL f16 bit pattern ([0x0400, 0x7BFF]), whose order as a float is
 // its order as an unsigned integer: the cell's best state is then ONE v_pk_maximum3_f16 (gfx950) of
 // (M, Ix, Iy) instead of two v_pk_max_u16.  Every other packed form keeps the same bias (the
 // range at_fits16 admits, [-16384 - small, 16383], still maps into [0, 65535]).
-#ifndef A2_MAX3
-#define A2_MAX3 1
-#endif
-constexpr int BIAS16 = A2_MAX3 ? 20480 : 32768;
+constexpr int BIAS16 = 20480;
 constexpr int AT_ESC = AT_DONE + 1;  // walk state: stepped outside the stored trace band
 constexpr uint32_t NEG16X2 = (uint32_t)(NEG16 + BIAS16) * 0x00010001u;  // -16384 biased, both halves
 
@@ -761,7 +721,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
         W_.ncol = ncol;
     };
     auto walk = [&](int pb, int budget, int target) {
-        if constexpr (RAW && A2_WALK_BF) walk_run_raw(pb, budget, target);
+        if constexpr (RAW) walk_run_raw(pb, budget, target);
         else walk_run(pb, budget, target);
     };
 
@@ -863,11 +823,6 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                 break;
             }
             const int nB = chs[cur].nB;
-            // column nB's slot in its lane (chain-uniform) and the internal Ix open as one add constant
-            const int knb = __builtin_amdgcn_readfirstlane((nB - 1) % K);
-            const uint32_t coi = pk_int(pk2(sc.io - dz, sc.io - dz));
-            (void)knb;
-            (void)coi;
 #ifdef TAXI2_GUARD
             {  // poison the row ring, the wave ring and this chain's trace buffer (see AT_OK)
                 at_poison_lds(xinfo, sizeof xinfo);
@@ -937,7 +892,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
             // One systolic step of a fill wave, specialised on the wave's role: FW = wave 0 (column-0
             // boundary from the row record, no ring read), HO = writes the ring to the next wave.  Per-step
             // uniform branches on w cost spilled SGPR masks (v_readlane) on every step.
-            auto step = [&](auto FW, auto HO, auto UNI, const int s) {
+            auto step = [&](auto FW, auto HO, const int s) {
                             // lane id recomputed (two v_mbcnt) rather than kept live across the chain
                             // loop: at 80 VGPRs it was spilled and reloaded from scratch every step
                             // (still so after the next-column M ordering: kept live, the step loop
@@ -951,29 +906,6 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                             const uint2 rec = xinfo[g & (XR - 1)];
                             uint2 o_ring = make_uint2(0u, 0u);
                             if constexpr (!decltype(FW)::value) o_ring = ring_in[(s + 1) & (RING - 1)];
-#if A2_EARLY_X
-                            if constexpr (RAW) {
-                                // best-open form: Ix(i, j) = max(B(i-1, j) + co_j, Ix(i-1, j)) needs no row
-                                // data, so the column updates run here while the row record and the ring
-                                // entry are in flight (in place: stX holds Ix of THIS row from now on; a
-                                // pair's first row sets it from the row-0 boundary itself, below)
-                                if constexpr (decltype(UNI)::value) {
-                                    // column nB is the lane's last (knb == K - 1, e.g. 1 000 bp with K = 8):
-                                    // columns 0..K-2 open with the internal score from one constant, the
-                                    // last from the per-lane LDS constant (the end-gap score on column nB)
-                                    const uint32_t cend = colc[K - 1][tq];
-    #pragma unroll
-                                    for (int k = 0; k < K - 1; ++k) stX[k] = as_u32(pmax(padd32(as_s2(stG[k]), coi), as_s2(stX[k])));
-                                    stX[K - 1] = as_u32(pmax(padd32(as_s2(stG[K - 1]), cend), as_s2(stX[K - 1])));
-                                } else {
-    #pragma unroll
-                                for (int k = 0; k < K; ++k) stX[k] = as_u32(pmax(padd32(as_s2(stG[k]), colc[k][tq]), as_s2(stX[k])));
-                                }
-                            }
-#endif
-                            uint32_t cend = 0u;
-                            if constexpr (RAW && decltype(UNI)::value && !A2_EARLY_X) cend = colc[K - 1][tq];
-                            (void)cend;
                             // trace band (a2_row_record): store iff (u16)(block - lo) <= hi - lo (covers
                             // j0 <= nB).  The lane mask is formed here, a whole cell block ahead of the
                             // store, so the exec-mask update there never waits on the compare.
@@ -1011,11 +943,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                     for (int k = 0; k < K; ++k) {
                                         const int g0 = sc.eo + sc.ee * (jb + k) - (jb + k + 1) * dz;
                                         stG[k] = (pk2b(g0, g0) & m) | (stG[k] & ~m);
-                                        // (early-X best-open form: stX already holds this row's Ix, which
-                                        // on a first row is B(0, j) + co_j)
-                                        const uint32_t x0 = (RAW && A2_EARLY_X) ? as_u32(padd32(as_s2(pk2b(g0, g0)), colc[k][tq]))
-                                                                                 : (NEG16X2 | ODD);
-                                        stX[k] = (x0 & m) | (stX[k] & ~m);
+                                        stX[k] = ((NEG16X2 | ODD) & m) | (stX[k] & ~m);
                                     }
                                     // diagonal of column j0 at row 1 = best of (0, j0 - 1), | 1
                                     // (best-open form: B(0, jb), plain)
@@ -1104,39 +1032,21 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
     #pragma unroll
                                     for (int k = 0; k < K; ++k) {
                                         const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
-                                        at_s2 M;
-                                        if constexpr (A2_MNEXT == 1 || (A2_MNEXT == 2 && decltype(FW)::value)) {
-                                            // the next column's M first: B(i-1, k) dies here, so column k's
-                                            // new B can take its register
-                                            M = Mk;
-                                            if (k + 1 < K) Mk = mcell(Bu, k + 1);
-                                        } else {
-                                            M = mcell(d1, k);
-                                        }
-#if A2_EARLY_X
-                                        const at_s2 Xn = Xu;  // updated at the top of the step
-#else
-                                        // Ix open of column j: one uniform constant except on column nB (UNI:
-                                        // the lane's last slot, its constant read once per step)
-                                        const at_s2 Xn = pmax(padd32(Bu, decltype(UNI)::value ? (k < K - 1 ? coi : cend) : colc[k][tq]), Xu);
-#endif
-                                        const at_s2 Fn = pmax(M, Xn);
-#if A2_BOPEN_Y
+                                        // the next column's M first: B(i-1, k) dies here, so column k's new B
+                                        // can take its register
+                                        const at_s2 M = Mk;
+                                        if (k + 1 < K) Mk = mcell(Bu, k + 1);
+                                        // Ix open of column j from LDS (the end-gap score on column nB)
+                                        const at_s2 Xn = pmax(padd32(Bu, colc[k][tq]), Xu);
                                         const at_s2 Yn = pmax(padd32(F1, oy1i), Y);  // Iy opens from B
-#else
-                                        // Iy opens from F = max(M, Ix) of the left column (Biopython's own
-                                        // recurrence, same values): the left-to-right dependency chain is then
-                                        // one maximum per column instead of add + two maxima through B
-                                        const at_s2 Yn = pmax(padd32(F1, oy1i), Y);
-#endif
                                         at_s2 Bn;
-                                        if constexpr (A2_MAX3 && DEF && A2_BOPEN_Y) {
+                                        if constexpr (DEF) {
                                             // max of three normal positive f16 patterns = their unsigned max
                                             uint32_t b3;
                                             asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(b3) : "v"(as_u32(M)), "v"(as_u32(Xn)), "v"(as_u32(Yn)));
                                             Bn = as_s2(b3);
                                         } else {
-                                            Bn = pmax(Fn, Yn);
+                                            Bn = pmax(pmax(M, Xn), Yn);
                                         }
                                         if constexpr (decltype(TR)::value) {
                                             // D1 = M - X, D2 = M - Y over both halves with 32-bit subtracts
@@ -1148,7 +1058,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                         d1 = Bu;
                                         stG[k] = as_u32(Bn);
                                         stX[k] = as_u32(Xn);
-                                        F1 = A2_BOPEN_Y ? Bn : Fn;
+                                        F1 = Bn;
                                         Y = Yn;
                                     }
                                 } else {
@@ -1197,7 +1107,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 }
                                 }
                                 };
-                                if ((RAW ? A2_SKIP_OUT_OF_BAND : A2_SKIP_SIGN) && !bmask) {
+                                if (!RAW && A2_SKIP_SIGN && !bmask) {
                                     cells(std::false_type{});
                                 } else {
                                 cells(std::true_type{});
@@ -1250,7 +1160,7 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                                 }
                             }
                             // best of (i, j0 - 1) (| 1 in the tagged forms): the next row's diagonal
-                            if constexpr (RAW) carry = A2_BOPEN_Y ? inF : as_u32(pmax(as_s2(inF), as_s2(inY)));
+                            if constexpr (RAW) carry = inF;
                             else carry = as_u32(pmax(as_s2(inF), as_s2(inY))) | 0x00010001u;
             };
 
@@ -1266,28 +1176,18 @@ alignt2_body(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, in
                     if (blk >= 0 && blk < nblk) {
                         const int s0 = blk * INTERVAL;
                         const int s1 = min(s0 + INTERVAL, nsteps);
-                        // uniform Ix-open constant when column nB is each lane's last slot (early-X
-                        // best-open form only; one step variant per wave role and layout)
-                        const bool uni = RAW && A2_UNI_CO && knb == K - 1;
-                        auto run = [&](auto UNI) {
+                        if (w == 0) {
+                            for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
+                        } else if (w == W - 1) {
                             // no vector memory in flight into the last wave's step loop (a scratch reload
                             // of a register it writes would cost a vmcnt(0) inside every step; gfx9
                             // encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  Only there: the same wait before
                             // every role's loop changes the register assignment and brings it back.
-                            auto drain = [] {
-                                if constexpr (A2_MNEXT_WAIT != 0) __builtin_amdgcn_s_waitcnt(0x0F70);
-                            };
-                            if (w == 0) {
-                                for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, UNI, s);
-                            } else if (w == W - 1) {
-                                drain();
-                                for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, UNI, s);
-                            } else {
-                                for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, UNI, s);
-                            }
-                        };
-                        if (uni) run(std::true_type{});
-                        else run(std::false_type{});
+                            __builtin_amdgcn_s_waitcnt(0x0F70);
+                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
+                        } else {
+                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::true_type{}, s);
+                        }
                     }
                 }
                 const int gpre = (it + 1) * INTERVAL + tid;

@@ -1013,9 +1013,14 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
 
 extern "C" {
 
+#ifndef TAXI2_SRC_HASH
+#define TAXI2_SRC_HASH "unknown"
+#endif
+// "... src:<hash>": TAXI2_SRC_HASH is taxi2_amd/srchash.py's hash of the sources the library was
+// built from (Makefile); bench.py and smoke() compare it with the hash of the tree they run in
 const char* taxi2_version(void) {
-    return "taxi2_mi355x 0.1 (gfx950; Gotoh K{4,6,8}xW{1,2,4,8} / NW K{4,8}xW{1,2,4,8}; "
-           "bit-plane pre-aligned counter)";
+    return "taxi2_mi355x 0.2 (gfx950; packed trace-and-walk Gotoh, column-tiled Gotoh / NW, "
+           "tiled bit-plane pre-aligned counter) src:" TAXI2_SRC_HASH;
 }
 
 int taxi2_device_count(void) {

@@ -42,9 +42,19 @@ from .common import (Results, console_report, create_parents, fixed_decimals, fo
 def walk_strings_ok(scores: tuple, seqs: list) -> bool:
     """Does the packed trace-and-walk aligner (which can write the aligned strings while its walks
     give the metrics) cover this run?  Gotoh scores (not every open == extend), pairs up to 2 048
-    columns, every DP difference within int16 (alignt2_kernel.hpp at_fits16, restated)."""
+    columns, every DP difference within int16 (alignt2_kernel.hpp at_fits16, restated), and the
+    same environment knobs that make the engine decline the shape (capi.hip launch_packed_strings).
+
+    Only all-ASCII sequences: the walkers copy sequence bytes straight into the aligned_pairs.txt
+    text, and the engine stores one latin-1 byte per character, while the reference writes str to a
+    UTF-8 text file (SequencePairHandler.Formatted) -- a character in U+0080..U+00FF must become two
+    bytes there, which the Python-formatted writer does."""
     ma, mi, io, ie, eo, ee = scores
     if io == ie and eo == ee:
+        return False
+    if any(os.environ.get(k) for k in ("TAXI2_NO_ALIGNT", "TAXI2_NO_PACKED", "TAXI2_LONG", "TAXI2_NO_WALK_STRINGS")):
+        return False
+    if not all(s.seq.isascii() for s in seqs):
         return False
     L = max((len(s.seq) for s in seqs), default=0)
     if L > 2048:
@@ -231,7 +241,7 @@ class VersusAll:
                 return out.reshape(count, 2 * M)
 
             walked = False
-            if pairs_fh is not None and cidx:
+            if pairs_fh is not None and cidx and walk_strings_ok(scores, seqs):
                 tri = self._tri_with_pairs_seq if os.environ.get("TAXI2_PAIRS_SEQ") else self._tri_with_pairs
                 walked = (tri(seqs, eng, st, D, cidx, clabels, scores, pairs_fh)
                           or self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh))

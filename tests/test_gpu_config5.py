@@ -31,7 +31,7 @@ def _bits(a):
 
 @pytest.mark.timeout(900)
 def test_config5_task_full_size(tmp_path, engine, oracle_c):
-    from tools.bench_config5_task import build_task
+    from bench_secondary import build_config5_task as build_task
 
     n, L = 200_000, 1000
     task, buf, offs = build_task(n, L, engine, tmp_path, 2.0)
@@ -62,7 +62,7 @@ def test_config5_task_full_size(tmp_path, engine, oracle_c):
 
 
 def test_streamed_subsets_exact_vs_dense(tmp_path, engine):
-    from tools.bench_config5_task import build_task
+    from bench_secondary import build_config5_task as build_task
 
     n, L = 4000, 600
     dense, _, _ = build_task(n, L, engine, tmp_path / "dense", 0.05)

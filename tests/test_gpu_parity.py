@@ -159,8 +159,13 @@ def test_align_edge_cases(engine, oracle_c):
         got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
         exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc, threads=1)
         assert_metrics_equal(got, exp)
-        nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
-        assert np.array_equal(gsc[nonempty], esc[nonempty])
+        assert np.array_equal(gsc, esc)  # empty sequences included: the end-gap score (restated)
+        # a pair with an empty side is the other sequence against one end gap: eo + ee (n - 1),
+        # 0 for two empty sequences (the restated fill's row / column 0, oracle/restatement.py _gotoh)
+        for k, (i, j) in enumerate(zip(a, b)):
+            ne = len(seqs[i]) + len(seqs[j])
+            if not seqs[i] or not seqs[j]:
+                assert gsc[k] == (0 if ne == 0 else sc[4] + sc[5] * (ne - 1)), (seqs[i], seqs[j], gsc[k])
     st.free()
 
 
@@ -194,6 +199,54 @@ def test_prealigned_samples_ca200(engine, oracle_c):
     exp, _ = oracle_c.batch(seqs, a, b, align=False, scores=SCORE_SETS["default"], metrics=("p", "jc", "k2p"))
     assert_metrics_equal(got, exp[:, 0, :], ("p", "jc", "k2p"))
     st.free()
+
+
+def test_prealigned_samples_ca2000(engine, oracle_c):
+    """The full samples/Taxi2test1_ca2000.tab (BASELINE.md's stand-in for the missing ca9000 of
+    config 2) pre-aligned, p / jc / k2p over all 1 999 000 unordered pairs against the oracle."""
+    from taxi2_amd.sequences import Sequences, SequenceHandler
+    from taxi2_amd._native import tri_pairs
+
+    seqs = [s.seq for s in Sequences.fromPath(GOLDEN / "samples" / "Taxi2test1_ca2000.tab",
+                                              SequenceHandler.Tabfile, idHeader="seqid", seqHeader="sequence")]
+    assert len(seqs) == 2000
+    st = engine.upload(seqs, align=False)
+    a, b = tri_pairs(len(seqs))
+    got = engine.all_pairs(st, 0, len(a), ("p", "jc", "k2p"))
+    exp, _ = oracle_c.batch(seqs, a, b, align=False, scores=SCORE_SETS["default"], metrics=("p", "jc", "k2p"),
+                            threads=16)
+    assert_metrics_equal(got, exp[:, 0, :], ("p", "jc", "k2p"))
+    assert_metrics_equal(got, exp[:, 1, :], ("p", "jc", "k2p"))
+    st.free()
+
+
+def test_config4_generator_rect_closest(engine, oracle_c):
+    """Config 4's generator (BASELINE.json configs[3]: 650 bp family sequences, references seed
+    0x7A13, queries 0x7A14, as bench_secondary.leg_config4) on a slice: every (query, reference)
+    pair's four metrics, and the closest reference + extras (versus_reference.py:119-129, 184-188)
+    against the oracle."""
+    from taxi2_amd.synth import family_sequences
+
+    refs = family_sequences(400, 650, 0x7A13)
+    qs_ = family_sequences(24, 650, 0x7A13 + 1)
+    sq = engine.upload(qs_, align=True)
+    sr = engine.upload(refs, align=True)
+    sc = SCORE_SETS["default"]
+    got = engine.rect_pairs(sq, sr, 0, len(qs_), METRICS, sc)
+    pa = np.repeat(np.arange(len(qs_)), len(refs))
+    pb = np.tile(np.arange(len(refs)), len(qs_)) + len(qs_)
+    exp, _ = oracle_c.batch(qs_ + refs, pa, pb, align=True, scores=sc, threads=16)
+    assert_metrics_equal(got, exp[:, 0, :])
+    idx, d, ex, _ = engine.closest(sq, sr, 0, len(qs_), "p", ("p-gaps", "jc", "k2p"), sc)
+    prim = exp[:, 0, 0].reshape(len(qs_), len(refs))
+    for k in range(len(qs_)):
+        row = prim[k]
+        ok = np.isfinite(row)
+        j = int(np.nonzero(ok & (row == row[ok].min()))[0][0])
+        assert idx[k] == j and d[k] == row[j]
+        assert_metrics_equal(ex[k][None, :], exp[k * len(refs) + j, 0, 1:][None, :], ("p-gaps", "jc", "k2p"))
+    sq.free()
+    sr.free()
 
 
 # ----------------------------------------------------------------------------- rect / closest
@@ -347,8 +400,7 @@ def test_chained_pairs(engine, oracle_c, chunk):
         one = _with_env("TAXI2_A1_NOCHAIN", "1", lambda: engine.all_pairs(st, 0, len(a), METRICS, sc))
         exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
         assert_metrics_equal(got, exp)
-        nonempty = np.array([len(seqs[i]) > 0 and len(seqs[j]) > 0 for i, j in zip(a, b)])
-        assert np.array_equal(gsc[nonempty], esc[nonempty])
+        assert np.array_equal(gsc, esc)  # empty sequences included: the end-gap score (restated)
         assert np.array_equal(np.nan_to_num(got, nan=9.0), np.nan_to_num(one, nan=9.0))
     # an offset block of the triangle (chunks start mid-row)
     k0, cnt = 40, 61

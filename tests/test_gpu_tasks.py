@@ -139,13 +139,19 @@ def test_versus_all_config1(tmp_path, engine, oracle_c):
     assert (tmp_path / "out/distances/matricial/p.tsv").read_text() == mats["p"].read_text()
 
 
-def test_versus_all_aligned_pairs_file(tmp_path, engine):
+@pytest.mark.parametrize("latin1", [False, True])
+def test_versus_all_aligned_pairs_file(tmp_path, engine, latin1):
+    """aligned_pairs.txt file-exact against the restatement; with a latin-1 character in a
+    sequence the file must stay the reference's UTF-8 text (the walk-strings path,
+    which copies single latin-1 bytes, is gated off for it: versus_all.walk_strings_ok)."""
     from oracle import restatement as R
     from taxi2_amd.pairs import SequencePair, SequencePairHandler
     from taxi2_amd.sequences import Sequence, Sequences
     from taxi2_amd.tasks import VersusAll
 
     seqs = [Sequence(s.id, s.seq[:80], s.extras) for s in read_tab("Taxi2test1_10.tab")[:5]]
+    if latin1:
+        seqs[2] = Sequence(seqs[2].id, seqs[2].seq[:30] + "é" + seqs[2].seq[30:], seqs[2].extras)
     task = VersusAll()
     task.engine = engine
     task.progress_handler = None
@@ -159,7 +165,9 @@ def test_versus_all_aligned_pairs_file(tmp_path, engine):
                 xn, yn = x.normalize(), y.normalize()
                 ax, ay, _ = R.align(xn.seq, yn.seq)
                 fh.write(SequencePair(Sequence(x.id, ax), Sequence(y.id, ay)))
-    assert (tmp_path / "out/align/aligned_pairs.txt").read_text() == exp.read_text()
+    got = (tmp_path / "out/align/aligned_pairs.txt").read_bytes()
+    assert got == exp.read_bytes()
+    got.decode("utf-8")  # valid UTF-8
 
 
 def test_versus_all_prealigned_ca200(tmp_path, engine, oracle_c):

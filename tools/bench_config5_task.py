@@ -26,44 +26,9 @@ sys.path.insert(0, str(ROOT))
 
 
 def build_task(n: int, L: int, eng, out: Path, block_gb: float, aligned: bool = False):
-    import numpy as np
+    from bench_secondary import build_config5_task
 
-    from taxi2_amd.distances import DistanceMetric
-    from taxi2_amd.partitions import Partition
-    from taxi2_amd.sequences import Sequence, Sequences
-    from taxi2_amd.tasks import VersusAll
-    from tools.bench_configs import prealigned_rows
-
-    if aligned:  # the config-3 generator: Gotoh alignment of every pair
-        from taxi2_amd.synth import family_sequences
-
-        buf = offs = None
-        seqs = [Sequence(f"s{k}", s) for k, s in enumerate(family_sequences(n, L, 0x7A12))]
-    else:
-        buf, offs = prealigned_rows(n, L, 0x7A14)
-        raw = buf[:-1].reshape(n, L)
-        seqs = [Sequence(f"s{k}", raw[k].tobytes().decode()) for k in range(n)]
-    rng = np.random.default_rng(0x7A15)
-    t = VersusAll()
-    t.engine, t.progress_handler, t.work_dir = eng, None, out
-    t.input.sequences = Sequences(seqs)
-    # two genera (the few-subsets case that used to serialise the sums) and ~1 000 species
-    t.input.genera = Partition({s.id: "g%d" % (k % 2) for k, s in enumerate(seqs)})
-    t.input.species = Partition({s.id: "sp%d" % int(rng.integers(0, 1000)) for s in seqs})
-    t.params.pairs.align = aligned
-    t.params.pairs.write = False
-    t.params.distances.write_linear = t.params.distances.write_matricial = False
-    t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.JukesCantor(),
-                                  DistanceMetric.Kimura2P()]
-    if aligned:
-        t.params.distances.metrics.insert(1, DistanceMetric.UncorrectedWithGaps())
-    t.params.format.percentage_multiply = True
-    t.params.engine.stream = True
-    t.params.engine.write_summary = False
-    t.params.engine.row_minima = "p"
-    t.params.engine.block_bytes = int(block_gb * (1 << 30))
-    t.params.engine.timings = True
-    return t, buf, offs
+    return build_config5_task(n, L, eng, out, block_gb, aligned)
 
 
 def main() -> None:

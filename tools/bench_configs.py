@@ -32,17 +32,9 @@ sys.path.insert(0, str(ROOT))
 
 
 def prealigned_rows(n: int, L: int, seed: int) -> tuple[np.ndarray, np.ndarray]:
-    from taxi2_amd.synth import family_codes
+    from bench_secondary import prealigned_rows as rows
 
-    rng = np.random.default_rng(seed)
-    codes = family_codes(n, L, seed, ancestors=64)
-    rows = np.frombuffer(b"acgt", dtype=np.uint8)[codes].copy()
-    gap = rng.random((n, L)) < 0.01
-    gap |= np.roll(gap, 1, axis=1)  # short runs
-    rows[gap] = ord("-")
-    rows[rng.random((n, L)) < 0.005] = ord("n")
-    buf = np.concatenate([rows.reshape(-1), np.zeros(1, np.uint8)])
-    return buf, np.arange(n + 1, dtype=np.int64) * L
+    return rows(n, L, seed)
 
 
 def config2(eng, steps: int) -> dict:

@@ -1,0 +1,89 @@
+#!/bin/bash
+# One runner for every GPU-box job of this repo (replaces round 1-3's one-off check scripts).
+#   gpurun --timeout 1200 -- 'bash tools/gpu_run.sh TAG STEP [STEP ...]'
+# Outputs go to gpurun_out/TAG/.  Each STEP runs under its own time limit; the steps are chained
+# and the runner stops at the first failure (no GPU step after a fault, abort or timeout).
+# Steps:
+#   suite            python -m pytest tests -m gpu (the driver's round-end command)
+#   tests:F1,F2      those test files only (tests/F.py), e.g. tests:test_gpu_alignt,test_gpu_band
+#   smoke            __graft_entry__.smoke()
+#   bench            bench.py (default settings: headline + secondary legs)
+#   headline         bench.py --secondary '' --steps 10 --warmup 2
+#   ab:LIBA,LIBB,R   R alternations of the headline with TAXI2_LIB=LIBA then LIBB (same box A/B)
+#   trace            rocprofv3 --kernel-trace --stats of the headline bench
+#   pmc_valu | pmc_fetch | pmc_write | pmc_lds
+#                    one rocprofv3 --pmc pass each over one bench launch (separate runs: rocprofv3
+#                    does not split counters over passes)
+#   guard            the poisoning guard build (make guard) on the packed aligner suites
+#   peak             tools/valu_peak (SIMD cycles per wave64 instruction)
+#   tool:SCRIPT      python tools/SCRIPT.py (bench tools), e.g. tool:bench_long
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:?tag}
+shift
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+BENCH="python3 $R/bench.py --secondary= --no-cpu-baseline"
+PMC_OPTS="--kernel-include-regex k_align --output-format csv"
+
+run_step() {
+    local s=$1
+    case "$s" in
+    suite)
+        (cd "$R" && timeout -k 10 1000 $PYT tests -m gpu > "$OUT/suite.log" 2>&1) ;;
+    tests:*)
+        local files=""
+        for f in $(echo "${s#tests:}" | tr ',' ' '); do files="$files tests/$f.py"; done
+        (cd "$R" && timeout -k 10 900 $PYT $files > "$OUT/tests_$(echo "${s#tests:}" | tr ',' '_').log" 2>&1) ;;
+    smoke)
+        (cd "$R" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1) ;;
+    bench)
+        (cd "$R" && timeout -k 10 600 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err") ;;
+    headline)
+        (cd "$R" && timeout -k 10 300 python3 -u bench.py --secondary= --steps 10 --warmup 2 > "$OUT/headline.json" 2> "$OUT/headline.err") ;;
+    ab:*)
+        IFS=, read -r la lb reps <<< "${s#ab:}"
+        for r in $(seq 1 "${reps:-2}"); do
+            (cd "$R" && TAXI2_LIB=$la timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_a_$r.json" 2> "$OUT/ab_a_$r.err") || return $?
+            (cd "$R" && TAXI2_LIB=$lb timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_b_$r.json" 2> "$OUT/ab_b_$r.err") || return $?
+        done ;;
+    trace)
+        (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+            $BENCH --steps 10 --warmup 2 > "$OUT/trace_bench.json" 2> "$OUT/trace.err") ;;
+    pmc_valu)
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE $PMC_OPTS -d "$OUT/pmc_valu" -o run -- \
+            $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_valu.err") ;;
+    pmc_lds)
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM \
+            SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE $PMC_OPTS -d "$OUT/pmc_lds" -o run -- \
+            $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_lds.err") ;;
+    pmc_fetch)
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE $PMC_OPTS -d "$OUT/pmc_fetch" -o run -- \
+            $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_fetch.err") ;;
+    pmc_write)
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE $PMC_OPTS -d "$OUT/pmc_write" -o run -- \
+            $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_write.err") ;;
+    guard)
+        (cd "$R" && TAXI2_LIB=libtaxi2_mi355x_guard.so timeout -k 10 900 $PYT tests/test_gpu_alignt.py \
+            tests/test_gpu_band.py tests/test_gpu_regress.py > "$OUT/guard.log" 2>&1) ;;
+    peak)
+        timeout -k 10 180 "$R/tools/valu_peak" > "$OUT/valu_peak.txt" 2>&1 ;;
+    tool:*)
+        (cd "$R" && timeout -k 10 900 python3 -u "tools/${s#tool:}.py" > "$OUT/${s#tool:}.json" 2> "$OUT/${s#tool:}.err") ;;
+    *)
+        echo "unknown step $s" >&2; return 2 ;;
+    esac
+}
+
+for s in "$@"; do
+    echo "[gpu_run $TAG] $s" >&2
+    run_step "$s"
+    rc=$?
+    echo "[gpu_run $TAG] $s rc=$rc" >&2
+    if [ $rc -ne 0 ]; then
+        exit $rc
+    fi
+done
