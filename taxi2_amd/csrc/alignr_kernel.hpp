@@ -1,0 +1,586 @@
+// Row-shared packed aligner (default scores): the packed trace-and-walk fill of alignt2_kernel.hpp
+// with the two 16-bit halves of every register holding two pairs that share their ROW sequence
+// instead of their column sequence.
+//
+// Why.  In k_alignt2 a lane's two halves are two different row sequences against the same column
+// sequence, so the substitution score of a cell pair needs a v_perm per column (the two halves'
+// fields come from two different table rows) -- one of the ten VALU instructions per column pair,
+// and a 4.09-cycle one.  Here the halves are two column sequences x0, x1 against one row sequence
+// y: the table word eqt[base(y_i)][lane][k] already holds (s(x0_k, y_i), s(x1_k, y_i)), so M is one
+// 32-bit add of an LDS word, and everything per row (the record, first / last row, the row byte,
+// the end-gap Iy open) is ONE value for both halves.
+//
+// Column shift.  Half h's columns are shifted right by off_h = (K - nB_h % K) % K virtual
+// columns, so that its last column nB_h sits in the last slot of its lane.  Then the Ix open
+// constant is the internal one on every slot but the last (an inline constant: no per-column LDS
+// constants), and column nB's readout is slot K - 1 (no dynamic select).  The off_h leading
+// "pre-columns" reproduce the column-0 boundary exactly: with default scores in drift coordinates
+// (cells hold V(i, j) - (i + j) ie) the boundary is B(i, 0) = 0, Iy(i, 0) = -inf, and a pre-column
+// with substitution 0 and the internal open keeps B = 0 on every row (M = B(i-1, c-1) + 0 = 0,
+// Ix <= -7, Iy = the row's Iy open <= 0), while its Iy = oy reaches the first real column as the
+// same Iy(i, 1) = max(B(i, 0) + oy, Iy(i, 0)) = oy the boundary gives.
+//
+// Work.  The host cuts the launch's pairs into segments of (x0, x1, consecutive y) with both pairs
+// (x_h, y) in the launch (x1 = -1: one pair per unit, the other half idle); a unit = one y and its
+// one or two pairs.  A chain = up to AR_UNITS consecutive units of one segment: the units' rows
+// stream back to back through the systolic layout of alignt2_kernel.hpp (two fill waves, one
+// walker wave, raw-difference trace, best-open fill, the f16 maximum3 best state).  Walks, trace
+// band, escape queue and the walkers' score check are alignt2_kernel.hpp's; queued pairs are redone
+// by k_alignt2_queued over the launch's PairSrc (the pair indices are the same).
+#pragma once
+#include "alignt2_kernel.hpp"
+
+namespace taxi2 {
+
+constexpr int AR_UNITS = 4;  // units (row sequences, up to two pairs each) per chain
+
+// Host-built segment: units u0 .. u0 + nb - 1 are (x0, x1, y = b0 + (u - u0)); pair (x_h, y) has
+// launch index p_h + (u - u0) (x1 = -1, p1 = -1: one pair per unit).
+struct ArSeg {
+    int64_t x0, x1, b0, nb, p0, p1, u0, pad;
+};
+
+struct ArRow {  // one unit of a chain: its row sequence and pairs
+    const uint8_t* rseq;
+    int64_t p[2];  // launch index of pair (x_h, y); -1: idle half
+    int nA, fx, lx, r0;
+};
+struct ArChain {
+    const uint8_t* cseq[2];
+    int nB[2], fy[2], ly[2], off[2];
+    int n;
+};
+struct ArWalk {
+    int i, j, st, first, t, h, prio;
+    uint32_t xa, yb;
+    int valid, ts, tv, gap, sc2, ncol;
+};
+
+// Row record (LDS, one per chain row): .x = byte offset of the row base's table (eqt) for an
+// A/C/G/T byte, .y = band lo (byte 0) and width (byte 1) in lanes, the row byte (byte 2) and flags.
+constexpr uint32_t AR_PRE = 1u << 31;    // first row of a unit or a byte other than A/C/G/T
+constexpr uint32_t AR_LAST = 1u << 30;   // last row of a unit
+constexpr uint32_t AR_FIRST = 1u << 29;  // first row of a unit
+constexpr uint32_t AR_OTHER = 1u << 28;  // byte other than A/C/G/T (byte-compare substitution)
+constexpr uint32_t AR_NOBAND = 0x0080u;  // lo 128, width 0: no lane stores
+
+// Default scores in drift coordinates (dz = ie = -1): substitution ma - 2 dz / mi - 2 dz, opens
+// relative to the extend, the column-0 / row-0 boundary 0.
+constexpr int AR_EQ_MATCH = 3, AR_EQ_MISMATCH = 1, AR_CO_I = -7, AR_CO_E = 0;
+
+__device__ __forceinline__ uint32_t ar_pk_int(int lo, int hi) { return pk_int(pk2(lo, hi)); }
+
+// band lanes [lo, hi] of row i (1-based) of a pair with nA rows and nB columns, shifted by off;
+// lo > hi: none (a2_band_blocks in virtual columns)
+__device__ __forceinline__ void ar_band_lanes(int i, int nA, int nB, int off, int band, int K, int& lo, int& hi) {
+    int jl, jh;
+    if (band <= 0) {
+        jl = 1;
+        jh = nB;
+    } else {
+        jl = max(1, i + min(0, nB - nA) - band);
+        jh = min(nB, i + max(0, nB - nA) + band);
+    }
+    lo = (jl + off - 1) / K;
+    hi = (jh + off - 1) / K;
+}
+
+template <int K, int W>
+__device__ __forceinline__ uint2 ar_row_record(const ArRow* __restrict__ tab, const ArChain& ch, int n, int rows, int g,
+                                               int band) {
+    constexpr int NT = 64 * W;
+    if (g < 0 || g >= rows) return make_uint2(0u, AR_NOBAND);
+    int t = 0;
+    for (int q = 1; q < n; ++q)
+        if (tab[q].r0 <= g) t = q;
+    const ArRow& r = tab[t];
+    const int i = g - r.r0;  // 0-based row of the unit
+    const uint32_t c = r.rseq[i];
+    const uint32_t ec = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+    uint32_t y = c << 16;
+    uint32_t x = 0u;
+    if (ec < 4u) x = ec * (uint32_t)(NT * K * 4);
+    else y |= AR_OTHER | AR_PRE;
+    if (i == 0) y |= AR_FIRST | AR_PRE;
+    if (i == r.nA - 1) y |= AR_LAST;
+    int lo = 0x7FFF, hi = -1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (r.p[h] < 0) continue;
+        int l, u;
+        ar_band_lanes(i + 1, r.nA, ch.nB[h], ch.off[h], band, K, l, u);
+        lo = min(lo, l);
+        hi = max(hi, u);
+    }
+    y |= hi < lo ? AR_NOBAND : ((uint32_t)lo | ((uint32_t)(hi - lo) << 8));
+    return make_uint2(x, y);
+}
+
+template <int K, int W, int OCC>
+__global__ void __launch_bounds__(64 * (W + 1), OCC)
+k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64_t total, int64_t npairs,
+         MetricSpec ms, int chunk_req, int out_mode, double* __restrict__ out, int32_t* __restrict__ sout,
+         uint8_t* __restrict__ trace, int64_t buf_bytes, int cap_rows, unsigned long long* __restrict__ next,
+         int band, int64_t* __restrict__ esc_list, unsigned long long* __restrict__ esc_n, StrOut so) {
+    static_assert(K % 2 == 0 && K <= 8 && W <= 2, "row-shared shapes: K <= 8 columns per lane, one or two fill waves");
+    constexpr int TB = 4 * K;  // trace bytes per lane and step: (D1 lo, D1 hi, D2 lo, D2 hi) per slot
+    constexpr int NT = 64 * W;
+    constexpr int XR = a1c_xr(W);
+    constexpr int dz = -1;                          // default scores: ie
+    const KScores sc{1, -1, -8, -1, -1, -1};        // align.py:20-27 defaults
+    constexpr int NW = 4 * AR_UNITS;                // walks per chain (both orientations of 2 pairs per unit)
+    __shared__ uint2 xinfo[XR];
+    __shared__ ArRow tab[2][AR_UNITS];
+    __shared__ ArChain chs[2];
+    __shared__ int fin[2][AR_UNITS][2];
+    __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * RING];
+    __shared__ uint32_t eqt[4][NT][K];  // (s(x0_k, base), s(x1_k, base)) as pk_int, per lane and slot
+    __shared__ int64_t s_qc, s_qend;
+    __shared__ int s_n, s_rows, s_seg;
+    __shared__ int s_fill;
+    __shared__ ArWalk wks[NW];
+    __shared__ int escf[2][AR_UNITS][2];
+
+    const int tid = (int)threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool walker = w == W;
+    const int nm = ms.n;
+    const int64_t chunk = chunk_req >= 1 ? min((int64_t)chunk_req, (int64_t)AR_UNITS)
+                                         : max((int64_t)1, min((int64_t)AR_UNITS, total / ((int64_t)gridDim.x * 8)));
+    uint8_t* const bufs = trace + (size_t)blockIdx.x * 2 * (size_t)buf_bytes;
+    if (tid == 0) {
+        s_qc = 0;
+        s_qend = 0;
+        s_seg = 0;
+    }
+    int cur = 0, prev_n = 0;
+
+    // outputs of a pair with an empty side (no fill): metrics of no columns, the end-gap score,
+    // the other sequence against gaps as its alignment (both orientation slots alike)
+    auto empty_pair = [&](int64_t p, const uint8_t* xs_, int lx_, const uint8_t* ys_, int ly_) {
+        for (int m = 0; m < nm; ++m) {
+            const double v = metric_value(ms.code[m], 0u, 0u, 0u, 0u);
+            if (out_mode == OUT_BOTH) {
+                out[(p * 2 + 0) * nm + m] = v;
+                out[(p * 2 + 1) * nm + m] = v;
+            } else {
+                out[p * nm + m] = v;
+            }
+        }
+        const int ne = lx_ + ly_;
+        if (sout) sout[p] = ne == 0 ? 0 : sc.eo + sc.ee * (ne - 1);
+        if (so.sx) {
+            for (int o = 0; o < so.nslot; ++o) {
+                uint8_t* ox = so.sx + ((size_t)p * so.nslot + o) * (size_t)so.cap;
+                uint8_t* oy = so.sy + ((size_t)p * so.nslot + o) * (size_t)so.cap;
+                for (int t = 0; t < ne; ++t) {
+                    ox[t] = lx_ ? xs_[t] : (uint8_t)'-';
+                    oy[t] = ly_ ? ys_[t] : (uint8_t)'-';
+                }
+                so.slen[p * so.nslot + o] = ne;
+            }
+        }
+    };
+
+    // walk slot q of the chain in buffer pb: unit q % n, half (q / n) & 1, orientation q / 2n (both)
+    auto walk_init = [&](int pb, int n) {
+        if (lane >= NW) return;
+        ArWalk& W_ = wks[lane];
+        W_ = ArWalk{0, 0, AT_DONE, 0, 0, 0, 0, 0u, 0u, 0, 0, 0, 0, 0, 0};
+        if (lane < AR_UNITS * 2) escf[pb][lane >> 1][lane & 1] = 0;
+        const int nw = (out_mode == OUT_BOTH ? 4 : 2) * n;
+        if (lane < nw) {
+            const int t = lane % n, h = (lane / n) & 1, o = lane / (2 * n);
+            const ArRow& r = tab[pb][t];
+            if (r.p[h] >= 0) {
+                W_.t = t;
+                W_.h = h;
+                // rows = y, the pair's second sequence: orientation A (prio 0) is (y, x) = slot 1
+                W_.prio = out_mode == OUT_BOTH ? o : 1;
+                W_.i = r.nA + 1;
+                W_.j = chs[pb].nB[h] + 1;
+                W_.st = AT_M;
+                W_.first = 1;
+            }
+        }
+    };
+
+    // branch-free best-open walker (alignt2_kernel.hpp walk_run_raw), per-half column sequence and
+    // shift; hops until the fill waves signal `target` interval completions (target 0: to the end)
+    auto walk = [&](int pb, int target) {
+        ArWalk& W_ = wks[lane < NW ? lane : 0];
+        int st = lane < NW ? W_.st : AT_DONE;
+        if (!__any(st != AT_DONE)) return;
+        const int t = W_.t, h = W_.h, prio = W_.prio;
+        const ArRow& r = tab[pb][t];
+        const ArChain& ch = chs[pb];
+        const int nA_ = r.nA, nB_ = ch.nB[h], off = ch.off[h];
+        const int fx = r.fx, lx = r.lx, fy = ch.fy[h], ly = ch.ly[h], r0 = r.r0;
+        const int64_t p = r.p[h];
+        const int bdl = min(0, nB_ - nA_) - band;
+        const uint32_t bwd = (uint32_t)(abs(nB_ - nA_) + 2 * band);
+        const uint8_t* rs = r.rseq;
+        const uint8_t* cs = ch.cseq[h];
+        const uint8_t* trb = bufs + (size_t)pb * (size_t)buf_bytes;
+        int i = W_.i, j = W_.j, first = W_.first;
+        uint32_t xa = W_.xa, yb = W_.yb;
+        int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap, sc2 = W_.sc2, ncol = W_.ncol;
+        const int co_i = sc.io - sc.ie, co_e = sc.eo - sc.ee;
+        const int bsh = h ? 8 : 0;
+        const int oslot = prio ^ 1;  // swp = 1: rows are the pair's second sequence
+        for (;;) {
+            if (!__any(st < AT_DONE)) break;
+            if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+            if (st < AT_DONE) {
+                const bool isM = st == AT_M, isX = st == AT_IX, isY = st == AT_IY;
+                const uint32_t bx = a2_wcode(xa), by = a2_wcode(yb);
+                const uint32_t dd = bx ^ by;
+                const bool cnt = isM && !first && (bx | by) < 4u;
+                valid += cnt;
+                ts += cnt && dd == 3u;
+                tv += cnt && (dd == 1u || dd == 2u);
+                gap += (isX && bx < 4 && j - 1 >= fy && j <= ly) || (isY && by < 4 && i - 1 >= fx && i <= lx);
+                sc2 += (isM && !first) ? (xa == yb ? sc.ma : sc.mi) : 0;
+                const int ni = isY ? i : i - 1, nj = isX ? j : j - 1;
+                if (so.sx && !first) {  // this column of the alignment, right to left, (x, y) order
+                    const uint32_t rc = isY ? (uint32_t)'-' : xa, cc = isX ? (uint32_t)'-' : yb;
+                    const size_t o = ((size_t)p * so.nslot + (oslot & (so.nslot - 1))) * (size_t)so.cap +
+                                     (size_t)(nA_ + nB_ - 1 - ncol);
+                    so.sx[o] = (uint8_t)cc;
+                    so.sy[o] = (uint8_t)rc;
+                    ++ncol;
+                }
+                first = 0;
+                if (ni == 0 && nj == 0) {
+                    if (!isM) sc2 += sc.eo;
+                    if (sc2 != fin[pb][t][h] + (nA_ + nB_) * dz) {
+                        st = AT_ESC;
+                    } else {
+                        double* o = out_mode == OUT_BOTH ? out + (p * 2 + oslot) * nm : out + p * nm;
+                        for (int m = 0; m < nm; ++m)
+                            o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
+                        if (sout && (out_mode != OUT_BOTH || oslot == 0)) sout[p] = fin[pb][t][h] + (nA_ + nB_) * dz;
+                        if (so.slen) so.slen[p * so.nslot + (oslot & (so.nslot - 1))] = ncol;
+                        st = AT_DONE;
+                    }
+                } else {
+                    const bool in = ni >= 1 && nj >= 1;
+                    const bool esc = in && band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
+                    const int cj = max(nj, 1) - 1 + off, ci = max(ni, 1) - 1;  // virtual column of (ni, nj) - 1
+                    const uint32_t tl = (uint32_t)cj / K, k = (uint32_t)cj - tl * K;
+                    const uint32_t toff = (((uint32_t)(r0 + ci) + (tl & 63u)) * (uint32_t)NT + tl) * (uint32_t)TB + 4u * k;
+                    const uint32_t xa_ = a2_load_byte(rs + ci), yb_ = a2_load_byte(cs + max(nj, 1) - 1);
+                    const uint32_t nb = a2_load_trace32(trb + toff);
+                    xa = ni >= 1 ? xa_ : 0u;
+                    yb = nj >= 1 ? yb_ : 0u;
+                    const int d1v = (int)(int8_t)(uint8_t)((nb >> bsh) + (h ? ((nb >> 7) & 1u) : 0u));
+                    const int d2v = (int)(int8_t)(uint8_t)((nb >> (16 + bsh)) + (h ? ((nb >> 23) & 1u) : 0u));
+                    const int co = j == nB_ ? co_e : co_i, oy = i == nA_ ? co_e : co_i;
+                    const int vM = d1v + (isX ? co : 0);
+                    const int vY = d1v - d2v + (isX ? co : isY ? -oy : 0);
+                    const int vm = max(max(vM, vY), 0);
+                    int nst = vM == vm ? AT_M : prio ? (vY == vm ? AT_IY : AT_IX) : (vm == 0 ? AT_IX : AT_IY);
+                    nst = ni == 0 ? AT_IY : nj == 0 ? AT_IX : nst;
+                    const bool ext = isX ? nst == AT_IX : nst == AT_IY;
+                    const bool en = isX ? (j == nB_ || j == 0) : (i == nA_ || i == 0);
+                    sc2 += isM ? 0 : ext ? (en ? sc.ee : sc.ie) : (en ? sc.eo : sc.io);
+                    i = ni;
+                    j = nj;
+                    st = esc ? AT_ESC : nst;
+                }
+            }
+        }
+        if (st == AT_ESC) {  // queue the pair (once) for the full-trace pass (k_alignt2_queued)
+            if (atomicOr(&escf[pb][t][h], 1) == 0 && esc_list) esc_list[atomicAdd(esc_n, 1ull)] = p;
+            st = AT_DONE;
+        }
+        if (lane >= NW) return;
+        W_.i = i;
+        W_.j = j;
+        W_.st = st;
+        W_.first = first;
+        W_.xa = xa;
+        W_.yb = yb;
+        W_.valid = valid;
+        W_.ts = ts;
+        W_.tv = tv;
+        W_.gap = gap;
+        W_.sc2 = sc2;
+        W_.ncol = ncol;
+    };
+
+    auto chain_loop = [&](auto WK) {
+        constexpr bool IS_W = decltype(WK)::value;
+        for (;;) {
+            // ---- cut the next chain (thread 0): up to AR_UNITS units of one segment
+            __syncthreads();
+            if (!IS_W && tid == 0) {
+                int n = 0, rows = 0;
+                while (n == 0) {
+                    if (s_qc >= s_qend) {
+                        const int64_t q0 = (int64_t)atomicAdd(next, (unsigned long long)chunk);
+                        if (q0 >= total) break;
+                        s_qc = q0;
+                        s_qend = min(q0 + chunk, total);
+                        // segment of unit q0 (binary search; units run in segment order)
+                        int lo = 0, hi = nseg - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (segs[mid].u0 <= q0) lo = mid;
+                            else hi = mid - 1;
+                        }
+                        s_seg = lo;
+                    }
+                    int64_t q = s_qc;
+                    for (; q < s_qend; ++q) {
+                        int sg = s_seg;
+                        while (sg + 1 < nseg && segs[sg + 1].u0 <= q) ++sg;
+                        if (n > 0 && sg != s_seg) break;  // a chain keeps one segment's columns
+                        s_seg = sg;
+                        const ArSeg S = segs[sg];
+                        const int64_t du = q - S.u0;
+                        const int64_t b = S.b0 + du;
+                        const int4 mb = YS.meta[b];
+                        const uint8_t* yb_ = YS.bytes + YS.offs[b];
+                        const int64_t xh[2] = {S.x0, S.x1};
+                        const int64_t ph[2] = {S.p0 + du, S.x1 >= 0 ? S.p1 + du : -1};
+                        int4 mx[2];
+                        const uint8_t* xs_[2];
+                        bool live[2];
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) {
+                            live[hh] = xh[hh] >= 0;
+                            if (live[hh]) {
+                                mx[hh] = XS.meta[xh[hh]];
+                                xs_[hh] = XS.bytes + XS.offs[xh[hh]];
+                                if (mx[hh].x == 0 || mb.x == 0) {  // an empty side: outputs now, no fill
+                                    empty_pair(ph[hh], xs_[hh], mx[hh].x, yb_, mb.x);
+                                    live[hh] = false;
+                                }
+                            }
+                        }
+                        if (!live[0] && !live[1]) continue;
+                        if (n > 0 && rows + mb.x > cap_rows) break;
+                        if (n == 0) {
+                            ArChain& c = chs[cur];
+#pragma unroll
+                            for (int hh = 0; hh < 2; ++hh) {
+                                const bool on = xh[hh] >= 0;
+                                const int4 m = on ? XS.meta[xh[hh]] : make_int4(0, 0, 0, 0);
+                                c.cseq[hh] = on ? XS.bytes + XS.offs[xh[hh]] : XS.bytes;
+                                c.nB[hh] = m.x;
+                                c.fy[hh] = m.y;
+                                c.ly[hh] = m.z;
+                                c.off[hh] = m.x > 0 ? (K - m.x % K) % K : 0;
+                            }
+                        }
+                        tab[cur][n] = ArRow{yb_, {live[0] ? ph[0] : -1, live[1] ? ph[1] : -1}, mb.x, mb.y, mb.z, rows};
+                        rows += mb.x;
+                        ++n;
+                        if (n == (int)chunk || n == AR_UNITS) {
+                            ++q;
+                            break;
+                        }
+                    }
+                    s_qc = q;
+                }
+                chs[cur].n = n;
+                s_n = n;
+                s_rows = rows;
+                s_fill = 0;
+            }
+            __syncthreads();
+            const int n = s_n;
+            const int rows = s_rows;
+            const int pb = cur ^ 1;
+            if constexpr (IS_W) walk_init(pb, prev_n);
+            if (n == 0) {
+                if constexpr (IS_W) walk(pb, 0);
+                break;
+            }
+            const ArChain& ch = chs[cur];
+            // ---- fill-lane substitution table (once per chain): virtual column v of half h is real
+            // column v - off_h; pre-columns (v <= off_h) score 0, columns past nB_h anything
+            if constexpr (!IS_W) {
+                const int v0 = tid * K + 1;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    int jr[2];
+                    uint32_t cb[2];
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        jr[hh] = v0 + k - ch.off[hh];
+                        cb[hh] = (jr[hh] >= 1 && jr[hh] <= ch.nB[hh]) ? (uint32_t)ch.cseq[hh][jr[hh] - 1] : 0u;
+                    }
+#pragma unroll
+                    for (int rb = 0; rb < 4; ++rb) {
+                        int s2[2];
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh)
+                            s2[hh] = jr[hh] < 1 ? 0 : (cb[hh] == (uint32_t)"ACGT"[rb] ? AR_EQ_MATCH : AR_EQ_MISMATCH);
+                        eqt[rb][tid][k] = ar_pk_int(s2[0], s2[1]);
+                    }
+                }
+            }
+            if (tid < 64) xinfo[tid] = ar_row_record<K, W>(tab[cur], ch, n, rows, tid, band);
+            else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(0u, AR_NOBAND);
+            // lane's end-column Ix open (slot K - 1): the end-gap open in the half whose column nB_h
+            // is this lane's last slot, the internal open elsewhere
+            const int tq0 = w * 64 + lane;
+            const int nbv0 = ch.nB[0] + ch.off[0], nbv1 = ch.nB[1] + ch.off[1];
+            const uint32_t cend = ar_pk_int((ch.nB[0] > 0 && tq0 == nbv0 / K - 1) ? AR_CO_E : AR_CO_I,
+                                            (ch.nB[1] > 0 && tq0 == nbv1 / K - 1) ? AR_CO_E : AR_CO_I);
+            const int own0 = ch.nB[0] > 0 ? nbv0 / K - 1 : -1, own1 = ch.nB[1] > 0 ? nbv1 / K - 1 : -1;
+            const uint32_t ZERO = pk2b(0, 0);
+            uint32_t stG[K], stX[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                stG[k] = ZERO;
+                stX[k] = NEG16X2;
+            }
+            uint32_t payF = NEG16X2, payY = NEG16X2, carry = ZERO;
+            const uint2* ring_in = (w > 0 && !IS_W) ? ring + (size_t)(w - 1) * RING : nullptr;
+            uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
+            uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
+            const uint32_t COI = ar_pk_int(AR_CO_I, AR_CO_I), OYD = ar_pk_int(AR_CO_E - AR_CO_I, AR_CO_E - AR_CO_I);
+            __syncthreads();  // xinfo block 0, tables
+
+            // one systolic step of a fill wave (FW: wave 0, column-0 boundary; HO: hands its last
+            // lane's row on to the next wave through the ring)
+            auto step = [&](auto FW, auto HO, const int s) {
+                int ln;
+                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+                const int g = s - ln;
+                const int tq = w * 64 + ln;
+                const uint2 rec = xinfo[g & (XR - 1)];
+                uint2 o_ring = make_uint2(0u, 0u);
+                if constexpr (!decltype(FW)::value) o_ring = ring_in[(s + 1) & (RING - 1)];
+                const bool in_band = (uint8_t)((uint32_t)tq - rec.y) <= (uint8_t)(rec.y >> 8);
+                const uint64_t bmask = __builtin_amdgcn_ballot_w64(in_band);
+                asm volatile("" ::"s"(bmask));
+                uint32_t inF, inY;
+                if constexpr (decltype(FW)::value) {  // column 0: B(i, 0) = 0, Iy(i, 0) = -inf (drift)
+                    inF = shr_old(payF, ZERO);
+                    inY = shr_old(payY, NEG16X2);
+                } else {
+                    inF = shr_old(payF, o_ring.x);
+                    inY = shr_old(payY, o_ring.y);
+                }
+                uint32_t eq[K];
+                {
+                    const uint32_t* tp = (const uint32_t*)((const char*)&eqt[0][0][0] + rec.x) + (size_t)tq * K;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) eq[k] = tp[k];
+                }
+                if ((int)rec.y < 0) {  // AR_PRE: a unit's first row, or a byte other than A/C/G/T
+                    if (rec.y & AR_FIRST) {  // row 0 of the new pair: B = 0, Ix = -inf, diagonal B(0, j0 - 1) = 0
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            stG[k] = ZERO;
+                            stX[k] = NEG16X2;
+                        }
+                        carry = ZERO;
+                    }
+                    if (rec.y & AR_OTHER) {  // byte compares against both halves' columns
+                        const uint32_t rb = (rec.y >> 16) & 0xFFu;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            int s2[2];
+#pragma unroll
+                            for (int hh = 0; hh < 2; ++hh) {
+                                const int jr = tq * K + k + 1 - ch.off[hh];
+                                const uint32_t cb = (jr >= 1 && jr <= ch.nB[hh]) ? (uint32_t)ch.cseq[hh][jr - 1] : 0u;
+                                s2[hh] = jr < 1 ? 0 : (cb == rb ? AR_EQ_MATCH : AR_EQ_MISMATCH);
+                            }
+                            eq[k] = ar_pk_int(s2[0], s2[1]);
+                        }
+                    }
+                }
+                // Iy open of the row: the end-gap open on a unit's last row (both halves share it)
+                const uint32_t oy = COI + ((rec.y >> 30) & 1u) * OYD;
+                at_s2 d1 = as_s2(carry);
+                at_s2 F1 = as_s2(inF), Y = as_s2(inY);
+                uint32_t acc[K];
+                // Best-open fill (alignt2_kernel.hpp cells, RAW): M = B(i-1, j-1) + s,
+                // X = max(B_up + co_j, X_up), Y = max(B_left + oy, Y_left), B = maximum3(M, X, Y)
+                at_s2 Mk = padd32(d1, eq[0]);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
+                    const at_s2 M = Mk;
+                    if (k + 1 < K) Mk = padd32(Bu, eq[k + 1]);
+                    const at_s2 Xn = pmax(padd32(Bu, k == K - 1 ? cend : COI), Xu);
+                    const at_s2 Yn = pmax(padd32(F1, oy), Y);
+                    uint32_t b3;
+                    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(b3) : "v"(as_u32(M)), "v"(as_u32(Xn)), "v"(as_u32(Yn)));
+                    const at_s2 Bn = as_s2(b3);
+                    const uint32_t dD = as_u32(M) - as_u32(Xn);
+                    const uint32_t dE = as_u32(M) - as_u32(Yn);
+                    acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
+                    stG[k] = as_u32(Bn);
+                    stX[k] = as_u32(Xn);
+                    F1 = Bn;
+                    Y = Yn;
+                }
+                if (in_band) {
+                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tq) * (uint32_t)TB));
+                    if constexpr (K % 4 == 0) {
+#pragma unroll
+                        for (int q = 0; q < K / 4; ++q)
+                            ((uint4*)dst)[q] = make_uint4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < K / 2; ++q) ((uint2*)dst)[q] = make_uint2(acc[2 * q], acc[2 * q + 1]);
+                    }
+                }
+                payF = as_u32(F1);
+                payY = as_u32(Y);
+                if constexpr (decltype(HO)::value)
+                    if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
+                if ((rec.y & AR_LAST) && (tq == own0 || tq == own1)) {  // owner of a half's column nB_h
+                    int t = 0;
+                    for (int q = 1; q < n; ++q)
+                        if (tab[cur][q].r0 <= g) t = q;
+                    const uint32_t e = stG[K - 1];
+                    if (tq == own0) fin[cur][t][0] = (int)(e & 0xFFFFu) - BIAS16;
+                    if (tq == own1) fin[cur][t][1] = (int)(e >> 16) - BIAS16;
+                }
+                carry = inF;  // B(i, j0 - 1): the next row's diagonal
+            };
+
+            const int nsteps = rows + 63;
+            const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
+            const int nint = nblk + WAVE_LAG * (W - 1);
+            for (int it = 0; it < nint; ++it) {
+                if constexpr (IS_W) {
+                    walk(pb, W * (it + 1));
+                } else {
+                    const int blk = it - WAVE_LAG * w;
+                    if (blk >= 0 && blk < nblk) {
+                        const int s0 = blk * INTERVAL;
+                        const int s1 = min(s0 + INTERVAL, nsteps);
+                        if (w == 0) {
+                            for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
+                        } else {
+                            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) once, outside the step loop
+                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
+                        }
+                    }
+                }
+                const int gpre = (it + 1) * INTERVAL + tid;
+                if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
+                if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
+                if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);
+                __syncthreads();
+            }
+            if constexpr (IS_W) walk(pb, 0);
+            prev_n = n;
+            cur ^= 1;
+        }
+    };
+    if (walker) chain_loop(std::true_type{});
+    else chain_loop(std::false_type{});
+}
+
+}  // namespace taxi2

@@ -20,6 +20,7 @@
 #include "align_kernel.hpp"
 #include "alignt_kernel.hpp"
 #include "alignt2_kernel.hpp"
+#include "alignr_kernel.hpp"
 #include "alignlong_kernel.hpp"
 #include "ncd_kernels.hpp"
 #include "format_kernels.hpp"
@@ -79,6 +80,15 @@ struct taxi2_ctx {
     // and an event recorded after that use order the next launch on another stream behind it.
     hipStream_t shared_st = nullptr;
     hipEvent_t shared_ev = nullptr;
+    // row-shared aligner (alignr_kernel.hpp): the launch's segment table, staged through two pinned
+    // host buffers used alternately (an event per buffer: its last copy has completed before the
+    // buffer is refilled) into one device buffer (stream-ordered, under shared_acquire)
+    void* d_seg = nullptr;
+    size_t d_seg_bytes = 0;
+    ArSeg* h_seg[2] = {nullptr, nullptr};
+    size_t h_seg_cap[2] = {0, 0};
+    hipEvent_t seg_ev[2] = {nullptr, nullptr};
+    int seg_flip = 0;
 };
 
 namespace {
@@ -588,6 +598,225 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     return 0;
 }
 
+// ---------------------------------------------------------------- row-shared packed aligner
+// (alignr_kernel.hpp): default scores, triangle and rectangle launches up to 1 024 columns and rows.
+struct VariantR {
+    int K, W, occ;
+    const void* fn;
+    void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, const ArSeg*, int, int64_t, int64_t, MetricSpec, int,
+                   int, double*, int32_t*, uint8_t*, int64_t, int, unsigned long long*, int, int64_t*,
+                   unsigned long long*, StrOut);
+};
+
+template <int K, int W, int OCC>
+void launch_alignr(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, const ArSeg* segs, int nseg, int64_t units,
+                   int64_t npairs, MetricSpec ms, int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb,
+                   int cap, unsigned long long* nx, int band, int64_t* el, unsigned long long* en, StrOut str) {
+    hipLaunchKernelGGL((k_alignr<K, W, OCC>), g, b, 0, st, x, y, segs, nseg, units, npairs, ms, chunk, om, out, so, tr, bb,
+                       cap, nx, band, el, en, str);
+}
+
+// waves per SIMD the row-shared shapes are compiled for: LDS (~23.5 KB per workgroup of three waves)
+// allows six workgroups per CU, i.e. 4.5 waves per SIMD, so 5 (96 VGPRs) costs no occupancy
+#ifndef AR_OCC
+#define AR_OCC 5
+#endif
+#define T2_VARIANTR(K, W) VariantR{K, W, AR_OCC, (const void*)&k_alignr<K, W, AR_OCC>, &launch_alignr<K, W, AR_OCC>}
+const VariantR kAlignR[] = {T2_VARIANTR(4, 1), T2_VARIANTR(8, 1), T2_VARIANTR(6, 2), T2_VARIANTR(8, 2)};
+
+static int64_t tri_row_host(int64_t g, int64_t N);
+
+// A run of row intervals: pairs (x, b) for lo <= b < hi, launch index pbase + b.
+struct RowIv {
+    int64_t x, lo, hi, pbase;
+};
+
+// Cut the launch's pairs into segments of units (x0, x1, b): a sweep over b keeps the rows active
+// on each elementary b-interval paired in x order (x1 = -1 for an odd one out), and a pair of rows
+// stays one segment for as long as the pairing keeps it.  Rows enter and leave the active set only
+// at their interval ends, and in the triangle they enter in x order at the end of the order, so the
+// pairing of earlier rows persists: few segments, few single units.
+void build_segments(std::vector<RowIv>& rows, std::vector<ArSeg>& segs, int64_t& units) {
+    segs.clear();
+    units = 0;
+    std::sort(rows.begin(), rows.end(), [](const RowIv& a, const RowIv& b) { return a.x < b.x; });
+    std::vector<int64_t> pts;
+    for (const auto& r : rows)
+        if (r.hi > r.lo) {
+            pts.push_back(r.lo);
+            pts.push_back(r.hi);
+        }
+    std::sort(pts.begin(), pts.end());
+    pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+    struct Open {
+        int r0, r1;  // row slots (r1 = -1: single)
+        int64_t b0, b1;
+    };
+    const int R = (int)rows.size();
+    std::vector<Open> open(R, Open{-1, -1, 0, 0});  // open segment by its first row slot
+    std::vector<int> act;
+    auto close = [&](const Open& o) {
+        const RowIv& a = rows[o.r0];
+        const int64_t nb = o.b1 - o.b0;
+        if (nb <= 0) return;
+        ArSeg sg{};
+        sg.x0 = a.x;
+        sg.p0 = a.pbase + o.b0;
+        if (o.r1 >= 0) {
+            sg.x1 = rows[o.r1].x;
+            sg.p1 = rows[o.r1].pbase + o.b0;
+        } else {
+            sg.x1 = -1;
+            sg.p1 = -1;
+        }
+        sg.b0 = o.b0;
+        sg.nb = nb;
+        sg.u0 = units;
+        units += nb;
+        segs.push_back(sg);
+    };
+    for (size_t e = 0; e + 1 < pts.size(); ++e) {
+        const int64_t b0 = pts[e], b1 = pts[e + 1];
+        act.clear();
+        for (int r = 0; r < R; ++r)
+            if (rows[r].lo <= b0 && rows[r].hi >= b1) act.push_back(r);
+        // pairs of this interval: continue an open segment of the same two rows ending at b0
+        std::vector<char> cont(R, 0);
+        for (size_t q = 0; q < act.size(); q += 2) {
+            const int r0 = act[q], r1 = q + 1 < act.size() ? act[q + 1] : -1;
+            Open& o = open[r0];
+            if (o.r0 == r0 && o.r1 == r1 && o.b1 == b0) {
+                o.b1 = b1;
+            } else {
+                if (o.r0 >= 0) close(o);
+                o = Open{r0, r1, b0, b1};
+            }
+            cont[r0] = 1;
+        }
+        for (int r = 0; r < R; ++r)
+            if (open[r].r0 >= 0 && !cont[r]) {
+                close(open[r]);
+                open[r].r0 = -1;
+            }
+    }
+    for (int r = 0; r < R; ++r)
+        if (open[r].r0 >= 0) close(open[r]);
+}
+
+const VariantR* pick_variantr(const KScores& k, const DevSet& X, const DevSet& Y, const PairSrc& ps) {
+    if (!is_default(k) || getenv("TAXI2_NO_ALIGNR") || getenv("TAXI2_NO_PACKED") || ps.sel) return nullptr;
+    if (ps.mode != PAIRS_TRI && ps.mode != PAIRS_RECT) return nullptr;
+    if (X.max_len > 1024 || Y.max_len > 1024) return nullptr;  // the f16-maximum3 value range (BIAS16)
+    for (const auto& v : kAlignR)
+        if (64 * v.K * v.W >= X.max_len) return &v;
+    return nullptr;
+}
+
+int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
+                        const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
+                        hipStream_t st, StrOut str = StrOut{}) {
+    // ---- segments of the launch's pairs (host), staged through a pinned buffer
+    std::vector<RowIv> rows;
+    if (ps.mode == PAIRS_TRI) {
+        auto start = [&](int64_t a) { return a * (2 * ps.N - a - 1) / 2; };
+        const int64_t g0 = ps.k0, g1 = ps.k0 + ps.count - 1;
+        const int64_t a0 = tri_row_host(g0, ps.N), a1 = tri_row_host(g1, ps.N);
+        for (int64_t a = a0; a <= a1; ++a) {
+            const int64_t lo = a == a0 ? a + 1 + (g0 - start(a)) : a + 1;
+            const int64_t hi = a == a1 ? a + 2 + (g1 - start(a)) : ps.N;
+            rows.push_back(RowIv{a, lo, hi, start(a) - a - 1 - ps.k0});
+        }
+    } else {
+        const int64_t g0 = ps.k0, g1 = ps.k0 + ps.count - 1;
+        const int64_t q0 = g0 / ps.R, q1 = g1 / ps.R;
+        for (int64_t q = q0; q <= q1; ++q) {
+            const int64_t lo = q == q0 ? g0 - q * ps.R : 0;
+            const int64_t hi = q == q1 ? g1 - q * ps.R + 1 : ps.R;
+            rows.push_back(RowIv{q, lo, hi, q * ps.R - ps.k0});
+        }
+    }
+    std::vector<ArSeg> segs;
+    int64_t units = 0;
+    build_segments(rows, segs, units);
+    if (segs.empty()) return 0;
+    const int f = ctx->seg_flip;
+    ctx->seg_flip ^= 1;
+    if (!ctx->seg_ev[f]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->seg_ev[f], hipEventDisableTiming));
+    else HIP_TRY(ctx, hipEventSynchronize(ctx->seg_ev[f]));  // this buffer's previous copy is done
+    if (ctx->h_seg_cap[f] < segs.size()) {
+        if (ctx->h_seg[f]) (void)hipHostFree(ctx->h_seg[f]);
+        ctx->h_seg[f] = nullptr;
+        ctx->h_seg_cap[f] = 0;
+        const size_t want = std::max(segs.size(), (size_t)4096);
+        HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_seg[f], want * sizeof(ArSeg), hipHostMallocDefault));
+        ctx->h_seg_cap[f] = want;
+    }
+    std::memcpy(ctx->h_seg[f], segs.data(), segs.size() * sizeof(ArSeg));
+
+    // ---- resident grid, chunk (units per cursor step) and trace buffers, as launch_alignt_pairs
+    int per_cu = 0;
+    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 64 * (v.W + 1), 0));
+    const int64_t resident =
+        (int64_t)std::max(1, ctx->num_cus - std::max(0, std::min(ctx->reserve_cus, ctx->num_cus - 1))) *
+        std::max(1, per_cu);
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(units, resident));
+    const int max_len = std::max(1, std::max(X.max_len, Y.max_len));
+    int chunk = 0;
+    if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(AR_UNITS, (atoi(c) + 1) / 2));
+    int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(AR_UNITS, units / (grid * 8)));
+    double budget_gb = 80.0;
+    if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
+    auto buf_bytes = [&](int64_t e) { return at_buf_bytes((int)e * std::max(1, Y.max_len), 4 * v.K, v.W); };
+    while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
+    chunk = (int)eff;
+    const int cap_rows = (int)eff * std::max(1, Y.max_len);
+    const size_t bb = buf_bytes(eff);
+    int band = std::max(32, (int)std::ceil(3.0 * std::sqrt((double)max_len)));
+    if (4 * band >= max_len) band = 0;
+    if (const char* e = getenv("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
+    // the queued pass (k_alignt2_queued over the launch's PairSrc, sign-digit full trace)
+    const VariantT* vq = pick_variantt2(k, max_len);
+    if (!vq) return fail(ctx, "no packed variant for the queued pass at length %d", max_len);
+    int per_cu_q = 0;
+    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_q, vq->fn, 64 * (vq->W + 1), 0));
+    const int64_t grid_q = std::max<int64_t>(1, std::min<int64_t>(ps.count, (int64_t)ctx->num_cus * std::max(1, per_cu_q)));
+    const int chunk_q = 2;  // one pair per stream: the queue is usually empty or a handful of pairs
+    const int cap_rows_q = max_len;
+    const size_t bb_q = at_buf_bytes(cap_rows_q, 2 * vq->K, vq->W);
+
+    if (shared_acquire(ctx, st)) return -1;
+    if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, std::max((size_t)grid * 2 * bb, (size_t)grid_q * 2 * bb_q)))
+        return -1;
+    if (ensure(ctx, &ctx->d_seg, &ctx->d_seg_bytes, segs.size() * sizeof(ArSeg))) return -1;
+    if (ensure(ctx, &ctx->d_work, &ctx->d_work_bytes, 64 + (size_t)ps.count * 8)) return -1;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_seg, ctx->h_seg[f], segs.size() * sizeof(ArSeg), hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx, hipEventRecord(ctx->seg_ev[f], st));
+    unsigned long long* next = (unsigned long long*)((char*)ctx->d_work + 8);
+    unsigned long long* next2 = (unsigned long long*)((char*)ctx->d_work + 16);
+    unsigned long long* esc_n = (unsigned long long*)((char*)ctx->d_work + 24);
+    int64_t* esc_list = (int64_t*)((char*)ctx->d_work + 64);
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 64, st));
+    v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), (const ArSeg*)ctx->d_seg, (int)segs.size(),
+             units, ps.count, ms, chunk, out_mode, d_out, d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, next,
+             band, esc_list, esc_n, str);
+    HIP_TRY(ctx, hipGetLastError());
+    PairSrc p2 = ps;
+    p2.sel = esc_list;
+    p2.dcount = esc_n;
+    vq->launch(dim3((unsigned)grid_q), dim3(64 * (vq->W + 1)), st, view(X), view(Y), p2, k, ms, chunk_q, out_mode, d_out,
+               d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb_q, cap_rows_q, 4096, next2, BandArgs{0, nullptr, nullptr}, str);
+    HIP_TRY(ctx, hipGetLastError());
+    if (getenv("TAXI2_AT_BAND_STATS")) {
+        unsigned long long q = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(&q, esc_n, sizeof q, hipMemcpyDeviceToHost, st));
+        HIP_TRY(ctx, hipStreamSynchronize(st));
+        fprintf(stderr, "taxi2 band: k_alignr<%d,%d> band %d: %llu of %lld pairs took the full-trace pass (%zu segments, "
+                "%lld units)\n", v.K, v.W, band, q, (long long)ps.count, segs.size(), (long long)units);
+    }
+    if (shared_release(ctx, st)) return -1;
+    return 0;
+}
+
 // ---------------------------------------------------------------- column-tiled (any length)
 struct VariantL {
     int K, W, occ;
@@ -681,6 +910,11 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (!is_linear(k) && !getenv("TAXI2_NO_ALIGNT")) {
         // packed 16-bit fill when every difference fits int16 (TAXI2_NO_PACKED=1: 32-bit fill)
         const bool packed = at_fits16(k, max_len) && !getenv("TAXI2_NO_PACKED");
+        if (packed)
+            if (const VariantR* vr = pick_variantr(k, X, Y, ps)) {
+                if (ps.count <= 0) return 0;
+                return launch_alignr_pairs(ctx, *vr, X, Y, ps, k, ms, out_mode, d_out, d_scores, st);
+            }
         const VariantT* vt = packed ? pick_variantt2(k, max_len) : pick_variantt(k, max_len);
         if (vt) {
             if (ps.count <= 0) return 0;
@@ -721,6 +955,8 @@ int launch_packed_strings(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, cons
     if (ps.count <= 0) return 0;
     if (str.cap < X.max_len + Y.max_len)
         return fail(ctx, "string slots of %d bytes < longest x + longest y (%d)", str.cap, X.max_len + Y.max_len);
+    if (const VariantR* vr = pick_variantr(k, X, Y, ps))
+        return launch_alignr_pairs(ctx, *vr, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, str) ? -1 : 0;
     const int rc = launch_alignt_pairs(ctx, *vt, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, max_len, true, str);
     return rc ? -1 : 0;
 }
@@ -1061,6 +1297,11 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
+    if (ctx->d_seg) (void)hipFree(ctx->d_seg);
+    for (int f = 0; f < 2; ++f) {
+        if (ctx->h_seg[f]) (void)hipHostFree(ctx->h_seg[f]);
+        if (ctx->seg_ev[f]) (void)hipEventDestroy(ctx->seg_ev[f]);
+    }
     if (ctx->d_bnd) (void)hipFree(ctx->d_bnd);
     if (ctx->d_fmt) (void)hipFree(ctx->d_fmt);
     if (ctx->d_sub) (void)hipFree(ctx->d_sub);

@@ -10,6 +10,7 @@
 #   bench            bench.py (default settings: headline + secondary legs)
 #   headline         bench.py --secondary '' --steps 10 --warmup 2
 #   ab:LIBA,LIBB,R   R alternations of the headline with TAXI2_LIB=LIBA then LIBB (same box A/B)
+#   abenv:VAR,R      R alternations of the headline with VAR=1 set, then unset (same box A/B)
 #   trace            rocprofv3 --kernel-trace --stats of the headline bench
 #   pmc_valu | pmc_fetch | pmc_write | pmc_lds
 #                    one rocprofv3 --pmc pass each over one bench launch (separate runs: rocprofv3
@@ -48,6 +49,12 @@ run_step() {
         for r in $(seq 1 "${reps:-2}"); do
             (cd "$R" && TAXI2_LIB=$la timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_a_$r.json" 2> "$OUT/ab_a_$r.err") || return $?
             (cd "$R" && TAXI2_LIB=$lb timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_b_$r.json" 2> "$OUT/ab_b_$r.err") || return $?
+        done ;;
+    abenv:*)
+        IFS=, read -r var reps <<< "${s#abenv:}"
+        for r in $(seq 1 "${reps:-2}"); do
+            (cd "$R" && env "$var=1" timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_env_$r.json" 2> "$OUT/ab_env_$r.err") || return $?
+            (cd "$R" && timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_def_$r.json" 2> "$OUT/ab_def_$r.err") || return $?
         done ;;
     trace)
         (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
