@@ -440,27 +440,28 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 stX[k] = NEG16X2;
             }
             uint32_t payF = NEG16X2, payY = NEG16X2, carry = ZERO;
-            const uint2* ring_in = (w > 0 && !IS_W) ? ring + (size_t)(w - 1) * RING : nullptr;
-            uint2* ring_out = (w < W - 1) ? ring + (size_t)w * RING : nullptr;
             uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
             const uint32_t COI = ar_pk_int(AR_CO_I, AR_CO_I), OYD = ar_pk_int(AR_CO_E - AR_CO_I, AR_CO_E - AR_CO_I);
             __syncthreads();  // xinfo block 0, tables
 
-            // one systolic step of a fill wave (FW: wave 0, column-0 boundary; HO: hands its last
-            // lane's row on to the next wave through the ring)
-            auto step = [&](auto FW, auto HO, const int s) {
+            // one systolic step of fill wave WI (a compile-time index: the ring slots, the lane's
+            // column block and its table row are immediate offsets).  Wave 0 takes the column-0
+            // boundary; every wave but the last hands its last lane's row on through the ring.
+            auto step = [&](auto WIC, const int s) {
+                constexpr int WI = decltype(WIC)::value;
+                constexpr bool FW = WI == 0, HO = WI < W - 1;
                 int ln;
                 asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
                 const int g = s - ln;
-                const int tq = w * 64 + ln;
+                const int tq = WI * 64 + ln;
                 const uint2 rec = xinfo[g & (XR - 1)];
                 uint2 o_ring = make_uint2(0u, 0u);
-                if constexpr (!decltype(FW)::value) o_ring = ring_in[(s + 1) & (RING - 1)];
+                if constexpr (!FW) o_ring = ring[(WI - 1) * RING + ((s + 1) & (RING - 1))];
                 const bool in_band = (uint8_t)((uint32_t)tq - rec.y) <= (uint8_t)(rec.y >> 8);
                 const uint64_t bmask = __builtin_amdgcn_ballot_w64(in_band);
                 asm volatile("" ::"s"(bmask));
                 uint32_t inF, inY;
-                if constexpr (decltype(FW)::value) {  // column 0: B(i, 0) = 0, Iy(i, 0) = -inf (drift)
+                if constexpr (FW) {  // column 0: B(i, 0) = 0, Iy(i, 0) = -inf (drift)
                     inF = shr_old(payF, ZERO);
                     inY = shr_old(payY, NEG16X2);
                 } else {
@@ -470,8 +471,19 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 uint32_t eq[K];
                 {
                     const uint32_t* tp = (const uint32_t*)((const char*)&eqt[0][0][0] + rec.x) + (size_t)tq * K;
+                    if constexpr (K % 4 == 0) {  // 16-byte aligned rows (K * 4 bytes per lane)
 #pragma unroll
-                    for (int k = 0; k < K; ++k) eq[k] = tp[k];
+                        for (int q = 0; q < K / 4; ++q) {
+                            const uint4 v = ((const uint4*)__builtin_assume_aligned(tp, 16))[q];
+                            eq[4 * q] = v.x;
+                            eq[4 * q + 1] = v.y;
+                            eq[4 * q + 2] = v.z;
+                            eq[4 * q + 3] = v.w;
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < K; ++k) eq[k] = tp[k];
+                    }
                 }
                 if ((int)rec.y < 0) {  // AR_PRE: a unit's first row, or a byte other than A/C/G/T
                     if (rec.y & AR_FIRST) {  // row 0 of the new pair: B = 0, Ix = -inf, diagonal B(0, j0 - 1) = 0
@@ -536,8 +548,8 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 }
                 payF = as_u32(F1);
                 payY = as_u32(Y);
-                if constexpr (decltype(HO)::value)
-                    if (ln == 63) ring_out[(g + 1) & (RING - 1)] = make_uint2(payF, payY);
+                if constexpr (HO)
+                    if (ln == 63) ring[WI * RING + ((g + 1) & (RING - 1))] = make_uint2(payF, payY);
                 if ((rec.y & AR_LAST) && (tq == own0 || tq == own1)) {  // owner of a half's column nB_h
                     int t = 0;
                     for (int q = 1; q < n; ++q)
@@ -561,10 +573,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         const int s0 = blk * INTERVAL;
                         const int s1 = min(s0 + INTERVAL, nsteps);
                         if (w == 0) {
-                            for (int s = s0; s < s1; ++s) step(std::true_type{}, std::integral_constant<bool, (W > 1)>{}, s);
-                        } else {
+                            for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 0>{}, s);
+                        } else if constexpr (W > 1) {
                             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) once, outside the step loop
-                            for (int s = s0; s < s1; ++s) step(std::false_type{}, std::false_type{}, s);
+                            for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 1>{}, s);
                         }
                     }
                 }
