@@ -32,7 +32,18 @@
 
 namespace taxi2 {
 
-constexpr int AR_UNITS = 4;  // units (row sequences, up to two pairs each) per chain
+#ifndef TAXI2_AR_UNITS
+#define TAXI2_AR_UNITS 4
+#endif
+constexpr int AR_UNITS = TAXI2_AR_UNITS;  // units (row sequences, up to two pairs each) per chain
+
+// Profiling build only (-DAR_PROF, `make variant VNAME=arprof VFLAGS=-DAR_PROF`): per-wave s_memtime
+// totals of the launch -- fill: step loops, interval barrier waits, chain set-up (cut, tables, first
+// barrier); walker: hops during intervals, the chain-end drain, interval barrier waits; chains; hops
+#ifdef AR_PROF
+__device__ unsigned long long ar_prof[8];
+#define AR_NOW() __builtin_amdgcn_s_memtime()
+#endif
 
 // Host-built segment: units u0 .. u0 + nb - 1 are (x0, x1, y = b0 + (u - u0)); pair (x_h, y) has
 // launch index p_h + (u - u0) (x1 = -1, p1 = -1: one pair per unit).
@@ -312,6 +323,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 
     auto chain_loop = [&](auto WK) {
         constexpr bool IS_W = decltype(WK)::value;
+#ifdef AR_PROF
+        unsigned long long pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long tA = AR_NOW();
+#endif
         for (;;) {
             // ---- cut the next chain (thread 0): up to AR_UNITS units of one segment
             __syncthreads();
@@ -443,6 +458,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
             const uint32_t COI = ar_pk_int(AR_CO_I, AR_CO_I), OYD = ar_pk_int(AR_CO_E - AR_CO_I, AR_CO_E - AR_CO_I);
             __syncthreads();  // xinfo block 0, tables
+#ifdef AR_PROF
+            pf[2] += AR_NOW() - tA;
+            pf[6] += 1;
+#endif
 
             // one systolic step of fill wave WI (a compile-time index: the ring slots, the lane's
             // column block and its table row are immediate offsets).  Wave 0 takes the column-0
@@ -565,6 +584,9 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
             const int nint = nblk + WAVE_LAG * (W - 1);
             for (int it = 0; it < nint; ++it) {
+#ifdef AR_PROF
+                const unsigned long long t1 = AR_NOW();
+#endif
                 if constexpr (IS_W) {
                     walk(pb, W * (it + 1));
                 } else {
@@ -580,17 +602,38 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         }
                     }
                 }
+#ifdef AR_PROF
+                const unsigned long long t2 = AR_NOW();
+                pf[IS_W ? 3 : 0] += t2 - t1;
+#endif
                 const int gpre = (it + 1) * INTERVAL + tid;
                 if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
                 if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
                 if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);
                 __syncthreads();
+#ifdef AR_PROF
+                pf[IS_W ? 5 : 1] += AR_NOW() - t2;
+#endif
             }
+#ifdef AR_PROF
+            const unsigned long long t3 = AR_NOW();
+#endif
             if constexpr (IS_W) walk(pb, 0);
+#ifdef AR_PROF
+            pf[4] += AR_NOW() - t3;
+            tA = AR_NOW();
+#endif
             prev_n = n;
             cur ^= 1;
         }
+#ifdef AR_PROF
+        if (lane == 0)
+            for (int q = 0; q < 8; ++q) atomicAdd(&ar_prof[q], pf[q]);
+#endif
     };
+#ifdef AR_WALK_PRIO
+    if (walker) __builtin_amdgcn_s_setprio(AR_WALK_PRIO);  // experiment: walker issue priority
+#endif
     if (walker) chain_loop(std::true_type{});
     else chain_loop(std::false_type{});
 }

@@ -813,6 +813,17 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
         fprintf(stderr, "taxi2 band: k_alignr<%d,%d> band %d: %llu of %lld pairs took the full-trace pass (%zu segments, "
                 "%lld units)\n", v.K, v.W, band, q, (long long)ps.count, segs.size(), (long long)units);
     }
+#ifdef AR_PROF
+    {  // profiling build: the launch's per-wave phase totals (alignr_kernel.hpp AR_PROF)
+        unsigned long long pf[8] = {0}, z[8] = {0};
+        HIP_TRY(ctx, hipStreamSynchronize(st));
+        HIP_TRY(ctx, hipMemcpyFromSymbol(pf, HIP_SYMBOL(ar_prof), sizeof pf));
+        HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(ar_prof), z, sizeof z));
+        fprintf(stderr, "taxi2 arprof: k_alignr<%d,%d> grid %lld units %lld chains %llu | fill steps %llu barrier %llu setup %llu"
+                " | walker hops %llu drain %llu barrier %llu\n", v.K, v.W, (long long)grid, (long long)units, pf[6], pf[0],
+                pf[1], pf[2], pf[3], pf[4], pf[5]);
+    }
+#endif
     if (shared_release(ctx, st)) return -1;
     return 0;
 }

@@ -242,8 +242,7 @@ class VersusAll:
 
             walked = False
             if pairs_fh is not None and cidx and walk_strings_ok(scores, seqs):
-                tri = self._tri_with_pairs_seq if os.environ.get("TAXI2_PAIRS_SEQ") else self._tri_with_pairs
-                walked = (tri(seqs, eng, st, D, cidx, clabels, scores, pairs_fh)
+                walked = (self._tri_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh)
                           or self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh))
             if walked:  # counter metrics and aligned_pairs.txt done; NCD (if any) from the triangle
                 if nidx:
@@ -292,198 +291,12 @@ class VersusAll:
         in row blocks (taxi2_tri_strings_dev: the walkers walk both orientations, as the metric
         kernel does), the (a, b) strings formatted with row a's block, the (b, a) strings compacted
         and kept in HBM until row b's block is written (the text kernel reads each pair's strings
-        through a pointer).  Two streams: block b aligns on one while the previous block is
-        post-processed on the other (compaction, metrics to the host, pointers, text, its D2H and the
-        file write), so the text hides behind the alignment.  False (nothing written) when
-        TAXI2_PAIRS_RECT is set or the packed aligner does not cover the shape -- then
-        _rows_with_pairs aligns every ordered pair once instead; when the kept strings outgrow
-        params.engine.keep_bytes, the remaining rows switch to it."""
-        import torch
-
-        from .._native import NativeError, pack_strings
-
-        n = len(seqs)
-        lens_h = np.array([len(s.seq) for s in seqs], dtype=np.int64)
-        if os.environ.get("TAXI2_PAIRS_RECT") or n < 2:
-            return False
-        keep_limit = int(self.params.engine.keep_bytes)
-        dev = torch.device("cuda", eng.device)
-        cap = 2 * int(lens_h.max()) + 1
-        Mc = len(cidx)
-        npairs = n * (n - 1) // 2
-        ids_b, ids_o = pack_strings([s.id for s in seqs])
-        idmax = int(np.max(np.diff(ids_o))) if n else 0
-        total = len(self.params.distances.metrics) * n * n
-        launch = int(self.params.engine.launch_pairs or 0)
-        slot_budget = max(int(self.params.engine.block_bytes), WALK_BLOCK_BYTES if launch else 0)
-        per_pair = 4 * cap + 16 * Mc + 8
-        target = max(1, min(launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
-        blocks, x0 = [], 0
-        while x0 < n:  # rows [x0, x1): ~target triangle pairs, at most 2 target ordered pairs of text
-            x1, cnt = x0, 0
-            while x1 < n and (x1 == x0 or (cnt + (n - 1 - x1) <= target and (x1 + 1 - x0) * n <= 2 * target)):
-                cnt += n - 1 - x1
-                x1 += 1
-            blocks.append((x0, x1, cnt, x0 * (2 * n - x0 - 1) // 2))
-            x0 = x1
-        # CUs the aligner leaves to the previous block's post-processing (its persistent grid would
-        # otherwise hold every CU until the block is done); TAXI2_PAIRS_RESERVE overrides
-        reserve = int(os.environ.get("TAXI2_PAIRS_RESERVE", "16"))
-        sa_ = torch.cuda.Stream(dev)  # alignment
-        sc_ = torch.cuda.Stream(dev)  # post-processing of the previous block
-        timed = isinstance(self.timings, dict)
-        with torch.cuda.stream(sc_):
-            lens = torch.as_tensor(lens_h, device=dev)
-            rid = torch.as_tensor(ids_b.copy(), device=dev)  # NUL-terminated (pack_strings)
-            roff = torch.as_tensor(np.ascontiguousarray(ids_o, dtype=np.int64), device=dev)
-            # self alignments (x, x) for the diagonal pairs' text
-            strings = eng.align_strings(st, st, np.arange(n), np.arange(n), scores)
-            sa = [a.encode("latin-1") for a, _ in strings]
-            sb = [b.encode("latin-1") for _, b in strings]
-            slen_self = torch.as_tensor(np.array([len(a) for a in sa], dtype=np.int32), device=dev)
-            soff = np.zeros(n, dtype=np.int64)
-            soff[1:] = np.cumsum([len(a) for a in sa])[:-1]
-            self_x = torch.as_tensor(np.frombuffer(b"".join(sa) + b"\0", dtype=np.uint8).copy(), device=dev)
-            self_y = torch.as_tensor(np.frombuffer(b"".join(sb) + b"\0", dtype=np.uint8).copy(), device=dev)
-            soff_d = torch.as_tensor(soff, device=dev)
-            px_self = self_x.data_ptr() + soff_d
-            py_self = self_y.data_ptr() + soff_d
-            # (b, a) strings of every pair, kept until row b: pointers per triangle pair
-            kpx = torch.zeros(npairs, dtype=torch.int64, device=dev)
-            kpy = torch.zeros(npairs, dtype=torch.int64, device=dev)
-            klen = torch.zeros(npairs, dtype=torch.int32, device=dev)
-            ar = torch.arange(cap, device=dev)
-            totals = torch.zeros(2, dtype=torch.int64, device=dev)
-            fscr = torch.empty(2 * max(x1 - x0 for x0, x1, _, _ in blocks), dtype=torch.int64, device=dev)
-        # two slot sets, allocated once (block b aligns into one while b - 1 is read from the other):
-        # no allocator traffic, hence no device-wide synchronisation, inside the pipeline
-        cmax = max(c for _, _, c, _ in blocks)
-        slots = [(torch.empty((cmax, 2, Mc), dtype=torch.float64, device=dev),
-                  torch.empty((cmax, 2, cap), dtype=torch.uint8, device=dev),
-                  torch.empty((cmax, 2, cap), dtype=torch.uint8, device=dev),
-                  torch.empty((cmax, 2), dtype=torch.int32, device=dev)) for _ in range(2 if cmax else 0)]
-        sc_.synchronize()
-        state = {"kept": [], "kept_bytes": 0, "text": None}
-
-        def launch_block(bi):
-            x0, x1, cnt, k0 = blocks[bi]
-            if not cnt:
-                return {"bi": bi}
-            with torch.cuda.stream(sa_):
-                d, sx, sy, sl = (t_[:cnt] for t_ in slots[bi % 2])
-                eng.tri_strings_dev(st, k0, cnt, clabels, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
-                                    sl.data_ptr(), scores, sa_.cuda_stream, reserve_cus=reserve)
-                ev = torch.cuda.Event()
-                ev.record(sa_)
-            return {"bi": bi, "d": d, "sx": sx, "sy": sy, "sl": sl, "ev": ev}
-
-        def finish_block(b):
-            x0, x1, cnt, k0 = blocks[b["bi"]]
-            with torch.cuda.stream(sc_):
-                blk = None
-                if cnt:
-                    sc_.wait_event(b["ev"])
-                    d, sx, sy, sl = b["d"], b["sx"], b["sy"], b["sl"]
-                    # pair (a, b) of the block: a in [x0, x1), b > a
-                    rows = torch.arange(x0, x1, device=dev)
-                    per = n - 1 - rows
-                    ra = torch.repeat_interleave(rows, per)
-                    rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(torch.cumsum(per, 0) - per, per)
-                    end = (lens[ra] + lens[rb]).to(torch.int64)
-                    # keep the (b, a) orientation compacted (mask of each slot's right-aligned bytes)
-                    L1 = sl[:, 1].to(torch.int64)
-                    m1 = (ar[None, :] >= (end - L1)[:, None]) & (ar[None, :] < end[:, None])
-                    kx, ky = sx[:, 1, :][m1], sy[:, 1, :][m1]
-                    del m1
-                    off = torch.cumsum(L1, 0) - L1
-                    kpx[k0:k0 + cnt] = kx.data_ptr() + off
-                    kpy[k0:k0 + cnt] = ky.data_ptr() + off
-                    klen[k0:k0 + cnt] = sl[:, 1]
-                    state["kept"].append((kx, ky))
-                    state["kept_bytes"] += 2 * kx.numel()
-                    blk = (sx, sy, sl, end)
-                    dd = d.cpu().numpy()
-                    a_h, b_h = ra.cpu().numpy(), rb.cpu().numpy()
-                    for q, kk in enumerate(cidx):
-                        D[a_h, b_h, kk] = dd[:, 0, q]
-                        D[b_h, a_h, kk] = dd[:, 1, q]
-                # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
-                # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
-                # and (x, x) from the self alignments
-                xs_ = torch.arange(x0, x1, device=dev)[:, None]
-                ys_ = torch.arange(n, device=dev)[None, :]
-                up, lo = ys_ > xs_, ys_ < xs_
-                pu = xs_ * (2 * n - xs_ - 1) // 2 + (ys_ - xs_ - 1)   # pair (x, y) for y > x
-                pl = (ys_ * (2 * n - ys_ - 1) // 2 + (xs_ - ys_ - 1)).clamp(0, npairs - 1)   # pair (y, x), y < x
-                sx_self = xs_.expand(-1, n)
-                px = torch.where(lo, kpy[pl], px_self[sx_self])
-                py = torch.where(lo, kpx[pl], py_self[sx_self])
-                ln = torch.where(lo, klen[pl], slen_self[sx_self])
-                if blk is not None:
-                    sx, sy, sl, end = blk
-                    q = (pu - k0).clamp(0, max(0, cnt - 1))
-                    start0 = q * 2 * cap + end[q] - sl[:, 0].to(torch.int64)[q]
-                    px = torch.where(up, sx.data_ptr() + start0, px)
-                    py = torch.where(up, sy.data_ptr() + start0, py)
-                    ln = torch.where(up, sl[:, 0][q], ln)
-                px, py, ln = px.contiguous(), py.contiguous(), ln.to(torch.int32).contiguous()
-                t0 = perf_counter()
-                est = (x1 - x0) * n * (2 * idmax + 8 + 3 * (cap // 2 + cap // 8 + 2))
-                for _ in range(2):
-                    if state["text"] is None or state["text"].numel() < est:
-                        state["text"] = torch.empty(int(est), dtype=torch.uint8, device=dev)
-                    tb = state["text"]
-                    eng.format_pairs_ptr_async(x1 - x0, n, px.data_ptr(), py.data_ptr(), ln.data_ptr(),
-                                               rid.data_ptr(), roff.data_ptr() + 8 * x0, rid.data_ptr(),
-                                               roff.data_ptr(), first=x0 == 0, text_ptr=tb.data_ptr(),
-                                               cap=tb.numel(), total_ptr=totals.data_ptr(),
-                                               scratch_ptr=fscr.data_ptr(), stream=sc_.cuda_stream)
-                    tot, ok = totals.tolist()
-                    if ok:
-                        break
-                    est = tot  # longer alignments than the estimate: once more with the exact size
-                host = eng._pinned_view(tot)
-                if tot:
-                    torch.from_numpy(host).copy_(state["text"][:tot], non_blocking=True)
-                    sc_.synchronize()
-                    fh.write(memoryview(host))
-                if timed:
-                    self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
-            report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1), total)
-
-        prev = None
-        try:
-            for bi in range(len(blocks)):
-                try:
-                    cur = launch_block(bi)
-                except NativeError as e:
-                    if bi == 0 and "walker strings need" in str(e):
-                        return False
-                    raise
-                if prev is not None:
-                    finish_block(prev)  # overlaps block bi's alignment
-                prev = cur
-                if state["kept_bytes"] > keep_limit and bi + 1 < len(blocks):
-                    # the kept strings outgrew their budget: the remaining rows align every ordered
-                    # pair once (row blocks of the rect path), nothing kept
-                    finish_block(prev)
-                    prev = None
-                    sa_.synchronize()
-                    sc_.synchronize()
-                    state["kept"].clear()
-                    return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=blocks[bi][1])
-            if prev is not None:
-                finish_block(prev)
-            sc_.synchronize()
-        finally:
-            sa_.synchronize()
-            sc_.synchronize()
-            state["kept"].clear()
-        return True
-
-    def _tri_with_pairs_seq(self, seqs, eng, st, D, cidx, clabels, scores, fh) -> bool:
-        """Round-3 sequential form of _tri_with_pairs (one stream, text after each block's
-        alignment), kept for A/B against the two-stream pipeline (TAXI2_PAIRS_SEQ=1)."""
+        through a pointer).  One stream, the text after each block's alignment: a two-stream
+        pipeline (block b aligning while block b - 1's text and D2H ran) measured slower on one
+        box (10.85 s vs 10.0 s at N = 5 000, profiles/r3/task_pipeline_ab/) and is gone.  False
+        (nothing written) when TAXI2_PAIRS_RECT is set or the packed aligner does not cover the
+        shape -- then _rows_with_pairs aligns every ordered pair once instead; when the kept strings
+        outgrow params.engine.keep_bytes, the remaining rows switch to it."""
         import torch
 
         from .._native import NativeError, pack_strings
