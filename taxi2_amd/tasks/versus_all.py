@@ -637,7 +637,9 @@ class VersusAll:
         eng = self._engine()
         cuda = torch.device("cuda", eng.device)
         store_dev = cuda if group_backend in (None, "nccl") else torch.device("cpu")
+        t_up = perf_counter()
         st = eng.upload([s.seq for s in seqs], align=align)
+        self._upload_s = perf_counter() - t_up
         # one real stream for the torch ops and the engine's *_dev calls of this path (the legacy
         # default stream has handle 0, which the engine would read as "its own stream")
         stream = torch.cuda.Stream(cuda)
@@ -715,8 +717,13 @@ class VersusAll:
                 times[key] += perf_counter() - t0
             return perf_counter()
 
+        t_prep = perf_counter()
         sink = _BlockWriters(self, seqs, eng, files=(rank == 0), walk=walk)
         sink.diag = self._diag_info(seqs, eng, st, bool(p.pairs.align), scores, labels)
+        # host-side phases outside the block loop: the set upload, the writers' and aggregators' set-up
+        # with the diagonal rule's groups, and the close (subset statistics files, row_minima.tsv)
+        times["upload_s"] = getattr(self, "_upload_s", 0.0)
+        times["prepare_s"] = perf_counter() - t_prep
         scale = 100.0 if p.format.percentage_multiply else 1.0
         cap = 2 * max((len(s.seq) for s in seqs), default=0) + 1
         B = (walk_block_rows(n, 8 * M + 2 * cap + 4, int(p.engine.block_bytes), int(p.engine.launch_pairs or 0)) if walk
@@ -799,7 +806,9 @@ class VersusAll:
                     sink.rmin_d[:] = allr[:, 1]
                     tick("comm_s", t)
             if rank == 0:
+                t_cl = perf_counter()
                 sink.close()
+                times["finish_s"] = perf_counter() - t_cl
         finally:
             st.free()
         self.timings = times
