@@ -227,3 +227,25 @@ def run_all(eng, seqset, n_seqs: int, legs=("allmetrics", "config4", "task", "co
             out[name] = {"error": f"{type(e).__name__}: {e}"}
         _log(f"{name} done in {time.perf_counter() - t0:.1f} s")
     return out
+
+
+def main() -> None:
+    """python bench_secondary.py LEG [LEG ...]: run legs alone (one JSON line each)."""
+    import json
+
+    import torch  # noqa: F401  -- torch's HIP runtime first (the engine shares it)
+
+    from taxi2_amd._native import Engine
+    from taxi2_amd.synth import family_packed
+
+    eng = Engine(0)
+    seqset = None
+    for name in sys.argv[1:]:
+        if name == "allmetrics" and seqset is None:
+            buf, offs = family_packed(50_000, 1000, 0x7A12)
+            seqset = eng.upload_packed(buf, offs, align=True)
+        print(json.dumps({name: run_all(eng, seqset, 50_000, [name])[name]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,8 @@
 #   guard            the poisoning guard build (make guard) on the packed aligner suites
 #   peak             tools/valu_peak (SIMD cycles per wave64 instruction)
 #   tool:SCRIPT      python tools/SCRIPT.py (bench tools), e.g. tool:bench_long
+#   sec:LEG          one bench_secondary.py leg alone (task, config5, config4, allmetrics)
+#   sectrace:LEG     rocprofv3 --kernel-trace --stats of that leg
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:?tag}
@@ -80,6 +82,11 @@ run_step() {
         timeout -k 10 180 "$R/tools/valu_peak" > "$OUT/valu_peak.txt" 2>&1 ;;
     tool:*)
         (cd "$R" && timeout -k 10 900 python3 -u "tools/${s#tool:}.py" > "$OUT/${s#tool:}.json" 2> "$OUT/${s#tool:}.err") ;;
+    sec:*)
+        (cd "$R" && timeout -k 10 600 python3 -u bench_secondary.py "${s#sec:}" > "$OUT/sec_${s#sec:}.json" 2> "$OUT/sec_${s#sec:}.err") ;;
+    sectrace:*)
+        (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sectrace_${s#sectrace:}" -o run -- \
+            python3 $R/bench_secondary.py "${s#sectrace:}" > "$OUT/sectrace_${s#sectrace:}.json" 2> "$OUT/sectrace_${s#sectrace:}.err") ;;
     *)
         echo "unknown step $s" >&2; return 2 ;;
     esac
