@@ -32,6 +32,11 @@
 
 namespace taxi2 {
 
+// 1: the fill waves pace each other with LDS progress counters instead of a barrier every 64 steps
+#ifndef AR_DECOUPLE
+#define AR_DECOUPLE 1
+#endif
+constexpr int AR_BLK = 16;  // steps between progress checks / publications
 #ifndef TAXI2_AR_UNITS
 #define TAXI2_AR_UNITS 4
 #endif
@@ -149,8 +154,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows, s_seg;
     __shared__ int s_fill;
+    __shared__ int s_prog[2];  // AR_DECOUPLE: steps completed by each fill wave in the current chain
     __shared__ ArWalk wks[NW];
     __shared__ int escf[2][AR_UNITS][2];
+#ifdef AR_PROF
+    __shared__ unsigned long long s_arr[W + 1];  // interval barrier arrival time of each wave
+#endif
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -404,6 +413,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 s_n = n;
                 s_rows = rows;
                 s_fill = 0;
+                s_prog[0] = s_prog[1] = 0;
             }
             __syncthreads();
             const int n = s_n;
@@ -581,6 +591,64 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             };
 
             const int nsteps = rows + 63;
+#if AR_DECOUPLE
+            // No interval barriers: the fill waves pace each other through two LDS progress counters
+            // (steps completed, published every AR_BLK steps), so a wave whose steps store no trace
+            // runs ahead instead of waiting at a barrier for the in-band wave (the band covers wave 0
+            // early in a unit and wave 1 late: ~60 % of the old intervals were unbalanced).  Wave 1 at
+            // step s reads ring slot s + 1, written by wave 0 at step s + 63; wave 0 at step s
+            // rewrites the slot wave 1 read at step s - 255 - 63.  The row records of the next 64 rows
+            // are written by wave 0 itself before it needs them, and wave 1 (>= 79 steps behind,
+            // <= 303 ahead is what wave 0 may run) reads them long before they are rewritten.  The
+            // walker walks the previous chain to its end; the chain's last barrier joins everyone.
+            if constexpr (IS_W) {
+#ifdef AR_PROF
+                const unsigned long long t1 = AR_NOW();
+#endif
+                walk(pb, 0);
+#ifdef AR_PROF
+                pf[3] += AR_NOW() - t1;
+#endif
+            } else {
+                const int mine = w, other = w ^ 1;
+                for (int s0 = 0; s0 < nsteps; s0 += AR_BLK) {
+                    const int s1 = min(s0 + AR_BLK, nsteps);
+                    if (W > 1) {  // wait for the other fill wave (rare: the ring holds 256 rows)
+                        const int need = w == 0 ? s1 - (RING - 63) : s1 + 63;
+                        while (__hip_atomic_load(&s_prog[other], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+                            __builtin_amdgcn_s_sleep(1);
+                    }
+#ifdef AR_PROF
+                    const unsigned long long t1 = AR_NOW();
+#endif
+                    if (w == 0) {
+                        for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 0>{}, s);
+                    } else if constexpr (W > 1) {
+                        for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 1>{}, s);
+                    }
+#ifdef AR_PROF
+                    pf[0] += AR_NOW() - t1;
+#endif
+                    if (w == 0 && (s1 & (INTERVAL - 1)) == 0) {  // the next 64 rows' records
+                        const int gpre = s1 + lane;
+                        xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
+                    }
+                    // publish (the ring / record writes above complete first: release)
+                    if (lane == 0)
+                        __hip_atomic_store(&s_prog[mine], s1 >= nsteps ? 0x3FFFFFFF : s1, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                __builtin_amdgcn_s_waitcnt(0);  // this chain's trace stores are done before the walker reads them
+            }
+#ifdef AR_PROF
+            const unsigned long long t2 = AR_NOW();
+#endif
+            __syncthreads();  // the chain is filled and the previous one walked
+#ifdef AR_PROF
+            pf[IS_W ? 5 : 1] += AR_NOW() - t2;
+            tA = AR_NOW();
+#endif
+#else
             const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
             const int nint = nblk + WAVE_LAG * (W - 1);
             for (int it = 0; it < nint; ++it) {
@@ -610,9 +678,18 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
                 if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
                 if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);
+#ifdef AR_PROF
+                if (lane == 0) s_arr[w] = AR_NOW();
+#endif
                 __syncthreads();
 #ifdef AR_PROF
                 pf[IS_W ? 5 : 1] += AR_NOW() - t2;
+                if (w == 0 && lane == 0) {  // the walker's lateness behind the last fill wave
+                    unsigned long long lf = 0;
+                    for (int q = 0; q < W; ++q) lf = max(lf, s_arr[q]);
+                    pf[7] += s_arr[W] > lf ? s_arr[W] - lf : 0ull;
+                }
+                __syncthreads();  // s_arr is rewritten at the next interval
 #endif
             }
 #ifdef AR_PROF
@@ -622,6 +699,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 #ifdef AR_PROF
             pf[4] += AR_NOW() - t3;
             tA = AR_NOW();
+#endif
 #endif
             prev_n = n;
             cur ^= 1;

@@ -820,8 +820,8 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
         HIP_TRY(ctx, hipMemcpyFromSymbol(pf, HIP_SYMBOL(ar_prof), sizeof pf));
         HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(ar_prof), z, sizeof z));
         fprintf(stderr, "taxi2 arprof: k_alignr<%d,%d> grid %lld units %lld chains %llu | fill steps %llu barrier %llu setup %llu"
-                " | walker hops %llu drain %llu barrier %llu\n", v.K, v.W, (long long)grid, (long long)units, pf[6], pf[0],
-                pf[1], pf[2], pf[3], pf[4], pf[5]);
+                " | walker hops %llu drain %llu barrier %llu | walker late %llu\n", v.K, v.W, (long long)grid, (long long)units,
+                pf[6], pf[0], pf[1], pf[2], pf[3], pf[4], pf[5], pf[7]);
     }
 #endif
     if (shared_release(ctx, st)) return -1;
