@@ -284,6 +284,18 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
                          const int64_t* label_offs, int decimals, const uint8_t* missing, int32_t missing_len,
                          uint8_t* out, int64_t cap, int64_t* out_len);
 
+/* Host-only (no context): the text of the subset statistics files (versus_all.py:642-684, written by
+ * tasks/subsets.py write_subset_statistics) for a partition of ns subsets and m metrics, with the
+ * handlers' "{:.Nf}" formatter (N = decimals) and missing text "NA".  mean / mn / mx / count are
+ * [ns][ns][m] (subset of x, subset of y, metric); names: the subsets' display names, packed.
+ * part 0: linear/pairs.tsv lines (a != b): name_a TAB name_b (TAB mean TAB min TAB max) per metric;
+ * part 1: linear/identity.tsv lines (a == b): name_a (TAB mean TAB min TAB max) per metric;
+ * part 2 + k: matricial/<metric k>.tsv rows: name_a (TAB "mean (min-max)" or "NA" when count is 0).
+ * Headers are the caller's.  Returns 1 when cap < *out_len (nothing written). */
+int taxi2_format_subset_stats(int64_t ns, int m, const double* mean, const double* mn, const double* mx,
+                              const int64_t* count, const uint8_t* names, const int64_t* name_offs, int decimals,
+                              int part, uint8_t* out, int64_t cap, int64_t* out_len, int threads);
+
 /* ---- subset aggregation (versus_all.py:57-96 SimpleAggregator / DistanceAggregator, fed by
  * _aggregate_distances :617-640) ------------------------------------------------------------ *
  * Host-only (no context).  d[n][n][m]: the (x100-adjusted) ordered-pair values, non-finite = None;

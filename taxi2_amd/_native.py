@@ -53,6 +53,7 @@ EXPORTS = (
     "taxi2_format_ragged",
     "taxi2_format_summary",
     "taxi2_subset_aggregate",
+    "taxi2_format_subset_stats",
     "taxi2_subset_aggregate_dev",
     "taxi2_dereplicate_walk",
 )
@@ -125,6 +126,8 @@ _SIGNATURES = {
     "taxi2_format_summary": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _INT, _INT,
                                     _P, _P, _INT, _P, _I32, _P, _I64, ctypes.POINTER(_I64)]),
     "taxi2_subset_aggregate": (_INT, [_P, _I64, _INT, _P, _I32, _P, _P, _P, _P, _INT]),
+    "taxi2_format_subset_stats": (_INT, [_I64, _INT, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _I64,
+                                         ctypes.POINTER(_I64), _INT]),
     "taxi2_subset_aggregate_dev": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _I32, _INT, _P, _P, _P, _P, _P]),
     "taxi2_dereplicate_walk": (_INT, [_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, ctypes.POINTER(_I64), _P,
                                       _P, _I64, ctypes.POINTER(_I64), _P]),
@@ -826,6 +829,30 @@ def subset_aggregate(d: np.ndarray, code, ns: int, threads: int = 0) -> Aggregat
     if rc != 0:
         raise NativeError(f"taxi2_subset_aggregate: bad arguments ({rc})")
     return Aggregates(*out)
+
+
+def format_subset_stats(mean: np.ndarray, mn: np.ndarray, mx: np.ndarray, count: np.ndarray, names,
+                        decimals: int, part: int, threads: int = 0) -> bytes:
+    """Text of one subset statistics file (taxi2_format_subset_stats, host code: part 0 pairs.tsv
+    lines, 1 identity.tsv lines, 2 + k matricial rows of metric k; no headers)."""
+    lib = load_library()
+    ns, _, m = mean.shape
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (mean, mn, mx)]
+    cnt = np.ascontiguousarray(count, dtype=np.int64)
+    nb, no = pack_strings(names)
+    cap = ctypes.c_int64(0)
+    est = int(ns * ns * (9 * m * 8 + 64) + 1024)
+    for _ in range(2):
+        buf = np.empty(max(1, est), dtype=np.uint8)
+        rc = lib.taxi2_format_subset_stats(ns, m, *[a.ctypes.data for a in arrs], cnt.ctypes.data, nb.ctypes.data,
+                                           no.ctypes.data, int(decimals), int(part), buf.ctypes.data, buf.size,
+                                           ctypes.byref(cap), int(threads))
+        if rc < 0:
+            raise NativeError(f"taxi2_format_subset_stats: bad arguments ({rc})")
+        if rc == 0:
+            return buf[: cap.value].tobytes()
+        est = cap.value
+    raise NativeError("taxi2_format_subset_stats: output size changed")
 
 
 class Walk(NamedTuple):

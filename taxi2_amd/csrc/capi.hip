@@ -2222,6 +2222,88 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     return 0;
 }
 
+int taxi2_format_subset_stats(int64_t ns, int m, const double* mean, const double* mn, const double* mx,
+                              const int64_t* count, const uint8_t* names, const int64_t* name_offs, int decimals,
+                              int part, uint8_t* out, int64_t cap, int64_t* out_len, int threads) {
+    if (ns < 0 || m < 1 || decimals < 0 || decimals > FMT_MAX_DECIMALS || !out_len || part < 0 || part >= 2 + m)
+        return -1;
+    if (ns > 0 && (!mean || !mn || !mx || !count || !names || !name_offs)) return -1;
+    // one token: Python "{:.Nf}" of a finite value, "NA" otherwise (subsets._text)
+    auto tok = [&](double v, std::string& o) {
+        if (!std::isfinite(v)) {
+            o += "NA";
+            return;
+        }
+        char b[400];
+        const int L = fmt_fixed(v, decimals, b);
+        o.append(b, (size_t)L);
+    };
+    auto name = [&](int64_t a, std::string& o) {
+        o.append((const char*)names + name_offs[a], (size_t)(name_offs[a + 1] - name_offs[a]));
+    };
+    // rows of the part: pairs (a != b), identity (a == b), or the matricial rows of metric part - 2
+    const int64_t nrows = part == 0 ? ns * ns : ns;
+    if (threads <= 0) threads = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, std::max<int64_t>(1, nrows / 1024)));
+    std::vector<std::string> chunk((size_t)threads);
+    auto work = [&](int t) {
+        std::string& o = chunk[(size_t)t];
+        const int64_t r0 = nrows * t / threads, r1 = nrows * (t + 1) / threads;
+        for (int64_t r = r0; r < r1; ++r) {
+            if (part == 0 || part == 1) {
+                const int64_t a = part == 0 ? r / ns : r, b = part == 0 ? r % ns : r;
+                if (part == 0 && a == b) continue;
+                name(a, o);
+                if (part == 0) {
+                    o += '\t';
+                    name(b, o);
+                }
+                const int64_t q = (a * ns + b) * m;
+                for (int k = 0; k < m; ++k) {
+                    o += '\t';
+                    tok(mean[q + k], o);
+                    o += '\t';
+                    tok(mn[q + k], o);
+                    o += '\t';
+                    tok(mx[q + k], o);
+                }
+            } else {
+                const int k = part - 2;
+                name(r, o);
+                for (int64_t b = 0; b < ns; ++b) {
+                    const int64_t q = (r * ns + b) * m + k;
+                    o += '\t';
+                    if (!count[q]) {
+                        o += "NA";
+                        continue;
+                    }
+                    tok(mean[q], o);
+                    o += " (";
+                    tok(mn[q], o);
+                    o += '-';
+                    tok(mx[q], o);
+                    o += ')';
+                }
+            }
+            o += '\n';
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    int64_t total = 0;
+    for (const auto& c : chunk) total += (int64_t)c.size();
+    *out_len = total;
+    if (total > cap) return 1;
+    int64_t o = 0;
+    for (const auto& c : chunk) {
+        std::memcpy(out + o, c.data(), c.size());
+        o += (int64_t)c.size();
+    }
+    return 0;
+}
+
 int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* code, int32_t ns, double* sum,
                            double* mn, double* mx, int64_t* count, int threads) {
     if (n < 0 || m < 1 || ns < 0 || (n > 0 && (!d || !code || !sum || !mn || !mx || !count))) return -1;

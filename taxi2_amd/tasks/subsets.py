@@ -323,6 +323,10 @@ def write_subset_statistics(path: Path, st: SubsetStats, metrics: list, fmt: str
     labels = [f"{m} {s}" for m in metrics for s in ("mean", "min", "max")]
     ns, m = len(st.subsets), len(metrics)
     names = ["?" if v is None else v for v in st.subsets]
+    dec = fixed_decimals(fmt)
+    if ns and dec is not None and all(gpu_text_ok(a, dec) for a in (st.mean, st.min, st.max)):
+        _write_subset_statistics_native(path, st, metrics, names, labels, dec, template)
+        return
     per = 3 * m
     # tok[(a * ns + b) * per + 3 k + s]: stat s (mean / min / max) of metric k for key (a, b)
     tok = _tokens(np.stack([st.mean, st.min, st.max], axis=-1), fmt, eng) if ns else []
@@ -370,3 +374,37 @@ def write_subset_statistics(path: Path, st: SubsetStats, metrics: list, fmt: str
                 if len(rows) >= 256 or a == ns - 1:
                     fh.write("\n".join(rows) + "\n")
                     rows = []
+
+
+def _write_subset_statistics_native(path: Path, st: SubsetStats, metrics: list, names: list, labels: list, dec: int,
+                                    template: str) -> None:
+    """write_subset_statistics through the engine library's host formatter (taxi2_format_subset_stats:
+    the same bytes, "{:.Nf}" exact, threaded): a 1 000-species partition is 3 M formatted cells, ~2 s
+    of Python string joins per partition otherwise."""
+    from .._native import format_subset_stats
+
+    lin = Path(path) / "linear"
+    mean, mn, mx, cnt = st.mean, st.min, st.max, st.count
+    with open(lin / "pairs.tsv", "wb") as fp:
+        body = format_subset_stats(mean, mn, mx, cnt, names, dec, 0)
+        if body:
+            fp.write(("\t".join(("target", "query", *labels)) + "\n").encode())
+            fp.write(body)
+    with open(lin / "identity.tsv", "wb") as fi:
+        fi.write(("\t".join(("target", *labels)) + "\n").encode())
+        fi.write(format_subset_stats(mean, mn, mx, cnt, names, dec, 1))
+    mat = Path(path) / "matricial"
+    create_parents(mat)
+    simple = template == "{mean} ({min}-{max})"
+    for k, metric in enumerate(metrics):
+        with open(mat / f"{metric}.tsv", "wb") as fh:
+            fh.write(("\t".join(("", *names)) + "\n").encode())
+            if simple:
+                fh.write(format_subset_stats(mean, mn, mx, cnt, names, dec, 2 + k))
+                continue
+            fmt = "{:.%df}" % dec
+            for a in range(len(names)):
+                cells = [template.format(mean=_text(mean[a, b, k], fmt), min=_text(mn[a, b, k], fmt),
+                                         max=_text(mx[a, b, k], fmt)) if cnt[a, b, k] else "NA"
+                         for b in range(len(names))]
+                fh.write(("\t".join((names[a], *cells)) + "\n").encode())
