@@ -132,6 +132,17 @@ int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64
                          const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* d_out,
                          int32_t* d_scores, void* stream);
 
+/* Row block of the streamed pre-aligned versusAll (versus_all.py:732-773 fed block by block, the
+ * reductions of config 5): as taxi2_rect_pairs_dev on PREALIGNED sets, with the task's epilogue
+ * fused -- every value x scale (percentage_multiply), NaN on x == y when diag (set_q == set_r: the
+ * diagonal rule for unique full tuples, versus_all.py:549) -- and, when rmin_metric >= 0, each
+ * row's first minimum of that metric over its defined values (-0.0 == 0.0, ties to the lower
+ * column): d_rmin_idx[q - q0] (-1: none) and d_rmin_val[q - q0] (NaN: none).  Asynchronous on
+ * `stream`; uses the context's staging buffer (one call at a time per context). */
+int taxi2_rect_block_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const int32_t* metrics,
+                         int nmetrics, double scale, int diag, int rmin_metric, int64_t* d_rmin_idx, double* d_rmin_val,
+                         double* d_out, void* stream);
+
 /* ---- explicit pair list (align.py:50-51 align_pairs, distances.py:297 calculate) ------- *
  * Pairs (xs[k] of set_x, ys[k] of set_y): out[count][2][nmetrics] in ALIGN mode
  * ([k][0] = (x, y), [k][1] = (y, x)), out[count][nmetrics] in PREALIGNED mode. */

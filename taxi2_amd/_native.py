@@ -39,6 +39,7 @@ EXPORTS = (
     "taxi2_counts_metrics_dev",
     "taxi2_rect_pairs",
     "taxi2_rect_pairs_dev",
+    "taxi2_rect_block_dev",
     "taxi2_rect_strings_dev",
     "taxi2_tri_strings_dev",
     "taxi2_format_pairs_ptr_dev",
@@ -103,6 +104,8 @@ _SIGNATURES = {
     "taxi2_counts_metrics_dev": (_INT, [_P, _P, _I64, _P, _INT, ctypes.c_double, _P, _P]),
     "taxi2_rect_pairs": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_rect_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
+    "taxi2_rect_block_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _P, _INT, ctypes.c_double, _INT, _INT, _P, _P, _P,
+                                    _P]),
     "taxi2_rect_strings_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _I32, _P, _P,
                                       _P, _P]),
     "taxi2_format_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
@@ -432,6 +435,24 @@ class Engine:
                     ctypes.c_void_p(stream) if stream else None,
                 ),
                 "taxi2_rect_pairs_dev",
+            )
+
+    def rect_block_dev(self, s: SeqSet, q0: int, q1: int, metrics, out_ptr: int, scale: float = 1.0,
+                       diag: bool = True, rmin_metric: int = -1, rmin_idx_ptr: int | None = None,
+                       rmin_val_ptr: int | None = None, stream: int | None = None) -> None:
+        """Row block [q0, q1) x set of the streamed pre-aligned versusAll with the task's epilogue on the
+        GPU (taxi2_rect_block_dev): values x scale, NaN on the diagonal, each row's first minimum of
+        metric index rmin_metric (idx -1 / NaN: none)."""
+        codes = metric_codes(metrics)
+        with self._lock:
+            self._check(
+                self._lib.taxi2_rect_block_dev(
+                    self._ctx, s.id, s.id, int(q0), int(q1), codes.ctypes.data, len(codes), float(scale),
+                    1 if diag else 0, int(rmin_metric), ctypes.c_void_p(rmin_idx_ptr) if rmin_idx_ptr else None,
+                    ctypes.c_void_p(rmin_val_ptr) if rmin_val_ptr else None, ctypes.c_void_p(out_ptr),
+                    ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_rect_block_dev",
             )
 
     def rect_strings_dev(self, q: SeqSet, r: SeqSet, q0: int, q1: int, metrics, out_ptr: int | None, cap: int,

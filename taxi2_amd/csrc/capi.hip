@@ -985,11 +985,11 @@ static int64_t tri_row_host(int64_t g, int64_t N) {
 }
 
 int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const PairSrc& ps,
-                      const MetricSpec& ms, double* d_out, hipStream_t st) {
+                      const MetricSpec& ms, double* d_out, hipStream_t st, TileBlock tb = TileBlock{1.0, 0, -1, nullptr, nullptr}) {
     if (ps.count <= 0) return 0;
     // triangle / rectangle blocks: PT x PT pair tiles with LDS-staged planes (prealigned_kernel.hpp);
     // TAXI2_PRE_NOTILE=1 keeps the one-thread-per-pair kernel (A/B and parity tests)
-    if (ps.mode != PAIRS_LIST && ps.count >= 4096 && !getenv("TAXI2_PRE_NOTILE")) {
+    if (ps.mode != PAIRS_LIST && (ps.count >= 4096 || tb.rmin_v) && !getenv("TAXI2_PRE_NOTILE")) {
         int64_t x0, nx, y0, ny;
         if (ps.mode == PAIRS_TRI) {
             const int64_t a0 = tri_row_host(ps.k0, ps.N), a1 = tri_row_host(ps.k0 + ps.count - 1, ps.N);
@@ -1008,13 +1008,14 @@ int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const Pa
         const int nwords = (std::max(X.max_len, Y.max_len) + 31) / 32;
         if (ps.mode == PAIRS_TRI)
             hipLaunchKernelGGL(k_prealigned_tile<PAIRS_TRI>, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0, st,
-                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out);
+                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out, tb);
         else
             hipLaunchKernelGGL(k_prealigned_tile<PAIRS_RECT>, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0, st,
-                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out);
+                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out, tb);
         HIP_TRY(ctx, hipGetLastError());
         return 0;
     }
+    if (tb.rmin_v || tb.diag || tb.scale != 1.0) return fail(ctx, "row-block epilogue needs the tiled kernel");
     const int64_t blocks = std::min<int64_t>((ps.count + 255) / 256, (int64_t)ctx->num_cus * 64);
     hipLaunchKernelGGL(k_prealigned, dim3((unsigned)blocks), dim3(256), 0, st, view(X), view(Y), ps,
                        ms, d_out);
@@ -1552,6 +1553,42 @@ int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64
         return launch_align_pairs(ctx, *Q, *R, ps, sc, ms, OUT_AB, d_out, d_scores, st);
     }
     return launch_prealigned(ctx, *Q, *R, ps, ms, d_out, st);
+}
+
+int taxi2_rect_block_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const int32_t* metrics,
+                         int nmetrics, double scale, int diag, int rmin_metric, int64_t* d_rmin_idx, double* d_rmin_val,
+                         double* d_out, void* stream) {
+    if (!ctx) return -1;
+    DevSet* Q = get_set(ctx, set_q);
+    DevSet* R = get_set(ctx, set_r);
+    if (!Q || !R) return fail(ctx, "unknown set");
+    if (Q->mode != TAXI2_MODE_PREALIGNED || R->mode != TAXI2_MODE_PREALIGNED)
+        return fail(ctx, "taxi2_rect_block_dev: PREALIGNED sets only");
+    MetricSpec ms;
+    if (check_metrics(ctx, metrics, nmetrics, ms, false, std::max(Q->max_len, R->max_len))) return -1;
+    if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
+    if (rmin_metric >= nmetrics || (rmin_metric >= 0 && (!d_rmin_idx || !d_rmin_val)))
+        return fail(ctx, "bad row-minimum metric or outputs");
+    if (diag && set_q != set_r) return fail(ctx, "the diagonal rule needs one set on both sides");
+    if ((q1 - q0) * R->n > 0 && !d_out) return fail(ctx, "null output");
+    if (q1 == q0 || R->n == 0) return 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    PairSrc ps{PAIRS_RECT, q0 * R->n, (q1 - q0) * R->n, 0, R->n, nullptr, nullptr};
+    const int64_t nx = q1 - q0, tiles_y = (R->n + PT - 1) / PT;
+    TileBlock tb{scale, diag ? 1 : 0, rmin_metric, nullptr, nullptr};
+    if (rmin_metric >= 0) {
+        if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)nx * tiles_y * 16)) return -1;
+        tb.rmin_v = (double*)ctx->d_aux;
+        tb.rmin_y = (int64_t*)ctx->d_aux + nx * tiles_y;
+    }
+    if (launch_prealigned(ctx, *Q, *R, ps, ms, d_out, st, tb)) return -1;
+    if (rmin_metric >= 0) {
+        hipLaunchKernelGGL(k_rowmin_finish, dim3((unsigned)((nx + 3) / 4)), dim3(256), 0, st, nx, tiles_y, tb.rmin_v,
+                           tb.rmin_y, d_rmin_idx, d_rmin_val);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return 0;
 }
 
 int taxi2_list_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys,

@@ -77,13 +77,31 @@ constexpr int PT = 64;        // sequences per tile side
 constexpr int PWC = 16;       // plane words staged per chunk
 constexpr int PWS = PWC + 1;  // padded LDS row (uint4): 16 lanes reading 16 rows hit 64 distinct banks
 
+// Row-block epilogue of the streamed versusAll (config 5; taxi2_rect_block_dev): every value x scale
+// (the task's x100, the same f64 multiply as D * 100), the diagonal rule's NaN on x == y (one set on
+// both sides), and per (x row, tile) the first minimum of metric rmin_k over the tile's defined values
+// (-0.0 == 0.0, ties to the lower y), reduced per row by k_rowmin_finish.
+struct TileBlock {
+    double scale;
+    int diag, rmin_k;
+    double* rmin_v;   // [nx][tiles_y]: tile minimum (+inf: none)
+    int64_t* rmin_y;  // its column (-1: none)
+};
+struct RowMin {
+    double v;
+    int64_t y;
+};
+__device__ __forceinline__ bool rowmin_less(double a, int64_t ya, double b, int64_t yb) {
+    return a < b || (a == b && ya < yb);
+}
+
 // Tile grid: x rows [x0, x0 + nx), y columns [y0, y0 + ny); tiles_y tiles per tile row.
 // MODE PAIRS_TRI: pair (a, b) exists for b > a, output slot tri(a, b) - ps.k0 when that lies in
 // [0, ps.count); PAIRS_RECT: output slot (a * ps.R + b) - ps.k0 (b indexes YS).
 template <int MODE>
 __global__ void __launch_bounds__(256)
 k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, int64_t y0, int64_t ny,
-                  int64_t tiles_y, int nwords, MetricSpec ms, double* __restrict__ out) {
+                  int64_t tiles_y, int nwords, MetricSpec ms, double* __restrict__ out, TileBlock tb) {
     __shared__ uint4 sx[PT * PWS], sy[PT * PWS];
     const int tid = (int)threadIdx.x;
     const int tx = tid & 15, ty = tid >> 4;
@@ -140,8 +158,12 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
         }
     }
     const int nm = ms.n;
+    double rv[4];
+    int64_t ry[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+        rv[i] = __builtin_inf();
+        ry[i] = -1;
         const int64_t x = xa + tx + 16 * i;
         if (x >= xe) continue;
 #pragma unroll
@@ -157,9 +179,72 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
                 slot = x * ps.R + y - ps.k0;
                 if (slot < 0 || slot >= ps.count) continue;  // a launch may start / end inside a row
             }
-            for (int m = 0; m < nm; ++m)
-                out[slot * nm + m] = metric_value(ms.code[m], c[i][j][0], c[i][j][1], c[i][j][2], c[i][j][3]);
+            const bool none = tb.diag && x == y;
+            for (int m = 0; m < nm; ++m) {
+                const double v = none ? __builtin_nan("")
+                                      : metric_value(ms.code[m], c[i][j][0], c[i][j][1], c[i][j][2], c[i][j][3]) * tb.scale;
+                out[slot * nm + m] = v;
+                // j ascending is y ascending: the first of equal values stays
+                if (m == tb.rmin_k && __builtin_isfinite(v) && v < rv[i]) {
+                    rv[i] = v;
+                    ry[i] = y;
+                }
+            }
         }
+    }
+    if (tb.rmin_v) {  // per (row, tile): the 16 threads of a row (ty = 0..15) through LDS, in y order
+        __syncthreads();  // the plane stages are free
+        RowMin* red = (RowMin*)sx;  // [ty][64 rows]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[ty * PT + tx + 16 * i] = RowMin{rv[i], ry[i]};
+        __syncthreads();
+        if (tid < PT) {
+            double v = __builtin_inf();
+            int64_t y = -1;
+            for (int t = 0; t < 16; ++t) {
+                const RowMin r = red[t * PT + tid];
+                if (r.y >= 0 && (y < 0 || rowmin_less(r.v, r.y, v, y))) {
+                    v = r.v;
+                    y = r.y;
+                }
+            }
+            const int64_t x = xa + tid;
+            if (x < xe) {
+                tb.rmin_v[(x - x0) * tiles_y + by] = v;
+                tb.rmin_y[(x - x0) * tiles_y + by] = y;
+            }
+        }
+    }
+}
+
+// Per row of a block: the first minimum over its tiles (in y order) -> idx (-1: none) and value (NaN).
+__global__ void __launch_bounds__(256) k_rowmin_finish(int64_t nx, int64_t tiles_y, const double* __restrict__ tv,
+                                                        const int64_t* __restrict__ ty_, int64_t* __restrict__ idx,
+                                                        double* __restrict__ val) {
+    const int lane = threadIdx.x & 63;
+    const int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (x >= nx) return;
+    double v = __builtin_inf();
+    int64_t y = -1;
+    for (int64_t t = lane; t < tiles_y; t += 64) {
+        const double a = tv[x * tiles_y + t];
+        const int64_t ya = ty_[x * tiles_y + t];
+        if (ya >= 0 && (y < 0 || rowmin_less(a, ya, v, y))) {
+            v = a;
+            y = ya;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a = __shfl_xor(v, o);
+        const int64_t ya = __shfl_xor(y, o);
+        if (ya >= 0 && (y < 0 || rowmin_less(a, ya, v, y))) {
+            v = a;
+            y = ya;
+        }
+    }
+    if (lane == 0) {
+        idx[x] = y;
+        val[x] = y >= 0 ? v : __builtin_nan("");
     }
 }
 

@@ -737,6 +737,8 @@ class VersusAll:
             ids = pack_strings(sink.ids)
         pairs_text = None
 
+        fused = [None]  # the block's fused row minima (pre-aligned, taxi2_rect_block_dev)
+
         def block(x0, x1):
             nonlocal pairs_text
             t = perf_counter()
@@ -754,6 +756,18 @@ class VersusAll:
                                                   stream=stream.cuda_stream)
                 del sx, sy, sl
                 t = tick("text_s", t)
+            elif not p.pairs.align:
+                # pre-aligned: x100, the diagonal's NaN and the row minima fused into the tile kernel
+                k = sink.rmin_k if sink.rmin_k is not None else -1
+                if k >= 0:
+                    fused[0] = (torch.empty(x1 - x0, dtype=torch.int64, device=cuda),
+                                torch.empty(x1 - x0, dtype=torch.float64, device=cuda))
+                eng.rect_block_dev(st, x0, x1, labels, D.data_ptr(), scale, True, k,
+                                   fused[0][0].data_ptr() if k >= 0 else None,
+                                   fused[0][1].data_ptr() if k >= 0 else None, stream.cuda_stream)
+                sink.diagonal(x0, x1, D, scale, main=False)
+                tick("compute_s", t)
+                return D
             else:
                 eng.rect_pairs_dev(st, st, x0, x1, labels, D.data_ptr(), scores, None, stream.cuda_stream)
             if scale != 1.0:
@@ -765,9 +779,10 @@ class VersusAll:
         try:
             for x0 in range(r0, r1, B):
                 x1 = min(r1, x0 + B)
+                fused[0] = None
                 D = block(x0, x1)
                 t = perf_counter()
-                sink.row_minima(x0, x1, D)
+                sink.row_minima(x0, x1, D, fused[0])
                 if not sharded:
                     sink.aggregate(x0, x1, D)
                 t = tick("reduce_s", t)
@@ -1064,7 +1079,7 @@ class _BlockWriters:
     def has_text(self) -> bool:
         return any(f is not None for f in (self.lin, self.summ, self.pairs_fh)) or bool(self.mats)
 
-    def diagonal(self, x0: int, x1: int, D, scale: float) -> None:
+    def diagonal(self, x0: int, x1: int, D, scale: float, main: bool = True) -> None:
         """Diagonal rule (versus_all.py:549) on rows [x0, x1): every (x, x) is None (one indexed
         store for the block), then the groups of identical full tuples with more than one member
         (every pair inside is None) and the sequences whose alignment with themselves is not the
@@ -1079,8 +1094,9 @@ class _BlockWriters:
             special.sort()
             self._special = special
             self._special_rows = np.array([i for i, _ in special], dtype=np.int64)
-        r = torch.arange(x1 - x0, device=D.device)
-        D[r, r + x0] = float("nan")
+        if main:  # (taxi2_rect_block_dev sets the diagonal's NaN itself)
+            r = torch.arange(x1 - x0, device=D.device)
+            D[r, r + x0] = float("nan")
         lo, hi = np.searchsorted(self._special_rows, [x0, x1])
         for i, gi in self._special[lo:hi]:
             g = dup[gi]
@@ -1094,8 +1110,26 @@ class _BlockWriters:
         for _, agg in self.aggs:
             agg.add(D, x0, x1)
 
-    def row_minima(self, x0: int, x1: int, D) -> None:
+    def row_minima(self, x0: int, x1: int, D, fused=None) -> None:
+        """Each row's first minimum over defined values (-0.0 == 0.0), None skipped.  `fused`: the
+        (index, value) device tensors taxi2_rect_block_dev computed with the diagonal's NaN; rows of
+        groups the diagonal rule changed afterwards (duplicate full tuples) are redone from D."""
         torch = self.torch
+        if self.rmin_k is not None and fused is not None:
+            idx, val = fused
+            self.rmin_idx[x0:x1] = idx.cpu().numpy()
+            self.rmin_d[x0:x1] = val.cpu().numpy()
+            lo, hi = np.searchsorted(self._special_rows, [x0, x1])
+            rows = np.unique(self._special_rows[lo:hi])
+            if rows.size:
+                rr = torch.as_tensor(rows - x0, device=D.device)
+                v = D[rr][:, :, self.rmin_k]
+                v = torch.where(torch.isfinite(v), v, torch.full_like(v, float("inf")))
+                d, ix = torch.min(v, dim=1)
+                ok = torch.isfinite(d)
+                self.rmin_idx[rows] = torch.where(ok, ix, torch.full_like(ix, -1)).cpu().numpy()
+                self.rmin_d[rows] = torch.where(ok, d, torch.full_like(d, float("nan"))).cpu().numpy()
+            return
         if self.rmin_k is not None:  # first minimum over defined values (-0.0 == 0.0), None skipped
             v = D[:, :, self.rmin_k]
             v = torch.where(torch.isfinite(v), v, torch.full_like(v, float("inf")))
