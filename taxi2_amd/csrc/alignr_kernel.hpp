@@ -38,7 +38,7 @@ namespace taxi2 {
 #endif
 constexpr int AR_BLK = 16;  // steps between progress checks / publications
 #ifndef TAXI2_AR_UNITS
-#define TAXI2_AR_UNITS 4
+#define TAXI2_AR_UNITS 8
 #endif
 constexpr int AR_UNITS = TAXI2_AR_UNITS;  // units (row sequences, up to two pairs each) per chain
 

@@ -53,6 +53,7 @@ struct DevSet {
 struct taxi2_ctx {
     int device = 0;
     int num_cus = 0;
+    size_t total_mem = 0;  // device memory (bytes)
     int reserve_cus = 0;  // packed aligner launches leave this many CUs' worth of workgroups free
     hipStream_t stream = nullptr;
     std::string err;
@@ -764,7 +765,9 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     int chunk = 0;
     if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(AR_UNITS, (atoi(c) + 1) / 2));
     int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(AR_UNITS, units / (grid * 8)));
-    double budget_gb = 80.0;
+    // trace buffers: two per resident workgroup, AR_UNITS rows of sequences each (8 x 1 000 bp: 33 MB);
+    // up to 120 GB of the 288 GB HBM, at most 45 % of the device's memory (TAXI2_AT_TRACE_GB overrides)
+    double budget_gb = std::min(120.0, 0.45 * (double)ctx->total_mem / 1e9);
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     auto buf_bytes = [&](int64_t e) { return at_buf_bytes((int)e * std::max(1, Y.max_len), 4 * v.K, v.W); };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
@@ -989,7 +992,9 @@ int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const Pa
     if (ps.count <= 0) return 0;
     // triangle / rectangle blocks: PT x PT pair tiles with LDS-staged planes (prealigned_kernel.hpp);
     // TAXI2_PRE_NOTILE=1 keeps the one-thread-per-pair kernel (A/B and parity tests)
-    if (ps.mode != PAIRS_LIST && (ps.count >= 4096 || tb.rmin_v) && !getenv("TAXI2_PRE_NOTILE")) {
+    // (the row-block epilogue of taxi2_rect_block_dev exists only in the tiled kernel)
+    const bool epi = tb.rmin_v || tb.diag || tb.scale != 1.0;
+    if (ps.mode != PAIRS_LIST && (epi || (ps.count >= 4096 && !getenv("TAXI2_PRE_NOTILE")))) {
         int64_t x0, nx, y0, ny;
         if (ps.mode == PAIRS_TRI) {
             const int64_t a0 = tri_row_host(ps.k0, ps.N), a1 = tri_row_host(ps.k0 + ps.count - 1, ps.N);
@@ -1015,7 +1020,7 @@ int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const Pa
         HIP_TRY(ctx, hipGetLastError());
         return 0;
     }
-    if (tb.rmin_v || tb.diag || tb.scale != 1.0) return fail(ctx, "row-block epilogue needs the tiled kernel");
+    if (epi) return fail(ctx, "row-block epilogue needs a triangle or rectangle launch");
     const int64_t blocks = std::min<int64_t>((ps.count + 255) / 256, (int64_t)ctx->num_cus * 64);
     hipLaunchKernelGGL(k_prealigned, dim3((unsigned)blocks), dim3(256), 0, st, view(X), view(Y), ps,
                        ms, d_out);
@@ -1292,6 +1297,7 @@ int taxi2_ctx_create(int device, taxi2_ctx** out) {
         return -5;
     }
     ctx->num_cus = prop.multiProcessorCount;
+    ctx->total_mem = prop.totalGlobalMem;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return -6;
