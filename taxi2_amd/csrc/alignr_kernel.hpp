@@ -73,8 +73,10 @@ struct ArWalk {
 };
 
 // Row record (LDS, one per chain row): .x = byte offset of the row base's table (eqt) for an
-// A/C/G/T byte, .y = band lo (byte 0) and width (byte 1) in lanes, the row byte (byte 2) and flags.
-constexpr uint32_t AR_PRE = 1u << 31;    // first row of a unit or a byte other than A/C/G/T
+// A/C/G/T byte, .y = band lo (byte 0) and width (byte 1) in lanes, the row byte (byte 2) and flags,
+// .z = the row's Iy open as a pk_int addend (the "open-shifted" cells below), .w = the column-0
+// boundary B(i, 0) = 0 in that form.
+constexpr uint32_t AR_PRE = 1u << 31;    // first or last row of a unit, or a byte other than A/C/G/T
 constexpr uint32_t AR_LAST = 1u << 30;   // last row of a unit
 constexpr uint32_t AR_FIRST = 1u << 29;  // first row of a unit
 constexpr uint32_t AR_OTHER = 1u << 28;  // byte other than A/C/G/T (byte-compare substitution)
@@ -82,6 +84,15 @@ constexpr uint32_t AR_NOBAND = 0x0080u;  // lo 128, width 0: no lane stores
 
 // Default scores in drift coordinates (dz = ie = -1): substitution ma - 2 dz / mi - 2 dz, opens
 // relative to the extend, the column-0 / row-0 boundary 0.
+//
+// Open-shifted cells.  The state kept per cell is G = B + o_i (the best score plus the row's Iy
+// open) instead of B: then Ix(i, j) = max(G(i-1, j), Ix(i-1, j)) and Iy(i, j) = max(G(i, j-1),
+// Iy(i, j-1)) need no add, and M(i, j) = G(i-1, j-1) + (s - co_i) takes the open into the table
+// word -- one add per cell (G = B + o_i) instead of two (B + co for Ix and for Iy).  o_i is the
+// internal open except on a unit's last row (the end-gap open), whose G feeds nothing but its own
+// row's Iy (the next row is a unit's first, whose states are reset).  The end column's Ix open
+// (slot K - 1 of its owner lane) adds cend - co_i once per step.  M, Ix, Iy and the trace are the
+// same values as before; only the stored best is shifted.
 constexpr int AR_EQ_MATCH = 3, AR_EQ_MISMATCH = 1, AR_CO_I = -7, AR_CO_E = 0;
 
 __device__ __forceinline__ uint32_t ar_pk_int(int lo, int hi) { return pk_int(pk2(lo, hi)); }
@@ -101,11 +112,17 @@ __device__ __forceinline__ void ar_band_lanes(int i, int nA, int nB, int off, in
     hi = (jh + off - 1) / K;
 }
 
+// the .z / .w words of a record: the row's open (pk_int) and B = 0 shifted by it (a biased pattern)
+__device__ __forceinline__ uint4 ar_record(uint32_t x, uint32_t y, bool last) {
+    const uint32_t o = last ? ar_pk_int(AR_CO_E, AR_CO_E) : ar_pk_int(AR_CO_I, AR_CO_I);
+    return make_uint4(x, y, o, pk2b(0, 0) + o);
+}
+
 template <int K, int W>
-__device__ __forceinline__ uint2 ar_row_record(const ArRow* __restrict__ tab, const ArChain& ch, int n, int rows, int g,
+__device__ __forceinline__ uint4 ar_row_record(const ArRow* __restrict__ tab, const ArChain& ch, int n, int rows, int g,
                                                int band) {
     constexpr int NT = 64 * W;
-    if (g < 0 || g >= rows) return make_uint2(0u, AR_NOBAND);
+    if (g < 0 || g >= rows) return ar_record(0u, AR_NOBAND, false);
     int t = 0;
     for (int q = 1; q < n; ++q)
         if (tab[q].r0 <= g) t = q;
@@ -118,7 +135,7 @@ __device__ __forceinline__ uint2 ar_row_record(const ArRow* __restrict__ tab, co
     if (ec < 4u) x = ec * (uint32_t)(NT * K * 4);
     else y |= AR_OTHER | AR_PRE;
     if (i == 0) y |= AR_FIRST | AR_PRE;
-    if (i == r.nA - 1) y |= AR_LAST;
+    if (i == r.nA - 1) y |= AR_LAST | AR_PRE;
     int lo = 0x7FFF, hi = -1;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -129,11 +146,13 @@ __device__ __forceinline__ uint2 ar_row_record(const ArRow* __restrict__ tab, co
         hi = max(hi, u);
     }
     y |= hi < lo ? AR_NOBAND : ((uint32_t)lo | ((uint32_t)(hi - lo) << 8));
-    return make_uint2(x, y);
+    return ar_record(x, y, i == r.nA - 1);
 }
 
+// <= 128 VGPRs: 4 waves per SIMD, so that the 5 workgroups of 3 waves the LDS allows fit a CU (the
+// launch bound alone lets the allocator take more and lose a workgroup per CU)
 template <int K, int W, int OCC>
-__global__ void __launch_bounds__(64 * (W + 1), OCC)
+__global__ void __launch_bounds__(64 * (W + 1), OCC) __attribute__((amdgpu_num_vgpr(128)))
 k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64_t total, int64_t npairs,
          MetricSpec ms, int chunk_req, int out_mode, double* __restrict__ out, int32_t* __restrict__ sout,
          uint8_t* __restrict__ trace, int64_t buf_bytes, int cap_rows, unsigned long long* __restrict__ next,
@@ -145,12 +164,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     constexpr int dz = -1;                          // default scores: ie
     const KScores sc{1, -1, -8, -1, -1, -1};        // align.py:20-27 defaults
     constexpr int NW = 4 * AR_UNITS;                // walks per chain (both orientations of 2 pairs per unit)
-    __shared__ uint2 xinfo[XR];
+    __shared__ uint4 xinfo[XR];
     __shared__ ArRow tab[2][AR_UNITS];
     __shared__ ArChain chs[2];
     __shared__ int fin[2][AR_UNITS][2];
     __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * RING];
-    __shared__ uint32_t eqt[4][NT][K];  // (s(x0_k, base), s(x1_k, base)) as pk_int, per lane and slot
+    __shared__ uint32_t eqt[4][NT][K];  // (s(x0_k, base), s(x1_k, base)) - co_i as pk_int, per lane and slot
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows, s_seg;
     __shared__ int s_fill;
@@ -443,13 +462,13 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         int s2[2];
 #pragma unroll
                         for (int hh = 0; hh < 2; ++hh)
-                            s2[hh] = jr[hh] < 1 ? 0 : (cb[hh] == (uint32_t)"ACGT"[rb] ? AR_EQ_MATCH : AR_EQ_MISMATCH);
+                            s2[hh] = (jr[hh] < 1 ? 0 : (cb[hh] == (uint32_t)"ACGT"[rb] ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
                         eqt[rb][tid][k] = ar_pk_int(s2[0], s2[1]);
                     }
                 }
             }
             if (tid < 64) xinfo[tid] = ar_row_record<K, W>(tab[cur], ch, n, rows, tid, band);
-            else if (tid < 128) xinfo[XR - 128 + tid] = make_uint2(0u, AR_NOBAND);
+            else if (tid < 128) xinfo[XR - 128 + tid] = ar_record(0u, AR_NOBAND, false);
             // lane's end-column Ix open (slot K - 1): the end-gap open in the half whose column nB_h
             // is this lane's last slot, the internal open elsewhere
             const int tq0 = w * 64 + lane;
@@ -457,16 +476,19 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             const uint32_t cend = ar_pk_int((ch.nB[0] > 0 && tq0 == nbv0 / K - 1) ? AR_CO_E : AR_CO_I,
                                             (ch.nB[1] > 0 && tq0 == nbv1 / K - 1) ? AR_CO_E : AR_CO_I);
             const int own0 = ch.nB[0] > 0 ? nbv0 / K - 1 : -1, own1 = ch.nB[1] > 0 ? nbv1 / K - 1 : -1;
-            const uint32_t ZERO = pk2b(0, 0);
+            const uint32_t COI = ar_pk_int(AR_CO_I, AR_CO_I);
+            const uint32_t GZ = pk2b(0, 0) + COI;  // B = 0 shifted by the internal open
+            const uint32_t cadj = cend - COI;      // the end column's Ix open over the internal one
             uint32_t stG[K], stX[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                stG[k] = ZERO;
+                stG[k] = GZ;
                 stX[k] = NEG16X2;
             }
-            uint32_t payF = NEG16X2, payY = NEG16X2, carry = ZERO;
+            uint32_t payF = NEG16X2, payY = NEG16X2, carry = GZ;
             uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
-            const uint32_t COI = ar_pk_int(AR_CO_I, AR_CO_I), OYD = ar_pk_int(AR_CO_E - AR_CO_I, AR_CO_E - AR_CO_I);
+            const int ln = __lane_id();
+            const uint32_t ln16 = (uint32_t)ln << 4;
             __syncthreads();  // xinfo block 0, tables
 #ifdef AR_PROF
             pf[2] += AR_NOW() - tA;
@@ -479,19 +501,19 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             auto step = [&](auto WIC, const int s) {
                 constexpr int WI = decltype(WIC)::value;
                 constexpr bool FW = WI == 0, HO = WI < W - 1;
-                int ln;
-                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
                 const int g = s - ln;
                 const int tq = WI * 64 + ln;
-                const uint2 rec = xinfo[g & (XR - 1)];
+                const uint4 rec = *(const uint4*)((const char*)xinfo + ((((uint32_t)s << 4) - ln16) & ((XR - 1) << 4)));
                 uint2 o_ring = make_uint2(0u, 0u);
                 if constexpr (!FW) o_ring = ring[(WI - 1) * RING + ((s + 1) & (RING - 1))];
                 const bool in_band = (uint8_t)((uint32_t)tq - rec.y) <= (uint8_t)(rec.y >> 8);
                 const uint64_t bmask = __builtin_amdgcn_ballot_w64(in_band);
                 asm volatile("" ::"s"(bmask));
+                const bool pre = (int)rec.y < 0;  // AR_PRE
+                const uint32_t orow = rec.z;      // the row's Iy open (pk_int)
                 uint32_t inF, inY;
-                if constexpr (FW) {  // column 0: B(i, 0) = 0, Iy(i, 0) = -inf (drift)
-                    inF = shr_old(payF, ZERO);
+                if constexpr (FW) {  // column 0: B(i, 0) = 0 (shifted: rec.w), Iy(i, 0) = -inf (drift)
+                    inF = shr_old(payF, rec.w);
                     inY = shr_old(payY, NEG16X2);
                 } else {
                     inF = shr_old(payF, o_ring.x);
@@ -514,14 +536,14 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         for (int k = 0; k < K; ++k) eq[k] = tp[k];
                     }
                 }
-                if ((int)rec.y < 0) {  // AR_PRE: a unit's first row, or a byte other than A/C/G/T
+                if (pre) {  // a unit's first or last row, or a byte other than A/C/G/T
                     if (rec.y & AR_FIRST) {  // row 0 of the new pair: B = 0, Ix = -inf, diagonal B(0, j0 - 1) = 0
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
-                            stG[k] = ZERO;
+                            stG[k] = GZ;
                             stX[k] = NEG16X2;
                         }
-                        carry = ZERO;
+                        carry = GZ;
                     }
                     if (rec.y & AR_OTHER) {  // byte compares against both halves' columns
                         const uint32_t rb = (rec.y >> 16) & 0xFFu;
@@ -532,36 +554,33 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                             for (int hh = 0; hh < 2; ++hh) {
                                 const int jr = tq * K + k + 1 - ch.off[hh];
                                 const uint32_t cb = (jr >= 1 && jr <= ch.nB[hh]) ? (uint32_t)ch.cseq[hh][jr - 1] : 0u;
-                                s2[hh] = jr < 1 ? 0 : (cb == rb ? AR_EQ_MATCH : AR_EQ_MISMATCH);
+                                s2[hh] = (jr < 1 ? 0 : (cb == rb ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
                             }
                             eq[k] = ar_pk_int(s2[0], s2[1]);
                         }
                     }
                 }
-                // Iy open of the row: the end-gap open on a unit's last row (both halves share it)
-                const uint32_t oy = COI + ((rec.y >> 30) & 1u) * OYD;
-                at_s2 d1 = as_s2(carry);
                 at_s2 F1 = as_s2(inF), Y = as_s2(inY);
                 uint32_t acc[K];
-                // Best-open fill (alignt2_kernel.hpp cells, RAW): M = B(i-1, j-1) + s,
-                // X = max(B_up + co_j, X_up), Y = max(B_left + oy, Y_left), B = maximum3(M, X, Y)
-                at_s2 Mk = padd32(d1, eq[0]);
+                // Best-open fill on open-shifted cells (alignt2_kernel.hpp cells, RAW): M = G(i-1, j-1) +
+                // (s - co_i), X = max(G_up, X_up), Y = max(G_left, Y_left), B = maximum3(M, X, Y), G = B + o_i
+                at_s2 Mk = padd32(as_s2(carry), eq[0]);
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const at_s2 Bu = as_s2(stG[k]), Xu = as_s2(stX[k]);
+                    const at_s2 Gu = as_s2(stG[k]), Xu = as_s2(stX[k]);
                     const at_s2 M = Mk;
-                    if (k + 1 < K) Mk = padd32(Bu, eq[k + 1]);
-                    const at_s2 Xn = pmax(padd32(Bu, k == K - 1 ? cend : COI), Xu);
-                    const at_s2 Yn = pmax(padd32(F1, oy), Y);
+                    if (k + 1 < K) Mk = padd32(Gu, eq[k + 1]);
+                    const at_s2 Xn = pmax(k == K - 1 ? padd32(Gu, cadj) : Gu, Xu);
+                    const at_s2 Yn = pmax(F1, Y);
                     uint32_t b3;
                     asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(b3) : "v"(as_u32(M)), "v"(as_u32(Xn)), "v"(as_u32(Yn)));
-                    const at_s2 Bn = as_s2(b3);
                     const uint32_t dD = as_u32(M) - as_u32(Xn);
                     const uint32_t dE = as_u32(M) - as_u32(Yn);
                     acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
-                    stG[k] = as_u32(Bn);
+                    const at_s2 Gn = padd32(as_s2(b3), orow);
+                    stG[k] = as_u32(Gn);
                     stX[k] = as_u32(Xn);
-                    F1 = Bn;
+                    F1 = Gn;
                     Y = Yn;
                 }
                 if (in_band) {
@@ -579,15 +598,15 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 payY = as_u32(Y);
                 if constexpr (HO)
                     if (ln == 63) ring[WI * RING + ((g + 1) & (RING - 1))] = make_uint2(payF, payY);
-                if ((rec.y & AR_LAST) && (tq == own0 || tq == own1)) {  // owner of a half's column nB_h
+                if (pre && (rec.y & AR_LAST) && (tq == own0 || tq == own1)) {  // owner of a half's column nB_h
                     int t = 0;
                     for (int q = 1; q < n; ++q)
                         if (tab[cur][q].r0 <= g) t = q;
-                    const uint32_t e = stG[K - 1];
+                    const uint32_t e = stG[K - 1] - orow;  // B = G - o_i
                     if (tq == own0) fin[cur][t][0] = (int)(e & 0xFFFFu) - BIAS16;
                     if (tq == own1) fin[cur][t][1] = (int)(e >> 16) - BIAS16;
                 }
-                carry = inF;  // B(i, j0 - 1): the next row's diagonal
+                carry = inF;  // G(i, j0 - 1): the next row's diagonal
             };
 
             const int nsteps = rows + 63;
