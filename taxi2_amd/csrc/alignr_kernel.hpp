@@ -41,6 +41,35 @@ constexpr int AR_BLK = 16;  // steps between progress checks / publications
 #define TAXI2_AR_UNITS 8
 #endif
 constexpr int AR_UNITS = TAXI2_AR_UNITS;  // units (row sequences, up to two pairs each) per chain
+// Trace layout.  AR_TS = 0 (default): [step][lane][4K bytes], a lane's K columns contiguous.
+// AR_TS >= 1: the columns are cut into pieces of ar_pw(K) columns (16 bytes for K % 4 == 0), and
+// piece q of all lanes over AR_TS consecutive steps is one run, [step / AR_TS][piece][lane][step %
+// AR_TS][piece bytes], so that the walker's diagonal hops (one step back per hop within a lane) share
+// a line for AR_TS hops.  Measured at config 3, band 64: AR_TS = 2 cuts the walker's
+// fetch from 110 to 74 KB per pair but the fill is 1 % slower; AR_TS = 1 is 11 % and AR_TS = 4
+// (42 KB per pair) 17 % slower -- the fill's stores, not the walker's reads, set the cost.
+#ifndef TAXI2_AR_TS
+#define TAXI2_AR_TS 0
+#endif
+constexpr int AR_TS = TAXI2_AR_TS;
+__host__ __device__ constexpr int ar_pw(int K) { return K % 4 == 0 ? 4 : 2; }
+// byte offset of (step, lane, column k) in a chain's trace buffer (NT lanes)
+// (AR_TS = 0: the plain [step][lane][4K bytes] layout, for comparison)
+template <int K, int NT>
+__device__ __forceinline__ uint32_t ar_trace_step_off(uint32_t step) {  // of (step, lane 0, column 0)
+    constexpr uint32_t PW = ar_pw(K), PB = 4 * PW, NP = K / PW;
+    if constexpr (AR_TS == 0) return step * (NT * 4 * K);
+    else return (step / AR_TS) * (NP * NT * AR_TS * PB) + (step % AR_TS) * PB;
+}
+template <int K> constexpr uint32_t ar_lane_bytes() { return AR_TS == 0 ? 4 * K : AR_TS * 4 * ar_pw(K); }
+template <int K, int NT> constexpr uint32_t ar_piece_stride() { return AR_TS == 0 ? 4 * ar_pw(K) : NT * AR_TS * 4 * ar_pw(K); }
+template <int K, int NT>
+__device__ __forceinline__ uint32_t ar_trace_off(uint32_t step, uint32_t lane, uint32_t k) {
+    constexpr uint32_t PW = ar_pw(K);
+    return ar_trace_step_off<K, NT>(step) + lane * ar_lane_bytes<K>() + (k / PW) * ar_piece_stride<K, NT>() + (k % PW) * 4;
+}
+// trace buffer rows for a chain of `rows` rows: steps up to rows + 62, rounded up to whole blocks
+__host__ __device__ constexpr int ar_trace_rows(int rows) { return rows + 64 + AR_TS; }
 
 // Profiling build only (-DAR_PROF, `make variant VNAME=arprof VFLAGS=-DAR_PROF`): per-wave s_memtime
 // totals of the launch -- fill: step loops, interval barrier waits, chain set-up (cut, tables, first
@@ -308,7 +337,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     const bool esc = in && band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
                     const int cj = max(nj, 1) - 1 + off, ci = max(ni, 1) - 1;  // virtual column of (ni, nj) - 1
                     const uint32_t tl = (uint32_t)cj / K, k = (uint32_t)cj - tl * K;
-                    const uint32_t toff = (((uint32_t)(r0 + ci) + (tl & 63u)) * (uint32_t)NT + tl) * (uint32_t)TB + 4u * k;
+                    const uint32_t toff = ar_trace_off<K, NT>((uint32_t)(r0 + ci) + (tl & 63u), tl, k);
                     const uint32_t xa_ = a2_load_byte(rs + ci), yb_ = a2_load_byte(cs + max(nj, 1) - 1);
                     const uint32_t nb = a2_load_trace32(trb + toff);
                     xa = ni >= 1 ? xa_ : 0u;
@@ -584,14 +613,17 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     Y = Yn;
                 }
                 if (in_band) {
-                    uint32_t* dst = (uint32_t*)(trb + (((uint32_t)s * NT + (uint32_t)tq) * (uint32_t)TB));
+                    constexpr uint32_t PSTRIDE = ar_piece_stride<K, NT>();  // bytes between pieces
+                    // uniform step offset (SGPR) + the lane's constant: one VALU add, saddr stores per piece
+                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane(ar_trace_step_off<K, NT>((uint32_t)s)) +
+                                        (uint32_t)tq * ar_lane_bytes<K>();
                     if constexpr (K % 4 == 0) {
 #pragma unroll
                         for (int q = 0; q < K / 4; ++q)
-                            ((uint4*)dst)[q] = make_uint4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                            *(uint4*)((trb + q * PSTRIDE) + o0) = make_uint4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
                     } else {
 #pragma unroll
-                        for (int q = 0; q < K / 2; ++q) ((uint2*)dst)[q] = make_uint2(acc[2 * q], acc[2 * q + 1]);
+                        for (int q = 0; q < K / 2; ++q) *(uint2*)((trb + q * PSTRIDE) + o0) = make_uint2(acc[2 * q], acc[2 * q + 1]);
                     }
                 }
                 payF = as_u32(F1);

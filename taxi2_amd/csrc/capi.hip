@@ -769,12 +769,15 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // up to 120 GB of the 288 GB HBM, at most 45 % of the device's memory (TAXI2_AT_TRACE_GB overrides)
     double budget_gb = std::min(120.0, 0.45 * (double)ctx->total_mem / 1e9);
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
-    auto buf_bytes = [&](int64_t e) { return at_buf_bytes((int)e * std::max(1, Y.max_len), 4 * v.K, v.W); };
+    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * std::max(1, Y.max_len)) - 64, 4 * v.K, v.W); };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
     chunk = (int)eff;
     const int cap_rows = (int)eff * std::max(1, Y.max_len);
     const size_t bb = buf_bytes(eff);
-    int band = std::max(32, (int)std::ceil(3.0 * std::sqrt((double)max_len)));
+    // trace band: 2.5 sqrt(L) (80 at 1 000 bp: the widest measured excursion is 67; escapes requeue
+    // exactly).  Narrower bands cut the trace writes (337 KB per pair at 80, 275 at 64) but the
+    // requeued pairs' full-trace pass costs more than the writes save
+    int band = std::max(32, (int)std::ceil(2.5 * std::sqrt((double)max_len)));
     if (4 * band >= max_len) band = 0;
     if (const char* e = getenv("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
     // the queued pass (k_alignt2_queued over the launch's PairSrc, sign-digit full trace)

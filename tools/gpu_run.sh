@@ -11,6 +11,7 @@
 #   headline         bench.py --secondary '' --steps 10 --warmup 2
 #   ab:LIBA,LIBB,R   R alternations of the headline with TAXI2_LIB=LIBA then LIBB (same box A/B)
 #   abenv:VAR,R      R alternations of the headline with VAR=1 set, then unset (same box A/B)
+#   hl:NAME:V=X,...  one headline run with those environment settings -> hl_NAME.json / .err
 #   trace            rocprofv3 --kernel-trace --stats of the headline bench
 #   pmc_valu | pmc_fetch | pmc_write | pmc_lds
 #                    one rocprofv3 --pmc pass each over one bench launch (separate runs: rocprofv3
@@ -49,8 +50,8 @@ run_step() {
     ab:*)
         IFS=, read -r la lb reps <<< "${s#ab:}"
         for r in $(seq 1 "${reps:-2}"); do
-            (cd "$R" && TAXI2_LIB=$la timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_a_$r.json" 2> "$OUT/ab_a_$r.err") || return $?
-            (cd "$R" && TAXI2_LIB=$lb timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_b_$r.json" 2> "$OUT/ab_b_$r.err") || return $?
+            (cd "$R" && TAXI2_LIB=$la timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_${la%.so}_$r.json" 2> "$OUT/ab_${la%.so}_$r.err") || return $?
+            (cd "$R" && TAXI2_LIB=$lb timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_${lb%.so}_$r.json" 2> "$OUT/ab_${lb%.so}_$r.err") || return $?
         done ;;
     abenv:*)
         IFS=, read -r var reps <<< "${s#abenv:}"
@@ -58,6 +59,11 @@ run_step() {
             (cd "$R" && env "$var=1" timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_env_$r.json" 2> "$OUT/ab_env_$r.err") || return $?
             (cd "$R" && timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/ab_def_$r.json" 2> "$OUT/ab_def_$r.err") || return $?
         done ;;
+    hl:*)
+        local rest=${s#hl:}
+        local name=${rest%%:*}
+        local envs=$(echo "${rest#*:}" | tr ',' ' ')
+        (cd "$R" && env $envs timeout -k 10 200 $BENCH --steps 8 --warmup 2 > "$OUT/hl_$name.json" 2> "$OUT/hl_$name.err") ;;
     trace)
         (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
             $BENCH --steps 10 --warmup 2 > "$OUT/trace_bench.json" 2> "$OUT/trace.err") ;;
