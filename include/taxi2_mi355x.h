@@ -246,6 +246,15 @@ int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, c
                                  int first, uint8_t* d_text, int64_t text_cap, int64_t* d_total,
                                  int64_t* d_scratch, void* stream);
 
+/* Compaction of walker string slots (taxi2_tri_strings_dev / taxi2_rect_strings_dev output):
+ * pair k's string of orientation `slot` -- the last d_slen[k * nslot + slot] bytes before byte
+ * d_end[k] of slot k * nslot + slot (cap bytes each) -- is copied to d_dx / d_dy + d_off[k], for
+ * both aligned strings.  Asynchronous on `stream`.  (The (b, a) strings kept for a later row
+ * block of aligned_pairs.txt, versus_all.py:746-750.) */
+int taxi2_pack_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
+                         int nslot, int slot, const int64_t* d_end, const int64_t* d_off, int64_t count, uint8_t* d_dx,
+                         uint8_t* d_dy, void* stream);
+
 /* ---- compressed length (alfpy ncd.complexity) --------------------------------------------- *
  * out[k] = len(zlib.compress(upper(x[xs[k]]) + upper(y[ys[k]]))), zlib 1.2.11 level 6;
  * ys == NULL compresses x[xs[k]] alone.  Any length. */

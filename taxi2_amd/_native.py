@@ -44,6 +44,7 @@ EXPORTS = (
     "taxi2_tri_strings_dev",
     "taxi2_format_pairs_ptr_dev",
     "taxi2_format_pairs_ptr_async",
+    "taxi2_pack_slots_dev",
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
@@ -116,6 +117,7 @@ _SIGNATURES = {
                                             _P]),
     "taxi2_format_pairs_ptr_dev": (_INT, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
                                           ctypes.POINTER(_I64), _P]),
+    "taxi2_pack_slots_dev": (_INT, [_P, _P, _P, _P, _I64, _INT, _INT, _P, _P, _I64, _P, _P, _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
@@ -504,6 +506,19 @@ class Engine:
                     ctypes.c_void_p(text_ptr), int(cap), ctypes.c_void_p(total_ptr), ctypes.c_void_p(scratch_ptr),
                     ctypes.c_void_p(stream)),
                 "taxi2_format_pairs_ptr_async",
+            )
+
+    def pack_slots_dev(self, sx_ptr: int, sy_ptr: int, slen_ptr: int, cap: int, nslot: int, slot: int, end_ptr: int,
+                       off_ptr: int, count: int, dx_ptr: int, dy_ptr: int, stream: int) -> None:
+        """Copy orientation ``slot`` of each pair's walker strings (the last slen bytes before end[k]
+        of its slot) to dx / dy + off[k], on ``stream`` (taxi2_pack_slots_dev)."""
+        with self._lock:
+            self._check(
+                self._lib.taxi2_pack_slots_dev(
+                    self._ctx, ctypes.c_void_p(sx_ptr), ctypes.c_void_p(sy_ptr), ctypes.c_void_p(slen_ptr), int(cap),
+                    int(nslot), int(slot), ctypes.c_void_p(end_ptr), ctypes.c_void_p(off_ptr), int(count),
+                    ctypes.c_void_p(dx_ptr), ctypes.c_void_p(dy_ptr), ctypes.c_void_p(stream)),
+                "taxi2_pack_slots_dev",
             )
 
     def format_pairs_ptr_dev(self, nrows: int, ncols: int, px_ptr: int, py_ptr: int, slen_ptr: int, row_ids, col_ids,

@@ -32,11 +32,7 @@
 
 namespace taxi2 {
 
-// 1: the fill waves pace each other with LDS progress counters instead of a barrier every 64 steps
-#ifndef AR_DECOUPLE
-#define AR_DECOUPLE 1
-#endif
-constexpr int AR_BLK = 16;  // steps between progress checks / publications
+constexpr int AR_BLK = 16;  // steps between the fill waves' progress checks / publications
 #ifndef TAXI2_AR_UNITS
 #define TAXI2_AR_UNITS 8
 #endif
@@ -72,8 +68,9 @@ __device__ __forceinline__ uint32_t ar_trace_off(uint32_t step, uint32_t lane, u
 __host__ __device__ constexpr int ar_trace_rows(int rows) { return rows + 64 + AR_TS; }
 
 // Profiling build only (-DAR_PROF, `make variant VNAME=arprof VFLAGS=-DAR_PROF`): per-wave s_memtime
-// totals of the launch -- fill: step loops, interval barrier waits, chain set-up (cut, tables, first
-// barrier); walker: hops during intervals, the chain-end drain, interval barrier waits; chains; hops
+// totals of the launch -- [0] fill step loops, [1] fill chain-end barrier, [2] chain set-up (cut,
+// tables, first barrier), [3] walker walking, [4] fill waits for the other fill wave, [5] walker
+// chain-end barrier, [6] chains
 #ifdef AR_PROF
 __device__ unsigned long long ar_prof[8];
 #define AR_NOW() __builtin_amdgcn_s_memtime()
@@ -125,6 +122,9 @@ constexpr uint32_t AR_NOBAND = 0x0080u;  // lo 128, width 0: no lane stores
 constexpr int AR_EQ_MATCH = 3, AR_EQ_MISMATCH = 1, AR_CO_I = -7, AR_CO_E = 0;
 
 __device__ __forceinline__ uint32_t ar_pk_int(int lo, int hi) { return pk_int(pk2(lo, hi)); }
+
+// 8 bytes at any byte address (one unaligned global store)
+__device__ __forceinline__ void ar_store8(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
 
 // band lanes [lo, hi] of row i (1-based) of a pair with nA rows and nB columns, shifted by off;
 // lo > hi: none (a2_band_blocks in virtual columns)
@@ -201,13 +201,9 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     __shared__ uint32_t eqt[4][NT][K];  // (s(x0_k, base), s(x1_k, base)) - co_i as pk_int, per lane and slot
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows, s_seg;
-    __shared__ int s_fill;
-    __shared__ int s_prog[2];  // AR_DECOUPLE: steps completed by each fill wave in the current chain
+    __shared__ int s_prog[2];  // steps completed by each fill wave in the current chain
     __shared__ ArWalk wks[NW];
     __shared__ int escf[2][AR_UNITS][2];
-#ifdef AR_PROF
-    __shared__ unsigned long long s_arr[W + 1];  // interval barrier arrival time of each wave
-#endif
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -275,8 +271,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     };
 
     // branch-free best-open walker (alignt2_kernel.hpp walk_run_raw), per-half column sequence and
-    // shift; hops until the fill waves signal `target` interval completions (target 0: to the end)
-    auto walk = [&](int pb, int target) {
+    // shift; walks the chain in buffer pb to the end.  Aligned strings (so.sx): each walk keeps the
+    // last 8 columns it produced in a 64-bit window per string and stores the window (8 bytes,
+    // unaligned) every 8 columns and at the walk's end -- not a byte store per column and string
+    auto walk = [&](int pb) {
         ArWalk& W_ = wks[lane < NW ? lane : 0];
         int st = lane < NW ? W_.st : AT_DONE;
         if (!__any(st != AT_DONE)) return;
@@ -294,12 +292,13 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
         int i = W_.i, j = W_.j, first = W_.first;
         uint32_t xa = W_.xa, yb = W_.yb;
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap, sc2 = W_.sc2, ncol = W_.ncol;
+        uint64_t wx = 0, wy = 0;  // string windows: bits 0-7 = the last column produced
         const int co_i = sc.io - sc.ie, co_e = sc.eo - sc.ee;
         const int bsh = h ? 8 : 0;
         const int oslot = prio ^ 1;  // swp = 1: rows are the pair's second sequence
+        const size_t sbase = so.sx ? ((size_t)p * so.nslot + (oslot & (so.nslot - 1))) * (size_t)so.cap : 0;
         for (;;) {
             if (!__any(st < AT_DONE)) break;
-            if (target > 0 && __hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
             if (st < AT_DONE) {
                 const bool isM = st == AT_M, isX = st == AT_IX, isY = st == AT_IY;
                 const uint32_t bx = a2_wcode(xa), by = a2_wcode(yb);
@@ -313,11 +312,14 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 const int ni = isY ? i : i - 1, nj = isX ? j : j - 1;
                 if (so.sx && !first) {  // this column of the alignment, right to left, (x, y) order
                     const uint32_t rc = isY ? (uint32_t)'-' : xa, cc = isX ? (uint32_t)'-' : yb;
-                    const size_t o = ((size_t)p * so.nslot + (oslot & (so.nslot - 1))) * (size_t)so.cap +
-                                     (size_t)(nA_ + nB_ - 1 - ncol);
-                    so.sx[o] = (uint8_t)cc;
-                    so.sy[o] = (uint8_t)rc;
+                    wx = (wx << 8) | cc;
+                    wy = (wy << 8) | rc;
                     ++ncol;
+                    if ((ncol & 7) == 0) {  // columns [E - ncol, E - ncol + 8) of the slot (E = nA + nB)
+                        const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
+                        ar_store8(so.sx + o, wx);
+                        ar_store8(so.sy + o, wy);
+                    }
                 }
                 first = 0;
                 if (ni == 0 && nj == 0) {
@@ -330,6 +332,18 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                             o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
                         if (sout && (out_mode != OUT_BOTH || oslot == 0)) sout[p] = fin[pb][t][h] + (nA_ + nB_) * dz;
                         if (so.slen) so.slen[p * so.nslot + (oslot & (so.nslot - 1))] = ncol;
+                        if (so.sx && (ncol & 7)) {  // the columns since the last window store
+                            const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
+                            if (ncol >= 8) {  // the window's older bytes are already in place
+                                ar_store8(so.sx + o, wx);
+                                ar_store8(so.sy + o, wy);
+                            } else {
+                                for (int q = 0; q < ncol; ++q) {
+                                    so.sx[o + q] = (uint8_t)(wx >> (8 * q));
+                                    so.sy[o + q] = (uint8_t)(wy >> (8 * q));
+                                }
+                            }
+                        }
                         st = AT_DONE;
                     }
                 } else {
@@ -460,7 +474,6 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 chs[cur].n = n;
                 s_n = n;
                 s_rows = rows;
-                s_fill = 0;
                 s_prog[0] = s_prog[1] = 0;
             }
             __syncthreads();
@@ -469,7 +482,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             const int pb = cur ^ 1;
             if constexpr (IS_W) walk_init(pb, prev_n);
             if (n == 0) {
-                if constexpr (IS_W) walk(pb, 0);
+                if constexpr (IS_W) walk(pb);
                 break;
             }
             const ArChain& ch = chs[cur];
@@ -642,11 +655,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             };
 
             const int nsteps = rows + 63;
-#if AR_DECOUPLE
             // No interval barriers: the fill waves pace each other through two LDS progress counters
             // (steps completed, published every AR_BLK steps), so a wave whose steps store no trace
             // runs ahead instead of waiting at a barrier for the in-band wave (the band covers wave 0
-            // early in a unit and wave 1 late: ~60 % of the old intervals were unbalanced).  Wave 1 at
+            // early in a unit and wave 1 late: ~60 % of barrier intervals were unbalanced).  Wave 1 at
             // step s reads ring slot s + 1, written by wave 0 at step s + 63; wave 0 at step s
             // rewrites the slot wave 1 read at step s - 255 - 63.  The row records of the next 64 rows
             // are written by wave 0 itself before it needs them, and wave 1 (>= 79 steps behind,
@@ -656,7 +668,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 #ifdef AR_PROF
                 const unsigned long long t1 = AR_NOW();
 #endif
-                walk(pb, 0);
+                walk(pb);
 #ifdef AR_PROF
                 pf[3] += AR_NOW() - t1;
 #endif
@@ -664,13 +676,17 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 const int mine = w, other = w ^ 1;
                 for (int s0 = 0; s0 < nsteps; s0 += AR_BLK) {
                     const int s1 = min(s0 + AR_BLK, nsteps);
-                    if (W > 1) {  // wait for the other fill wave (rare: the ring holds 256 rows)
+#ifdef AR_PROF
+                    const unsigned long long t0 = AR_NOW();
+#endif
+                    if (W > 1) {  // wait for the other fill wave
                         const int need = w == 0 ? s1 - (RING - 63) : s1 + 63;
                         while (__hip_atomic_load(&s_prog[other], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
                             __builtin_amdgcn_s_sleep(1);
                     }
 #ifdef AR_PROF
                     const unsigned long long t1 = AR_NOW();
+                    pf[4] += t1 - t0;
 #endif
                     if (w == 0) {
                         for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 0>{}, s);
@@ -699,59 +715,6 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             pf[IS_W ? 5 : 1] += AR_NOW() - t2;
             tA = AR_NOW();
 #endif
-#else
-            const int nblk = (nsteps + INTERVAL - 1) / INTERVAL;
-            const int nint = nblk + WAVE_LAG * (W - 1);
-            for (int it = 0; it < nint; ++it) {
-#ifdef AR_PROF
-                const unsigned long long t1 = AR_NOW();
-#endif
-                if constexpr (IS_W) {
-                    walk(pb, W * (it + 1));
-                } else {
-                    const int blk = it - WAVE_LAG * w;
-                    if (blk >= 0 && blk < nblk) {
-                        const int s0 = blk * INTERVAL;
-                        const int s1 = min(s0 + INTERVAL, nsteps);
-                        if (w == 0) {
-                            for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 0>{}, s);
-                        } else if constexpr (W > 1) {
-                            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) once, outside the step loop
-                            for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 1>{}, s);
-                        }
-                    }
-                }
-#ifdef AR_PROF
-                const unsigned long long t2 = AR_NOW();
-                pf[IS_W ? 3 : 0] += t2 - t1;
-#endif
-                const int gpre = (it + 1) * INTERVAL + tid;
-                if (tid < INTERVAL && it + 1 < nblk) xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
-                if (it + 1 == nint) __builtin_amdgcn_s_waitcnt(0);
-                if (!IS_W && lane == 0) atomicAdd(&s_fill, 1);
-#ifdef AR_PROF
-                if (lane == 0) s_arr[w] = AR_NOW();
-#endif
-                __syncthreads();
-#ifdef AR_PROF
-                pf[IS_W ? 5 : 1] += AR_NOW() - t2;
-                if (w == 0 && lane == 0) {  // the walker's lateness behind the last fill wave
-                    unsigned long long lf = 0;
-                    for (int q = 0; q < W; ++q) lf = max(lf, s_arr[q]);
-                    pf[7] += s_arr[W] > lf ? s_arr[W] - lf : 0ull;
-                }
-                __syncthreads();  // s_arr is rewritten at the next interval
-#endif
-            }
-#ifdef AR_PROF
-            const unsigned long long t3 = AR_NOW();
-#endif
-            if constexpr (IS_W) walk(pb, 0);
-#ifdef AR_PROF
-            pf[4] += AR_NOW() - t3;
-            tA = AR_NOW();
-#endif
-#endif
             prev_n = n;
             cur ^= 1;
         }
@@ -760,9 +723,6 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             for (int q = 0; q < 8; ++q) atomicAdd(&ar_prof[q], pf[q]);
 #endif
     };
-#ifdef AR_WALK_PRIO
-    if (walker) __builtin_amdgcn_s_setprio(AR_WALK_PRIO);  // experiment: walker issue priority
-#endif
     if (walker) chain_loop(std::true_type{});
     else chain_loop(std::false_type{});
 }

@@ -825,9 +825,9 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
         HIP_TRY(ctx, hipStreamSynchronize(st));
         HIP_TRY(ctx, hipMemcpyFromSymbol(pf, HIP_SYMBOL(ar_prof), sizeof pf));
         HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(ar_prof), z, sizeof z));
-        fprintf(stderr, "taxi2 arprof: k_alignr<%d,%d> grid %lld units %lld chains %llu | fill steps %llu barrier %llu setup %llu"
-                " | walker hops %llu drain %llu barrier %llu | walker late %llu\n", v.K, v.W, (long long)grid, (long long)units,
-                pf[6], pf[0], pf[1], pf[2], pf[3], pf[4], pf[5], pf[7]);
+        fprintf(stderr, "taxi2 arprof: k_alignr<%d,%d> grid %lld units %lld chains %llu | fill steps %llu waits %llu barrier %llu"
+                " setup %llu | walker walking %llu barrier %llu\n", v.K, v.W, (long long)grid, (long long)units,
+                pf[6], pf[0], pf[4], pf[1], pf[2], pf[3], pf[5]);
     }
 #endif
     if (shared_release(ctx, st)) return -1;
@@ -2100,6 +2100,22 @@ int taxi2_format_pairs_ptr_dev(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, con
     PairFmtArgs a{nullptr, nullptr, d_slen, 0, nullptr, nullptr, ncols, nullptr, nullptr, nullptr, nullptr,
                   first ? 1 : 0, d_px, d_py};
     return format_pairs_impl(ctx, nrows, ncols, a, row_ids, row_offs, col_ids, col_offs, out, out_cap, out_len, st);
+}
+
+int taxi2_pack_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
+                         int nslot, int slot, const int64_t* d_end, const int64_t* d_off, int64_t count, uint8_t* d_dx,
+                         uint8_t* d_dy, void* stream) {
+    if (!ctx) return -1;
+    if (count < 0 || cap <= 0 || nslot < 1 || slot < 0 || slot >= nslot) return fail(ctx, "bad slot arguments");
+    if (count == 0) return 0;
+    if (!d_sx || !d_sy || !d_slen || !d_end || !d_off || !d_dx || !d_dy) return fail(ctx, "null device argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    const int64_t blocks = std::min<int64_t>((count + 3) / 4, (int64_t)ctx->num_cus * 32);
+    hipLaunchKernelGGL(k_pack_slots, dim3((unsigned)blocks), dim3(256), 0, st, d_sx, d_sy, d_slen, cap, nslot, slot, d_end,
+                       d_off, count, d_dx, d_dy);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
 }
 
 int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, const uint64_t* d_px,

@@ -384,6 +384,24 @@ k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restri
         __syncthreads();
     }
 }
+// Compaction of one orientation's aligned strings out of the walkers' slots (StrOut): pair k's
+// string is the last slen[k * nslot + slot] bytes before byte end[k] of its slot, copied to
+// dst + off[k].  One wave per pair, lanes striding over the bytes (coalesced loads and stores).
+__global__ void __launch_bounds__(256) k_pack_slots(const uint8_t* __restrict__ sx, const uint8_t* __restrict__ sy,
+                                                    const int32_t* __restrict__ slen, int64_t cap, int nslot, int slot,
+                                                    const int64_t* __restrict__ end, const int64_t* __restrict__ off,
+                                                    int64_t count, uint8_t* __restrict__ dx, uint8_t* __restrict__ dy) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < count; k += (int64_t)gridDim.x * 4) {
+        const int64_t L = slen[k * nslot + slot];
+        const int64_t src = (k * nslot + slot) * cap + end[k] - L, dst = off[k];
+        for (int64_t b = lane; b < L; b += 64) {
+            dx[dst + b] = sx[src + b];
+            dy[dst + b] = sy[src + b];
+        }
+    }
+}
+
 #endif
 
 }  // namespace taxi2

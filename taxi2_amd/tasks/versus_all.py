@@ -69,6 +69,7 @@ def walk_strings_ok(scores: tuple, seqs: list) -> bool:
 
 WALK_LAUNCH_PAIRS = 1 << 19  # ordered pairs per string-emitting aligner launch (the bench's batch)
 WALK_BLOCK_BYTES = 8 << 30   # HBM for one block's string slots + metrics
+DEVICE_D_BYTES = 16 << 30    # the walked path's device copy of the counter metrics, at most
 
 
 def walk_block_rows(n: int, per_pair: int, block_bytes: int, launch_pairs: int = WALK_LAUNCH_PAIRS) -> int:
@@ -318,6 +319,17 @@ class VersusAll:
         per_pair = 4 * cap + 16 * Mc + 8
         target = max(1, min(launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
         stream = torch.cuda.Stream(dev)
+        # the counter metrics land in a device copy of D (scattered on the GPU, one D2H at the end)
+        # unless that copy would be large
+        Dd = None
+        if n * n * Mc * 8 <= DEVICE_D_BYTES:
+            Dd = torch.full((n, n, Mc), float("nan"), dtype=torch.float64, device=dev)
+
+        def flush_d() -> None:
+            if Dd is not None:
+                stream.synchronize()
+                D[:, :, cidx] = Dd.cpu().numpy()
+
         with torch.cuda.stream(stream):
             lens = torch.as_tensor(lens_h, device=dev)
             # self alignments (x, x) for the diagonal pairs' text
@@ -337,7 +349,6 @@ class VersusAll:
             kpy = torch.zeros(npairs, dtype=torch.int64, device=dev)
             klen = torch.zeros(npairs, dtype=torch.int32, device=dev)
             kept = []
-            ar = torch.arange(cap, device=dev)
             x0 = 0
             while x0 < n:
                 # rows [x0, x1): about `target` triangle pairs, at most 2 * target ordered pairs of text
@@ -364,23 +375,30 @@ class VersusAll:
                     first = torch.cumsum(n - 1 - torch.arange(x0, x1, device=dev), 0) - (n - 1 - torch.arange(x0, x1, device=dev))
                     rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(first, n - 1 - torch.arange(x0, x1, device=dev))
                     end = (lens[ra] + lens[rb]).to(torch.int64)
-                    # keep the (b, a) orientation compacted (mask of each slot's right-aligned bytes)
+                    # keep the (b, a) orientation compacted (taxi2_pack_slots_dev: each slot's
+                    # right-aligned bytes to a running offset)
                     L1 = sl[:, 1].to(torch.int64)
-                    m1 = (ar[None, :] >= (end - L1)[:, None]) & (ar[None, :] < end[:, None])
-                    kx, ky = sx[:, 1, :][m1], sy[:, 1, :][m1]
                     off = torch.cumsum(L1, 0) - L1
+                    tot = int(L1.sum().item())
+                    kx = torch.empty(max(1, tot), dtype=torch.uint8, device=dev)
+                    ky = torch.empty(max(1, tot), dtype=torch.uint8, device=dev)
+                    eng.pack_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 1, end.data_ptr(),
+                                       off.data_ptr(), cnt, kx.data_ptr(), ky.data_ptr(), stream.cuda_stream)
                     kpx[k0:k0 + cnt] = kx.data_ptr() + off
                     kpy[k0:k0 + cnt] = ky.data_ptr() + off
                     klen[k0:k0 + cnt] = sl[:, 1]
                     kept.append((kx, ky))
-                    kept_bytes += 2 * kx.numel()
-                    del m1
+                    kept_bytes += 2 * tot
                     blk = (sx, sy, sl, end, d, ra, rb)
-                    dd = d.cpu().numpy()
-                    a_h, b_h = ra.cpu().numpy(), rb.cpu().numpy()
-                    for q, kk in enumerate(cidx):
-                        D[a_h, b_h, kk] = dd[:, 0, q]
-                        D[b_h, a_h, kk] = dd[:, 1, q]
+                    if Dd is not None:
+                        Dd[ra, rb] = d[:, 0, :]
+                        Dd[rb, ra] = d[:, 1, :]
+                    else:
+                        dd = d.cpu().numpy()
+                        a_h, b_h = ra.cpu().numpy(), rb.cpu().numpy()
+                        for q, kk in enumerate(cidx):
+                            D[a_h, b_h, kk] = dd[:, 0, q]
+                            D[b_h, a_h, kk] = dd[:, 1, q]
                 # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
                 # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
                 # and (x, x) from the self alignments
@@ -416,10 +434,10 @@ class VersusAll:
                 if x0 < n and kept_bytes > keep_limit:
                     # the kept strings outgrew their budget: the remaining rows align every ordered
                     # pair once (row blocks of the rect path), nothing kept
-                    stream.synchronize()
-                    del kept, kpx, kpy, klen
+                    flush_d()
+                    del kept, kpx, kpy, klen, Dd
                     return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
-            stream.synchronize()
+            flush_d()
             del kept
         return True
 
