@@ -76,6 +76,7 @@ k_prealigned(SetView XS, SetView YS, PairSrc ps, MetricSpec ms, double* __restri
 constexpr int PT = 64;        // sequences per tile side
 constexpr int PWC = 16;       // plane words staged per chunk
 constexpr int PWS = PWC + 1;  // padded LDS row (uint4): 16 lanes reading 16 rows hit 64 distinct banks
+constexpr int TILE_STAGE_NM = 4;  // metrics per pair the epilogue's LDS stage holds (16 x PT x 4 f64 = 32 KB)
 
 // Row-block epilogue of the streamed versusAll (config 5; taxi2_rect_block_dev): every value x scale
 // (the task's x100, the same f64 multiply as D * 100), the diagonal rule's NaN on x == y (one set on
@@ -102,7 +103,9 @@ template <int MODE>
 __global__ void __launch_bounds__(256)
 k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, int64_t y0, int64_t ny,
                   int64_t tiles_y, int nwords, MetricSpec ms, double* __restrict__ out, TileBlock tb) {
-    __shared__ uint4 sx[PT * PWS], sy[PT * PWS];
+    __shared__ uint4 sxy[2 * PT * PWS];  // both sides' plane stages; the epilogue's output / row-min stage
+    uint4* const sx = sxy;
+    uint4* const sy = sxy + PT * PWS;
     const int tid = (int)threadIdx.x;
     const int tx = tid & 15, ty = tid >> 4;
     const int64_t bx = (int64_t)blockIdx.x / tiles_y, by = (int64_t)blockIdx.x - bx * tiles_y;
@@ -160,40 +163,62 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
     const int nm = ms.n;
     double rv[4];
     int64_t ry[4];
+    // Output through LDS, 16 rows at a time: a thread's pairs are spread over 16 rows, so direct
+    // stores would write 16 short strided pieces per instruction; staged, the workgroup writes
+    // each row's run of slots (nm values per pair, up to 64 pairs) as one contiguous stretch.
+    double* stg = (double*)sxy;  // [16 rows][PT cols][nm] (24 KB at nm = 3; the stages hold 34 KB)
+    const bool staged = nm <= TILE_STAGE_NM;
+    if (staged) __syncthreads();  // the plane stages are free
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         rv[i] = __builtin_inf();
         ry[i] = -1;
         const int64_t x = xa + tx + 16 * i;
-        if (x >= xe) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int64_t y = ya + ty + 16 * j;
-            if (y >= ye) continue;
-            int64_t slot;
+            bool ok = x < xe && y < ye;
+            int64_t slot = 0;
             if (MODE == PAIRS_TRI) {
-                if (y <= x) continue;
+                ok = ok && y > x;
                 slot = x * (2 * ps.N - x - 1) / 2 + (y - x - 1) - ps.k0;
-                if (slot < 0 || slot >= ps.count) continue;
             } else {
-                slot = x * ps.R + y - ps.k0;
-                if (slot < 0 || slot >= ps.count) continue;  // a launch may start / end inside a row
+                slot = x * ps.R + y - ps.k0;  // a launch may start / end inside a row
             }
+            ok = ok && slot >= 0 && slot < ps.count;
             const bool none = tb.diag && x == y;
             for (int m = 0; m < nm; ++m) {
                 const double v = none ? __builtin_nan("")
                                       : metric_value(ms.code[m], c[i][j][0], c[i][j][1], c[i][j][2], c[i][j][3]) * tb.scale;
-                out[slot * nm + m] = v;
+                if (staged) stg[(tx * PT + ty + 16 * j) * nm + m] = v;
+                else if (ok) out[slot * nm + m] = v;
                 // j ascending is y ascending: the first of equal values stays
-                if (m == tb.rmin_k && __builtin_isfinite(v) && v < rv[i]) {
+                if (ok && m == tb.rmin_k && __builtin_isfinite(v) && v < rv[i]) {
                     rv[i] = v;
                     ry[i] = y;
                 }
             }
         }
+        if (staged) {
+            __syncthreads();
+            // rows xa + r + 16 i (r = 0..15): the row's pairs y in [ya, ye) (TRI: y > x) are consecutive
+            // slots; element e of the row's run is pair y = y_lo + e / nm, metric e % nm
+            for (int r = tid >> 4; r < 16; r += 16) {
+                const int64_t x = xa + r + 16 * i;
+                if (x >= xe) continue;
+                const int64_t ylo = MODE == PAIRS_TRI ? max(ya, x + 1) : ya;
+                if (ylo >= ye) continue;
+                const int64_t s0 = MODE == PAIRS_TRI ? x * (2 * ps.N - x - 1) / 2 + (ylo - x - 1) - ps.k0
+                                                     : x * ps.R + ylo - ps.k0;
+                const int64_t lo = max((int64_t)0, -s0), hi = min(ye - ylo, ps.count - s0);  // pairs in the launch
+                for (int64_t e = lo * nm + (tid & 15); e < hi * nm; e += 16)
+                    out[s0 * nm + e] = stg[(r * PT + (ylo - ya)) * nm + e];
+            }
+            __syncthreads();  // the stage is rewritten by the next i
+        }
     }
     if (tb.rmin_v) {  // per (row, tile): the 16 threads of a row (ty = 0..15) through LDS, in y order
-        __syncthreads();  // the plane stages are free
+        __syncthreads();  // the plane / output stages are free
         RowMin* red = (RowMin*)sx;  // [ty][64 rows]
 #pragma unroll
         for (int i = 0; i < 4; ++i) red[ty * PT + tx + 16 * i] = RowMin{rv[i], ry[i]};

@@ -175,8 +175,77 @@ __global__ void __launch_bounds__(1024) k_subset_cofs(const int64_t* __restrict_
     if (t == 1023) cofs[ns] = part[1023];
 }
 
+// Running partial of one (row, subset, metric) inside a wave's lanes.
+struct SubAcc {
+    double rs[SUB_J], mn, mx;
+    long long c, mnp;
+    uint32_t fl;
+    int sc;
+    bool grid;
+    __device__ __forceinline__ void init(double key_sum) {
+        int e = 0;
+        grid = sub_grid(key_sum, e);
+        sc = 53 - e;
+#pragma unroll
+        for (int q = 0; q < SUB_J; ++q) rs[q] = 0.0;
+        mn = __builtin_inf();
+        mx = 0.0;
+        c = 0;
+        mnp = 0x7FFFFFFFFFFFFFFFll;
+        fl = grid ? 0u : SP_NOGRID;
+    }
+    __device__ __forceinline__ void add(double v, int64_t j) {
+        if (!isfinite(v)) return;
+        ++c;
+        if (v < mn) {
+            mn = v;
+            mnp = j;
+        }
+        if (v > mx) mx = v;
+        if (grid) {
+            if (v < 0.0) fl |= SP_NEG;
+#pragma unroll
+            for (int q = 0; q < SUB_J; ++q) {
+                const double r = ldexp(v, sc - q);
+                const double R = rint(r);
+                if (fabs(r - R) == 0.5) fl |= (uint32_t)SP_TIE << q;
+                rs[q] += R;
+            }
+        }
+    }
+    // the wave's lanes merged; lane 0 holds the partial
+    __device__ __forceinline__ SubPart reduce() {
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int q = 0; q < SUB_J; ++q) rs[q] += __shfl_xor(rs[q], o);
+            c += __shfl_xor(c, o);
+            fl |= (uint32_t)__shfl_xor((int)fl, o);
+            const double omx = __shfl_xor(mx, o);
+            if (omx > mx) mx = omx;
+            const double omn = __shfl_xor(mn, o);
+            const long long omp = __shfl_xor(mnp, o);
+            if (omn < mn || (omn == mn && omp < mnp)) {  // the first position among equal minima
+                mn = omn;
+                mnp = omp;
+            }
+        }
+        SubPart P;
+#pragma unroll
+        for (int q = 0; q < SUB_J; ++q) P.rsum[q] = rs[q];
+        P.mn = mn;
+        P.mx = mx;
+        P.cnt = c;
+        P.flags = fl;
+        P.pad = 0;
+        return P;
+    }
+};
+
 // One wave per (block row x, chunk t of the row's chunks; tmax >= cofs[ns] bounds the grid), every
-// metric.  Chunk t belongs to subset b with cofs[b] <= t < cofs[b + 1].
+// metric: up to SUB_MG metrics per pass over the chunk, each column's values read together (one
+// gather of m consecutive values per column instead of one per metric).  Chunk t belongs to subset
+// b with cofs[b] <= t < cofs[b + 1].
+constexpr int SUB_MG = 4;
 __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ vals, int64_t nrows, int64_t ncols,
                                                      int m, const int32_t* __restrict__ row_code,
                                                      const int64_t* __restrict__ col_start,
@@ -200,57 +269,23 @@ __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ 
     const int64_t j0 = col_start[b] + (int64_t)(t - cofs[b]) * SUB_CH;
     const int64_t j1 = min(col_start[b + 1], j0 + SUB_CH);
     const double* row = vals + x * ncols * m;
-    for (int k = 0; k < m; ++k) {
-        int e;
-        const bool grid = sub_grid(sum[((int64_t)a * ns + b) * m + k], e);
-        const int sc = 53 - e;
-        double rs[SUB_J], mn = __builtin_inf(), mx = 0.0;
-        for (int q = 0; q < SUB_J; ++q) rs[q] = 0.0;
-        long long c = 0, mnp = 0x7FFFFFFFFFFFFFFFll;
-        uint32_t fl = grid ? 0u : SP_NOGRID;
+    for (int k0 = 0; k0 < m; k0 += SUB_MG) {
+        const int g = min(SUB_MG, m - k0);
+        SubAcc acc[SUB_MG];
+#pragma unroll
+        for (int q = 0; q < SUB_MG; ++q)
+            if (q < g) acc[q].init(sum[((int64_t)a * ns + b) * m + k0 + q]);
         for (int64_t j = j0 + lane; j < j1; j += 64) {
-            const double v = row[(int64_t)col_idx[j] * m + k];
-            if (!isfinite(v)) continue;
-            ++c;
-            if (v < mn) {
-                mn = v;
-                mnp = j;
-            }
-            if (v > mx) mx = v;
-            if (grid) {
-                if (v < 0.0) fl |= SP_NEG;
+            const double* vp = row + (int64_t)col_idx[j] * m + k0;
 #pragma unroll
-                for (int q = 0; q < SUB_J; ++q) {
-                    const double r = ldexp(v, sc - q);
-                    const double R = rint(r);
-                    if (fabs(r - R) == 0.5) fl |= (uint32_t)SP_TIE << q;
-                    rs[q] += R;
-                }
-            }
+            for (int q = 0; q < SUB_MG; ++q)
+                if (q < g) acc[q].add(vp[q], j);
         }
-        for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-            for (int q = 0; q < SUB_J; ++q) rs[q] += __shfl_xor(rs[q], o);
-            c += __shfl_xor(c, o);
-            fl |= (uint32_t)__shfl_xor((int)fl, o);
-            const double omx = __shfl_xor(mx, o);
-            if (omx > mx) mx = omx;
-            const double omn = __shfl_xor(mn, o);
-            const long long omp = __shfl_xor(mnp, o);
-            if (omn < mn || (omn == mn && omp < mnp)) {  // the first position among equal minima
-                mn = omn;
-                mnp = omp;
-            }
-        }
-        if (lane == 0) {
-            SubPart P;
-            for (int q = 0; q < SUB_J; ++q) P.rsum[q] = rs[q];
-            P.mn = mn;
-            P.mx = mx;
-            P.cnt = c;
-            P.flags = fl;
-            P.pad = 0;
-            part[(x * tmax + t) * m + k] = P;
+        for (int q = 0; q < SUB_MG; ++q) {
+            if (q >= g) break;
+            const SubPart P = acc[q].reduce();
+            if (lane == 0) part[(x * tmax + t) * m + k0 + q] = P;
         }
     }
 }
@@ -280,6 +315,7 @@ __global__ void __launch_bounds__(256) k_subset_rows_nat(const double* __restric
                                                          int64_t ncols, int m, const int32_t* __restrict__ row_code,
                                                          const uint8_t* __restrict__ col_code, int ns, int nch,
                                                          const double* __restrict__ sum, SubPart* __restrict__ part) {
+    constexpr int MG = NSB <= 2 ? 2 : 1;  // metrics per pass (NSB x MG accumulators in registers)
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w >= nrows * nch) return;
@@ -289,75 +325,34 @@ __global__ void __launch_bounds__(256) k_subset_rows_nat(const double* __restric
     const int64_t j0 = (int64_t)c * SUB_CH, j1 = min(ncols, j0 + SUB_CH);
     const double* row = vals + x * ncols * m;
     const int tmax = ns * nch;
-    for (int k = 0; k < m; ++k) {
-        int sc[NSB];
-        bool grid[NSB];
-        double rs[NSB][SUB_J], mn[NSB], mx[NSB];
-        long long cnt[NSB], mnp[NSB];
-        uint32_t fl[NSB];
+    for (int k0 = 0; k0 < m; k0 += MG) {
+        const int g = min(MG, m - k0);
+        SubAcc acc[NSB][MG];
 #pragma unroll
-        for (int b = 0; b < NSB; ++b) {
-            int e = 0;
-            grid[b] = b < ns && sub_grid(sum[((int64_t)a * ns + b) * m + k], e);
-            sc[b] = 53 - e;
-            for (int q = 0; q < SUB_J; ++q) rs[b][q] = 0.0;
-            mn[b] = __builtin_inf();
-            mx[b] = 0.0;
-            cnt[b] = 0;
-            mnp[b] = 0x7FFFFFFFFFFFFFFFll;
-            fl[b] = grid[b] ? 0u : SP_NOGRID;
-        }
+        for (int b = 0; b < NSB; ++b)
+#pragma unroll
+            for (int q = 0; q < MG; ++q)
+                acc[b][q].init(b < ns && q < g ? sum[((int64_t)a * ns + b) * m + k0 + q] : 0.0);
         for (int64_t j = j0 + lane; j < j1; j += 64) {
-            const double v = row[j * m + k];
+            const double* vp = row + j * m + k0;
             const int cb = col_code[j];
-            if (!isfinite(v)) continue;
 #pragma unroll
-            for (int b = 0; b < NSB; ++b) {
-                if (cb != b) continue;
-                ++cnt[b];
-                if (v < mn[b]) {
-                    mn[b] = v;
-                    mnp[b] = j;
-                }
-                if (v > mx[b]) mx[b] = v;
-                if (grid[b]) {
-                    if (v < 0.0) fl[b] |= SP_NEG;
+            for (int q = 0; q < MG; ++q) {
+                if (q >= g) break;
+                const double v = vp[q];
 #pragma unroll
-                    for (int q = 0; q < SUB_J; ++q) {
-                        const double r = ldexp(v, sc[b] - q);
-                        const double R = rint(r);
-                        if (fabs(r - R) == 0.5) fl[b] |= (uint32_t)SP_TIE << q;
-                        rs[b][q] += R;
-                    }
-                }
+                for (int b = 0; b < NSB; ++b)
+                    if (cb == b) acc[b][q].add(v, j);
             }
         }
 #pragma unroll
         for (int b = 0; b < NSB; ++b) {
             if (b >= ns) break;
-            for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-                for (int q = 0; q < SUB_J; ++q) rs[b][q] += __shfl_xor(rs[b][q], o);
-                cnt[b] += __shfl_xor(cnt[b], o);
-                fl[b] |= (uint32_t)__shfl_xor((int)fl[b], o);
-                const double omx = __shfl_xor(mx[b], o);
-                if (omx > mx[b]) mx[b] = omx;
-                const double omn = __shfl_xor(mn[b], o);
-                const long long omp = __shfl_xor(mnp[b], o);
-                if (omn < mn[b] || (omn == mn[b] && omp < mnp[b])) {
-                    mn[b] = omn;
-                    mnp[b] = omp;
-                }
-            }
-            if (lane == 0) {
-                SubPart P;
-                for (int q = 0; q < SUB_J; ++q) P.rsum[q] = rs[b][q];
-                P.mn = mn[b];
-                P.mx = mx[b];
-                P.cnt = cnt[b];
-                P.flags = fl[b];
-                P.pad = 0;
-                part[(x * tmax + (int64_t)b * nch + c) * m + k] = P;
+            for (int q = 0; q < MG; ++q) {
+                if (q >= g) break;
+                const SubPart P = acc[b][q].reduce();
+                if (lane == 0) part[(x * tmax + (int64_t)b * nch + c) * m + k0 + q] = P;
             }
         }
     }

@@ -215,6 +215,7 @@ class VersusAll:
             check_ncd_strings(s.seq for s in seqs)
         eng = self._engine()
         st = eng.upload([s.seq for s in seqs], align=align)
+        t_up = perf_counter()
         try:
             npairs = n * (n - 1) // 2
 
@@ -260,6 +261,7 @@ class VersusAll:
                 D[a, b] = res[:, :M]
                 D[b, a] = res[:, M:]
             self.pairs_walked = walked
+            t_walk = perf_counter()
             # diagonal rule on full tuples: identical (id, seq, extras) -> None unless the
             # alignment of the sequence with itself is not the identity (non-default scores)
             groups: dict = {}
@@ -285,6 +287,9 @@ class VersusAll:
                     D[i, g] = np.nan
         finally:
             st.free()
+        if isinstance(self.timings, dict):  # sub-phases of compute_s (walk includes the pairs text)
+            self.timings["walk_s"] = t_walk - t_up
+            self.timings["diag_s"] = perf_counter() - t_walk
         return D
 
     def _tri_with_pairs(self, seqs, eng, st, D, cidx, clabels, scores, fh) -> bool:
@@ -319,20 +324,38 @@ class VersusAll:
         per_pair = 4 * cap + 16 * Mc + 8
         target = max(1, min(launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
         stream = torch.cuda.Stream(dev)
-        # the counter metrics land in a device copy of D (scattered on the GPU, one D2H at the end)
-        # unless that copy would be large
+        # the counter metrics land in a device copy of D (scattered on the GPU) unless that copy
+        # would be large.  Rows [x0, x1) are complete once their block is scattered (the (r, c < r)
+        # values come from earlier blocks): they go to a pinned staging buffer behind the block's
+        # text, and into D while the GPU aligns the next block
         Dd = None
         if n * n * Mc * 8 <= DEVICE_D_BYTES:
             Dd = torch.full((n, n, Mc), float("nan"), dtype=torch.float64, device=dev)
+        stage = [None, None, None]  # pinned buffer, its event, the rows (x0, x1) it holds
 
-        def flush_d() -> None:
-            if Dd is not None:
-                stream.synchronize()
-                D[:, :, cidx] = Dd.cpu().numpy()
+        def rows_out(x0: int, x1: int) -> None:  # queue rows [x0, x1) of Dd to the staging buffer
+            if Dd is None or x1 <= x0:
+                return
+            if stage[0] is None or stage[0].shape[0] < x1 - x0:
+                stage[0] = torch.empty((x1 - x0, n, Mc), dtype=torch.float64, pin_memory=True)
+            with torch.cuda.stream(stream):
+                stage[0][: x1 - x0].copy_(Dd[x0:x1], non_blocking=True)
+                stage[1] = torch.cuda.Event()
+                stage[1].record(stream)
+            stage[2] = (x0, x1)
+
+        def rows_in() -> None:  # the staged rows into D (waits for their copy only)
+            if stage[2] is None:
+                return
+            x0, x1 = stage[2]
+            stage[1].synchronize()
+            D[x0:x1, :, cidx] = stage[0][: x1 - x0].numpy()
+            stage[2] = None
 
         with torch.cuda.stream(stream):
             lens = torch.as_tensor(lens_h, device=dev)
             # self alignments (x, x) for the diagonal pairs' text
+            t_self = perf_counter()
             strings = eng.align_strings(st, st, np.arange(n), np.arange(n), scores)
             sa = [a.encode("latin-1") for a, _ in strings]
             sb = [b.encode("latin-1") for _, b in strings]
@@ -344,6 +367,8 @@ class VersusAll:
             soff_d = torch.as_tensor(soff, device=dev)
             px_self = self_x.data_ptr() + soff_d
             py_self = self_y.data_ptr() + soff_d
+            if isinstance(self.timings, dict):
+                self.timings["walk_self_s"] = perf_counter() - t_self
             # (b, a) strings of every pair, kept until row b: pointers per triangle pair
             kpx = torch.zeros(npairs, dtype=torch.int64, device=dev)
             kpy = torch.zeros(npairs, dtype=torch.int64, device=dev)
@@ -399,6 +424,7 @@ class VersusAll:
                         for q, kk in enumerate(cidx):
                             D[a_h, b_h, kk] = dd[:, 0, q]
                             D[b_h, a_h, kk] = dd[:, 1, q]
+                rows_in()  # the previous block's rows, while this block aligns
                 # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
                 # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
                 # and (x, x) from the self alignments
@@ -428,16 +454,18 @@ class VersusAll:
                 if isinstance(self.timings, dict):
                     self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
                 del blk, px, py, ln
+                rows_out(x0, x1)
                 report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
                        total)
                 x0 = x1
                 if x0 < n and kept_bytes > keep_limit:
                     # the kept strings outgrew their budget: the remaining rows align every ordered
                     # pair once (row blocks of the rect path), nothing kept
-                    flush_d()
+                    rows_in()
                     del kept, kpx, kpy, klen, Dd
                     return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
-            flush_d()
+            rows_in()
+            stream.synchronize()
             del kept
         return True
 
