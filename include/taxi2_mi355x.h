@@ -132,16 +132,25 @@ int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64
                          const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* d_out,
                          int32_t* d_scores, void* stream);
 
+/* A column view of PREALIGNED set `set_id`: view column c is the set's sequence d_perm[c] (device,
+ * n = the set's size).  It shares the set's bit-planes (destroy it before the set) and is accepted
+ * only as set_r of taxi2_rect_block_dev with the same map as d_col_nat. */
+int taxi2_set_permuted(taxi2_ctx* ctx, int set_id, const int64_t* d_perm, int64_t n, int* view_id);
+
 /* Row block of the streamed pre-aligned versusAll (versus_all.py:732-773 fed block by block, the
  * reductions of config 5): as taxi2_rect_pairs_dev on PREALIGNED sets, with the task's epilogue
  * fused -- every value x scale (percentage_multiply), NaN on x == y when diag (set_q == set_r: the
  * diagonal rule for unique full tuples, versus_all.py:549) -- and, when rmin_metric >= 0, each
  * row's first minimum of that metric over its defined values (-0.0 == 0.0, ties to the lower
- * column): d_rmin_idx[q - q0] (-1: none) and d_rmin_val[q - q0] (NaN: none).  Asynchronous on
- * `stream`; uses the context's staging buffer (one call at a time per context). */
+ * column): d_rmin_idx[q - q0] (-1: none) and d_rmin_val[q - q0] (NaN: none).  d_col_nat (device,
+ * optional): set_r is a permuted copy of set_q whose column c is the task's column d_col_nat[c] --
+ * the block's columns are then stored in set_r's order (config 5: subset order, so the subset
+ * aggregation reads contiguous runs) while the diagonal rule and the row minima (index and tie
+ * order) follow the task's columns.  Asynchronous on `stream`; uses the context's staging buffer
+ * (one call at a time per context). */
 int taxi2_rect_block_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const int32_t* metrics,
                          int nmetrics, double scale, int diag, int rmin_metric, int64_t* d_rmin_idx, double* d_rmin_val,
-                         double* d_out, void* stream);
+                         const int64_t* d_col_nat, double* d_out, void* stream);
 
 /* ---- explicit pair list (align.py:50-51 align_pairs, distances.py:297 calculate) ------- *
  * Pairs (xs[k] of set_x, ys[k] of set_y): out[count][2][nmetrics] in ALIGN mode
@@ -333,11 +342,14 @@ int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* cod
  * the block rows' subset codes, the columns grouped by subset as a CSR (d_col_start[ns + 1],
  * d_col_idx[ncols]: each subset's columns in ascending order).  The state arrays [ns][ns][m] are
  * initialised first when init != 0, else accumulated into; blocks fed in ascending row order give
- * exactly taxi2_subset_aggregate's (= the reference's x-major) sums.  Asynchronous on `stream`. */
+ * exactly taxi2_subset_aggregate's (= the reference's x-major) sums.  d_col_nat (optional): the block's
+ * columns are stored in another order (taxi2_rect_block_dev's column map) -- d_col_idx then holds
+ * stored positions and d_col_nat[c] the task's column of stored column c, which orders ties of the
+ * minimum (-0.0 against 0.0).  Asynchronous on `stream`. */
 int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,
                                const int32_t* d_row_code, const int64_t* d_col_start, const int32_t* d_col_idx,
                                int32_t ns, int init, double* d_sum, double* d_min, double* d_max, int64_t* d_count,
-                               void* stream);
+                               const int64_t* d_col_nat, void* stream);
 
 /* ---- Dereplicate's greedy walk (dereplicate.py:180-196 drop_*_pairs, 289-337 find_replicates,
  * 393-425 the lazily pulled chain that interleaves them) ------------------------------------ *

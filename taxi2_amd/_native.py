@@ -40,6 +40,7 @@ EXPORTS = (
     "taxi2_rect_pairs",
     "taxi2_rect_pairs_dev",
     "taxi2_rect_block_dev",
+    "taxi2_set_permuted",
     "taxi2_rect_strings_dev",
     "taxi2_tri_strings_dev",
     "taxi2_format_pairs_ptr_dev",
@@ -105,8 +106,9 @@ _SIGNATURES = {
     "taxi2_counts_metrics_dev": (_INT, [_P, _P, _I64, _P, _INT, ctypes.c_double, _P, _P]),
     "taxi2_rect_pairs": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_rect_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P, _P]),
+    "taxi2_set_permuted": (_INT, [_P, _INT, _P, _I64, ctypes.POINTER(_INT)]),
     "taxi2_rect_block_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _P, _INT, ctypes.c_double, _INT, _INT, _P, _P, _P,
-                                    _P]),
+                                    _P, _P]),
     "taxi2_rect_strings_dev": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _I32, _P, _P,
                                       _P, _P]),
     "taxi2_format_pairs_dev": (_INT, [_P, _INT, _INT, _I64, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
@@ -133,7 +135,8 @@ _SIGNATURES = {
     "taxi2_subset_aggregate": (_INT, [_P, _I64, _INT, _P, _I32, _P, _P, _P, _P, _INT]),
     "taxi2_format_subset_stats": (_INT, [_I64, _INT, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _I64,
                                          ctypes.POINTER(_I64), _INT]),
-    "taxi2_subset_aggregate_dev": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _I32, _INT, _P, _P, _P, _P, _P]),
+    "taxi2_subset_aggregate_dev": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _I32, _INT, _P, _P, _P, _P, _P,
+                                          _P]),
     "taxi2_dereplicate_walk": (_INT, [_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, ctypes.POINTER(_I64), _P,
                                       _P, _I64, ctypes.POINTER(_I64), _P]),
 }
@@ -343,6 +346,15 @@ class Engine:
             )
         return SeqSet(self, sid.value, nn.value, ml.value, md.value, np.diff(offs))
 
+    def permuted_view(self, s: SeqSet, perm_ptr: int) -> SeqSet:
+        """A column view of pre-aligned set ``s`` whose column c is s's sequence perm[c] (device int64
+        array of s.n entries; taxi2_set_permuted).  Free it before ``s``."""
+        vid = _INT()
+        with self._lock:
+            self._check(self._lib.taxi2_set_permuted(self._ctx, s.id, ctypes.c_void_p(perm_ptr), int(s.n),
+                                                     ctypes.byref(vid)), "taxi2_set_permuted")
+        return SeqSet(self, vid.value, s.n, s.max_len, s.mode, None)
+
     # ------------------------------------------------------------------ pair blocks
     def all_pairs(self, s: SeqSet, k0: int, count: int, metrics, scores=None, *, with_scores=False):
         """Upper-triangle block of ``s``.  ALIGN: (count, 2, M) [(a,b), (b,a)]; else (count, M)."""
@@ -394,15 +406,17 @@ class Engine:
 
     def subset_aggregate_dev(self, vals_ptr: int, nrows: int, ncols: int, m: int, row_code_ptr: int,
                              col_start_ptr: int, col_idx_ptr: int, ns: int, init: bool, sum_ptr: int, min_ptr: int,
-                             max_ptr: int, count_ptr: int, stream: int | None = None) -> None:
-        """taxi2_subset_aggregate_dev on device buffers (see taxi2_amd/streaming.py)."""
+                             max_ptr: int, count_ptr: int, stream: int | None = None, col_nat_ptr: int | None = None) -> None:
+        """taxi2_subset_aggregate_dev on device buffers (see taxi2_amd/streaming.py); ``col_nat_ptr``:
+        the task column of each stored column when the block is stored permuted."""
         with self._lock:
             self._check(
                 self._lib.taxi2_subset_aggregate_dev(
                     self._ctx, ctypes.c_void_p(vals_ptr), int(nrows), int(ncols), int(m), ctypes.c_void_p(row_code_ptr),
                     ctypes.c_void_p(col_start_ptr), ctypes.c_void_p(col_idx_ptr), int(ns), 1 if init else 0,
                     ctypes.c_void_p(sum_ptr), ctypes.c_void_p(min_ptr), ctypes.c_void_p(max_ptr),
-                    ctypes.c_void_p(count_ptr), ctypes.c_void_p(stream) if stream else None,
+                    ctypes.c_void_p(count_ptr), ctypes.c_void_p(col_nat_ptr) if col_nat_ptr else None,
+                    ctypes.c_void_p(stream) if stream else None,
                 ),
                 "taxi2_subset_aggregate_dev",
             )
@@ -441,17 +455,20 @@ class Engine:
 
     def rect_block_dev(self, s: SeqSet, q0: int, q1: int, metrics, out_ptr: int, scale: float = 1.0,
                        diag: bool = True, rmin_metric: int = -1, rmin_idx_ptr: int | None = None,
-                       rmin_val_ptr: int | None = None, stream: int | None = None) -> None:
+                       rmin_val_ptr: int | None = None, stream: int | None = None, cols: SeqSet | None = None,
+                       col_nat_ptr: int | None = None) -> None:
         """Row block [q0, q1) x set of the streamed pre-aligned versusAll with the task's epilogue on the
         GPU (taxi2_rect_block_dev): values x scale, NaN on the diagonal, each row's first minimum of
-        metric index rmin_metric (idx -1 / NaN: none)."""
+        metric index rmin_metric (idx -1 / NaN: none).  ``cols`` / ``col_nat_ptr``: the columns come
+        from a permuted copy of ``s`` (stored in its order), column c being task column col_nat[c]."""
         codes = metric_codes(metrics)
         with self._lock:
             self._check(
                 self._lib.taxi2_rect_block_dev(
-                    self._ctx, s.id, s.id, int(q0), int(q1), codes.ctypes.data, len(codes), float(scale),
+                    self._ctx, s.id, (cols or s).id, int(q0), int(q1), codes.ctypes.data, len(codes), float(scale),
                     1 if diag else 0, int(rmin_metric), ctypes.c_void_p(rmin_idx_ptr) if rmin_idx_ptr else None,
-                    ctypes.c_void_p(rmin_val_ptr) if rmin_val_ptr else None, ctypes.c_void_p(out_ptr),
+                    ctypes.c_void_p(rmin_val_ptr) if rmin_val_ptr else None,
+                    ctypes.c_void_p(col_nat_ptr) if col_nat_ptr else None, ctypes.c_void_p(out_ptr),
                     ctypes.c_void_p(stream) if stream else None,
                 ),
                 "taxi2_rect_block_dev",

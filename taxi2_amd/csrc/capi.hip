@@ -46,6 +46,9 @@ struct DevSet {
     int64_t* offs = nullptr;
     int4* meta = nullptr;
     uint4* planes = nullptr;
+    // a column view (taxi2_set_permuted): its own meta, the parent's planes; no bytes / offsets, so
+    // only the pre-aligned row-block entry (taxi2_rect_block_dev) accepts it
+    bool view = false;
 };
 
 }  // namespace
@@ -138,7 +141,7 @@ int shared_release(taxi2_ctx* ctx, hipStream_t st) {
 }
 
 DevSet* get_set(taxi2_ctx* ctx, int id) {
-    if (id < 0 || id >= (int)ctx->sets.size() || !ctx->sets[id].live) return nullptr;
+    if (id < 0 || id >= (int)ctx->sets.size() || !ctx->sets[id].live || ctx->sets[id].view) return nullptr;
     return &ctx->sets[id];
 }
 
@@ -996,7 +999,7 @@ int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const Pa
     // triangle / rectangle blocks: PT x PT pair tiles with LDS-staged planes (prealigned_kernel.hpp);
     // TAXI2_PRE_NOTILE=1 keeps the one-thread-per-pair kernel (A/B and parity tests)
     // (the row-block epilogue of taxi2_rect_block_dev exists only in the tiled kernel)
-    const bool epi = tb.rmin_v || tb.diag || tb.scale != 1.0;
+    const bool epi = tb.rmin_v || tb.diag || tb.scale != 1.0 || tb.ynat;
     if (ps.mode != PAIRS_LIST && (epi || (ps.count >= 4096 && !getenv("TAXI2_PRE_NOTILE")))) {
         int64_t x0, nx, y0, ny;
         if (ps.mode == PAIRS_TRI) {
@@ -1406,8 +1409,38 @@ int taxi2_set_create(taxi2_ctx* ctx, const uint8_t* bytes, const int64_t* offset
     return 0;
 }
 
+int taxi2_set_permuted(taxi2_ctx* ctx, int set_id, const int64_t* d_perm, int64_t n, int* view_id) {
+    if (!ctx || !view_id) return -1;
+    DevSet* P = get_set(ctx, set_id);
+    if (!P) return fail(ctx, "unknown set %d", set_id);
+    if (P->mode != TAXI2_MODE_PREALIGNED) return fail(ctx, "taxi2_set_permuted: PREALIGNED sets only");
+    if (n != P->n || (n && !d_perm)) return fail(ctx, "taxi2_set_permuted: the permutation must cover the set");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    DevSet v = *P;  // the parent's planes and sizes
+    v.view = true;
+    v.bytes = nullptr;
+    v.offs = nullptr;
+    v.meta = nullptr;
+    HIP_TRY(ctx, hipMalloc(&v.meta, std::max<int64_t>(n, 1) * sizeof(int4)));
+    if (n) {
+        hipLaunchKernelGGL(k_meta_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, P->meta, d_perm,
+                           n, v.meta);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->sets.push_back(v);
+    *view_id = (int)ctx->sets.size() - 1;
+    return 0;
+}
+
 int taxi2_set_destroy(taxi2_ctx* ctx, int set_id) {
     if (!ctx) return -1;
+    if (set_id >= 0 && set_id < (int)ctx->sets.size() && ctx->sets[set_id].live && ctx->sets[set_id].view) {
+        (void)hipSetDevice(ctx->device);
+        if (ctx->sets[set_id].meta) (void)hipFree(ctx->sets[set_id].meta);
+        ctx->sets[set_id] = DevSet();
+        return 0;
+    }
     DevSet* s = get_set(ctx, set_id);
     if (!s) return 0;
     (void)hipSetDevice(ctx->device);
@@ -1566,26 +1599,31 @@ int taxi2_rect_pairs_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64
 
 int taxi2_rect_block_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1, const int32_t* metrics,
                          int nmetrics, double scale, int diag, int rmin_metric, int64_t* d_rmin_idx, double* d_rmin_val,
-                         double* d_out, void* stream) {
+                         const int64_t* d_col_nat, double* d_out, void* stream) {
     if (!ctx) return -1;
     DevSet* Q = get_set(ctx, set_q);
-    DevSet* R = get_set(ctx, set_r);
+    // the column side may be a view of Q (taxi2_set_permuted)
+    DevSet* R = (set_r >= 0 && set_r < (int)ctx->sets.size() && ctx->sets[set_r].live) ? &ctx->sets[set_r] : nullptr;
     if (!Q || !R) return fail(ctx, "unknown set");
     if (Q->mode != TAXI2_MODE_PREALIGNED || R->mode != TAXI2_MODE_PREALIGNED)
         return fail(ctx, "taxi2_rect_block_dev: PREALIGNED sets only");
+    if (R->view && (!d_col_nat || R->planes != Q->planes))
+        return fail(ctx, "taxi2_rect_block_dev: a column view needs its parent as the row set and the column map");
     MetricSpec ms;
     if (check_metrics(ctx, metrics, nmetrics, ms, false, std::max(Q->max_len, R->max_len))) return -1;
     if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
     if (rmin_metric >= nmetrics || (rmin_metric >= 0 && (!d_rmin_idx || !d_rmin_val)))
         return fail(ctx, "bad row-minimum metric or outputs");
-    if (diag && set_q != set_r) return fail(ctx, "the diagonal rule needs one set on both sides");
+    if (diag && set_q != set_r && !d_col_nat)
+        return fail(ctx, "the diagonal rule needs one set on both sides (or the column map of a permuted copy)");
+    if (d_col_nat && R->n != Q->n) return fail(ctx, "a column map needs a permuted copy of the row set");
     if ((q1 - q0) * R->n > 0 && !d_out) return fail(ctx, "null output");
     if (q1 == q0 || R->n == 0) return 0;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     PairSrc ps{PAIRS_RECT, q0 * R->n, (q1 - q0) * R->n, 0, R->n, nullptr, nullptr};
     const int64_t nx = q1 - q0, tiles_y = (R->n + PT - 1) / PT;
-    TileBlock tb{scale, diag ? 1 : 0, rmin_metric, nullptr, nullptr};
+    TileBlock tb{scale, diag ? 1 : 0, rmin_metric, nullptr, nullptr, d_col_nat};
     if (rmin_metric >= 0) {
         if (ensure(ctx, &ctx->d_aux, &ctx->d_aux_bytes, (size_t)nx * tiles_y * 16)) return -1;
         tb.rmin_v = (double*)ctx->d_aux;
@@ -2186,7 +2224,7 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
 int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,
                                const int32_t* d_row_code, const int64_t* d_col_start, const int32_t* d_col_idx,
                                int32_t ns, int init, double* d_sum, double* d_min, double* d_max, int64_t* d_count,
-                               void* stream) {
+                               const int64_t* d_col_nat, void* stream) {
     if (!ctx) return -1;
     if (nrows < 0 || ncols < 0 || m < 1 || ns < 0) return fail(ctx, "invalid sizes to taxi2_subset_aggregate_dev");
     const int64_t nk = (int64_t)ns * ns * m;
@@ -2235,15 +2273,11 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     int32_t* ngrp = (int32_t*)(base + o_n);
     unsigned int* wcount = (unsigned int*)(base + o_n + 64);
     uint8_t* ccode = (uint8_t*)(base + o_ccode);
-    if (nat) {
-        std::vector<int32_t> hc(ns + 1);
-        for (int b = 0; b <= ns; ++b) hc[b] = (int32_t)(b * nch);
-        HIP_TRY(ctx, hipMemcpyAsync(cofs, hc.data(), (ns + 1) * 4, hipMemcpyHostToDevice, st));
+    if (nat) {  // cofs[b] = b * nch, on the device (no host staging, no synchronisation)
+        hipLaunchKernelGGL(k_subset_natcofs, dim3(1), dim3(64), 0, st, (int)ns, (int)nch, cofs);
         if (ncols > 0)
             hipLaunchKernelGGL(k_subset_colcode, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, st, d_col_start,
                                d_col_idx, (int)ns, ncols, ccode);
-        // the host vector must outlive the async copy
-        HIP_TRY(ctx, hipStreamSynchronize(st));
     } else {
         hipLaunchKernelGGL(k_subset_cofs, dim3(1), dim3(1024), 0, st, d_col_start, (int)ns, cofs);
     }
@@ -2258,10 +2292,10 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
             const dim3 g((unsigned)((nr * nch + 3) / 4)), b(256);
             if (ns <= 2)
                 hipLaunchKernelGGL(k_subset_rows_nat<2>, g, b, 0, st, v, nr, ncols, m, rc, (const uint8_t*)ccode, (int)ns,
-                                   (int)nch, (const double*)d_sum, cpart);
+                                   (int)nch, (const double*)d_sum, cpart, d_col_nat);
             else
                 hipLaunchKernelGGL(k_subset_rows_nat<4>, g, b, 0, st, v, nr, ncols, m, rc, (const uint8_t*)ccode, (int)ns,
-                                   (int)nch, (const double*)d_sum, cpart);
+                                   (int)nch, (const double*)d_sum, cpart, d_col_nat);
         } else {
             hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * tmax + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m,
                                rc, d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum,

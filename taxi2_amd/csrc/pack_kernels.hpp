@@ -105,4 +105,12 @@ __global__ void __launch_bounds__(256) k_counts_metrics(const uint64_t* __restri
     }
 }
 
+// A column view's meta: view[c] = meta[perm[c]] (taxi2_set_permuted; the plane offsets keep
+// pointing into the parent's planes).
+__global__ void __launch_bounds__(256) k_meta_gather(const int4* __restrict__ meta, const int64_t* __restrict__ perm,
+                                                     int64_t n, int4* __restrict__ view) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n) view[c] = meta[perm[c]];
+}
+
 }  // namespace taxi2

@@ -87,6 +87,9 @@ struct TileBlock {
     int diag, rmin_k;
     double* rmin_v;   // [nx][tiles_y]: tile minimum (+inf: none)
     int64_t* rmin_y;  // its column (-1: none)
+    // column y of the Y set is the task's column ynat[y] (a permuted copy of the X set: config 5's
+    // columns in subset order); nullptr: y itself.  The diagonal and the row minima use it.
+    const int64_t* ynat = nullptr;
 };
 struct RowMin {
     double v;
@@ -186,16 +189,17 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
                 slot = x * ps.R + y - ps.k0;  // a launch may start / end inside a row
             }
             ok = ok && slot >= 0 && slot < ps.count;
-            const bool none = tb.diag && x == y;
+            const int64_t yn = tb.ynat ? (ok ? tb.ynat[y] : -1) : y;  // the task's column
+            const bool none = tb.diag && x == yn;
             for (int m = 0; m < nm; ++m) {
                 const double v = none ? __builtin_nan("")
                                       : metric_value(ms.code[m], c[i][j][0], c[i][j][1], c[i][j][2], c[i][j][3]) * tb.scale;
                 if (staged) stg[(tx * PT + ty + 16 * j) * nm + m] = v;
                 else if (ok) out[slot * nm + m] = v;
-                // j ascending is y ascending: the first of equal values stays
-                if (ok && m == tb.rmin_k && __builtin_isfinite(v) && v < rv[i]) {
+                // the first (lowest task column) of equal values stays
+                if (ok && m == tb.rmin_k && __builtin_isfinite(v) && (ry[i] < 0 || rowmin_less(v, yn, rv[i], ry[i]))) {
                     rv[i] = v;
-                    ry[i] = y;
+                    ry[i] = yn;
                 }
             }
         }

@@ -50,7 +50,7 @@ struct SubPart {            // one (block row, column subset b, metric k)
     double mn, mx;          // first minimum (from +inf), maximum (from 0.0)
     long long cnt;          // defined values
     uint32_t flags;         // SP_*: where the integer step does not reproduce the sequential sum
-    int32_t pad;
+    int32_t mnp;            // the minimum's column (ties between chunks: the lower one is first)
 };
 // SP_TIE << j: some value lies exactly halfway between two multiples of 2^j u
 enum : uint32_t { SP_NOGRID = 1, SP_NEG = 2, SP_TIE = 4 };
@@ -236,7 +236,7 @@ struct SubAcc {
         P.mx = mx;
         P.cnt = c;
         P.flags = fl;
-        P.pad = 0;
+        P.mnp = (int32_t)min(mnp, (long long)INT32_MAX);
         return P;
     }
 };
@@ -290,6 +290,11 @@ __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ 
     }
 }
 
+// cofs[b] = b * nch (k_subset_rows_nat's chunk slots: ns subsets x nch chunks per row).
+__global__ void k_subset_natcofs(int ns, int nch, int32_t* __restrict__ cofs) {
+    for (int b = threadIdx.x; b <= ns; b += blockDim.x) cofs[b] = b * nch;
+}
+
 // Column codes from the sorted layout: code[col_idx[j]] = b for j in [col_start[b], col_start[b+1]).
 __global__ void __launch_bounds__(256) k_subset_colcode(const int64_t* __restrict__ col_start,
                                                         const int32_t* __restrict__ col_idx, int ns, int64_t ncols,
@@ -314,7 +319,8 @@ template <int NSB>
 __global__ void __launch_bounds__(256) k_subset_rows_nat(const double* __restrict__ vals, int64_t nrows,
                                                          int64_t ncols, int m, const int32_t* __restrict__ row_code,
                                                          const uint8_t* __restrict__ col_code, int ns, int nch,
-                                                         const double* __restrict__ sum, SubPart* __restrict__ part) {
+                                                         const double* __restrict__ sum, SubPart* __restrict__ part,
+                                                         const int64_t* __restrict__ nat) {
     constexpr int MG = NSB <= 2 ? 2 : 1;  // metrics per pass (NSB x MG accumulators in registers)
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -336,13 +342,14 @@ __global__ void __launch_bounds__(256) k_subset_rows_nat(const double* __restric
         for (int64_t j = j0 + lane; j < j1; j += 64) {
             const double* vp = row + j * m + k0;
             const int cb = col_code[j];
+            const int64_t jn = nat ? nat[j] : j;  // the task's column of stored column j
 #pragma unroll
             for (int q = 0; q < MG; ++q) {
                 if (q >= g) break;
                 const double v = vp[q];
 #pragma unroll
                 for (int b = 0; b < NSB; ++b)
-                    if (cb == b) acc[b][q].add(v, j);
+                    if (cb == b) acc[b][q].add(v, jn);
             }
         }
 #pragma unroll
@@ -372,7 +379,10 @@ __global__ void __launch_bounds__(256) k_subset_rowmerge(int64_t nrows, int ns, 
     for (int t = cofs[b] + 1; t < cofs[b + 1]; ++t) {
         const SubPart& P = cpart[(x * tmax + t) * m + k];
         for (int q = 0; q < SUB_J; ++q) R.rsum[q] += P.rsum[q];  // integers: exact in any order
-        if (P.mn < R.mn) R.mn = P.mn;                            // strict: the earlier chunk's on ties
+        if (P.mn < R.mn || (P.mn == R.mn && P.mnp < R.mnp)) {  // ties: the lower column (-0.0 vs 0.0)
+            R.mn = P.mn;
+            R.mnp = P.mnp;
+        }
         if (P.mx > R.mx) R.mx = P.mx;
         R.cnt += P.cnt;
         R.flags |= P.flags;

@@ -254,13 +254,23 @@ class SubsetAggregatorDev:
         self.eng, self.m, self.ns, self.n = eng, m, ns, len(ids)
         self.row_code = torch.as_tensor(code, dtype=torch.int32, device=dev)
         self.col_start = torch.as_tensor(start, dtype=torch.int64, device=dev)
+        self.order = order  # the task's columns in subset order (ascending within a subset)
         self.col_idx = torch.as_tensor(order.astype(np.int32), dtype=torch.int32, device=dev)
+        self.col_nat = None
         shape = (ns, ns, m)
         self.sum = torch.zeros(shape, dtype=torch.float64, device=dev)
         self.min = torch.full(shape, float("inf"), dtype=torch.float64, device=dev)
         self.max = torch.zeros(shape, dtype=torch.float64, device=dev)
         self.count = torch.zeros(shape, dtype=torch.int64, device=dev)
         self.torch = torch
+
+    def set_storage(self, inv: np.ndarray, nat) -> None:
+        """The blocks arrive with their columns stored permuted: stored column c is task column nat[c]
+        (device int64), inv its inverse (host).  The subsets' columns are indexed by stored position
+        from then on; sums are exact in any order and nat orders the minimum's ties."""
+        self.col_idx = self.torch.as_tensor(inv[self.order].astype(np.int32), dtype=self.torch.int32,
+                                            device=self.col_idx.device)
+        self.col_nat = nat
 
     def add(self, D, x0: int, x1: int) -> None:
         """D: (x1 - x0, n, m) float64 device tensor of the rows' adjusted values (NaN = None),
@@ -278,7 +288,8 @@ class SubsetAggregatorDev:
         self.eng.subset_aggregate_dev(D.data_ptr(), x1 - x0, self.n, self.m, self.row_code[x0:x1].data_ptr(),
                                       self.col_start.data_ptr(), self.col_idx.data_ptr(), self.ns, False,
                                       self.sum.data_ptr(), self.min.data_ptr(), self.max.data_ptr(),
-                                      self.count.data_ptr(), st)
+                                      self.count.data_ptr(), st,
+                                      col_nat_ptr=self.col_nat.data_ptr() if self.col_nat is not None else None)
         if side is not None:
             cur.wait_stream(side)
 

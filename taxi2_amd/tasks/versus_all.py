@@ -784,6 +784,21 @@ class VersusAll:
         pairs_text = None
 
         fused = [None]  # the block's fused row minima (pre-aligned, taxi2_rect_block_dev)
+        # Pre-aligned reductions without text: the blocks' columns are stored in the order of the
+        # partition with the most subsets (a column view of the set, taxi2_set_permuted), so its
+        # aggregation reads each subset as one contiguous run instead of gathering it column by
+        # column; the diagonal rule, the row minima and the other partition follow the task's columns
+        cols_view = col_nat = None
+        big = [agg for _, agg in sink.aggs if agg.ns > 4]
+        if not walk and not p.pairs.align and not text and big and not os.environ.get("TAXI2_NO_COLPERM"):
+            order = max(big, key=lambda a: a.ns).order.astype(np.int64)
+            col_nat = torch.as_tensor(order, device=cuda)
+            cols_view = eng.permuted_view(st, col_nat.data_ptr())
+            inv = np.empty(n, dtype=np.int64)
+            inv[order] = np.arange(n, dtype=np.int64)
+            for _, agg in sink.aggs:
+                agg.set_storage(inv, col_nat)
+            sink.col_map = (order, inv, col_nat)
 
         def block(x0, x1):
             nonlocal pairs_text
@@ -810,7 +825,8 @@ class VersusAll:
                                 torch.empty(x1 - x0, dtype=torch.float64, device=cuda))
                 eng.rect_block_dev(st, x0, x1, labels, D.data_ptr(), scale, True, k,
                                    fused[0][0].data_ptr() if k >= 0 else None,
-                                   fused[0][1].data_ptr() if k >= 0 else None, stream.cuda_stream)
+                                   fused[0][1].data_ptr() if k >= 0 else None, stream.cuda_stream, cols=cols_view,
+                                   col_nat_ptr=col_nat.data_ptr() if col_nat is not None else None)
                 sink.diagonal(x0, x1, D, scale, main=False)
                 tick("compute_s", t)
                 return D
@@ -871,6 +887,8 @@ class VersusAll:
                 sink.close()
                 times["finish_s"] = perf_counter() - t_cl
         finally:
+            if cols_view is not None:
+                cols_view.free()  # before its parent set
             st.free()
         self.timings = times
 
@@ -1113,6 +1131,7 @@ class _BlockWriters:
             self.aligner = (PairwiseAligner.Biopython(p.pairs.scores, engine=eng) if p.pairs.align else None)
         self.walk = walk
         self.torch = torch
+        self.col_map = None  # (order, inverse, device order) when the blocks' columns are stored permuted
 
     def consume(self, x0: int, x1: int, D, scale: float) -> None:
         """D: (x1 - x0, n, M) device tensor of the rows' values, x100 applied, diagonal not yet."""
@@ -1144,13 +1163,15 @@ class _BlockWriters:
             r = torch.arange(x1 - x0, device=D.device)
             D[r, r + x0] = float("nan")
         lo, hi = np.searchsorted(self._special_rows, [x0, x1])
+        inv = self.col_map[1] if self.col_map is not None else None  # task column -> stored column
         for i, gi in self._special[lo:hi]:
             g = dup[gi]
             if strings is not None and strings[gi][0] != strings[gi][1]:
-                D[i - x0, i] = torch.as_tensor(self_vals[gi] * scale if scale != 1.0 else self_vals[gi],
-                                               device=D.device)
+                D[i - x0, i if inv is None else int(inv[i])] = torch.as_tensor(
+                    self_vals[gi] * scale if scale != 1.0 else self_vals[gi], device=D.device)
             else:
-                D[i - x0, torch.as_tensor(g, device=D.device)] = float("nan")
+                cols = np.asarray(g) if inv is None else inv[np.asarray(g)]
+                D[i - x0, torch.as_tensor(cols, device=D.device)] = float("nan")
 
     def aggregate(self, x0: int, x1: int, D) -> None:
         for _, agg in self.aggs:
@@ -1171,8 +1192,11 @@ class _BlockWriters:
                 rr = torch.as_tensor(rows - x0, device=D.device)
                 v = D[rr][:, :, self.rmin_k]
                 v = torch.where(torch.isfinite(v), v, torch.full_like(v, float("inf")))
+                if self.col_map is not None:  # stored columns permuted: back to the task's order
+                    v = v[:, torch.as_tensor(self.col_map[1], device=D.device)]
                 d, ix = torch.min(v, dim=1)
                 ok = torch.isfinite(d)
+                d = torch.gather(v, 1, ix[:, None])[:, 0]  # the first minimum's own value (-0.0 / 0.0)
                 self.rmin_idx[rows] = torch.where(ok, ix, torch.full_like(ix, -1)).cpu().numpy()
                 self.rmin_d[rows] = torch.where(ok, d, torch.full_like(d, float("nan"))).cpu().numpy()
             return
