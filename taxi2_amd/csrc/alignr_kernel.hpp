@@ -33,6 +33,14 @@
 namespace taxi2 {
 
 constexpr int AR_BLK = 16;  // steps between the fill waves' progress checks / publications
+// Rows buffered between the fill waves (the ring) and how far wave 0 may run ahead of wave 1: wave 0
+// rewrites a ring slot AR_RING - 63 steps after wave 1 read it, and the row record of row r
+// (XR = 512 slots, written up to 64 rows ahead) AR_XR - 64 - 63 rows after wave 1's oldest use.
+#ifndef TAXI2_AR_RING
+#define TAXI2_AR_RING 256
+#endif
+constexpr int AR_RING = TAXI2_AR_RING;
+constexpr int AR_AHEAD = (AR_RING - 63) < (512 - 64 - 63 - AR_BLK) ? (AR_RING - 63) : (512 - 64 - 63 - AR_BLK);
 #ifndef TAXI2_AR_UNITS
 #define TAXI2_AR_UNITS 8
 #endif
@@ -197,7 +205,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     __shared__ ArRow tab[2][AR_UNITS];
     __shared__ ArChain chs[2];
     __shared__ int fin[2][AR_UNITS][2];
-    __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * RING];
+    __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * AR_RING];
     __shared__ uint32_t eqt[4][NT][K];  // (s(x0_k, base), s(x1_k, base)) - co_i as pk_int, per lane and slot
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows, s_seg;
@@ -547,7 +555,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 const int tq = WI * 64 + ln;
                 const uint4 rec = *(const uint4*)((const char*)xinfo + ((((uint32_t)s << 4) - ln16) & ((XR - 1) << 4)));
                 uint2 o_ring = make_uint2(0u, 0u);
-                if constexpr (!FW) o_ring = ring[(WI - 1) * RING + ((s + 1) & (RING - 1))];
+                if constexpr (!FW) o_ring = ring[(WI - 1) * AR_RING + ((s + 1) & (AR_RING - 1))];
                 const bool in_band = (uint8_t)((uint32_t)tq - rec.y) <= (uint8_t)(rec.y >> 8);
                 const uint64_t bmask = __builtin_amdgcn_ballot_w64(in_band);
                 asm volatile("" ::"s"(bmask));
@@ -642,7 +650,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 payF = as_u32(F1);
                 payY = as_u32(Y);
                 if constexpr (HO)
-                    if (ln == 63) ring[WI * RING + ((g + 1) & (RING - 1))] = make_uint2(payF, payY);
+                    if (ln == 63) ring[WI * AR_RING + ((g + 1) & (AR_RING - 1))] = make_uint2(payF, payY);
                 if (pre && (rec.y & AR_LAST) && (tq == own0 || tq == own1)) {  // owner of a half's column nB_h
                     int t = 0;
                     for (int q = 1; q < n; ++q)
@@ -680,7 +688,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     const unsigned long long t0 = AR_NOW();
 #endif
                     if (W > 1) {  // wait for the other fill wave
-                        const int need = w == 0 ? s1 - (RING - 63) : s1 + 63;
+                        const int need = w == 0 ? s1 - AR_AHEAD : s1 + 63;
                         while (__hip_atomic_load(&s_prog[other], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
                             __builtin_amdgcn_s_sleep(1);
                     }

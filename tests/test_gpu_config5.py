@@ -80,3 +80,37 @@ def test_streamed_subsets_exact_vs_dense(tmp_path, engine):
     for f in sorted((tmp_path / "dense" / "subsets").rglob("*.tsv")):
         rel = f.relative_to(tmp_path / "dense")
         assert (tmp_path / "stream" / rel).read_bytes() == f.read_bytes(), rel
+
+
+def test_column_view_matches_task_order(tmp_path, engine, monkeypatch):
+    """The reductions-only stream stores its blocks' columns in species order (taxi2_set_permuted);
+    with duplicated rows (the diagonal rule's NaN groups), row minima and every subset statistic
+    equal the run that keeps the task's column order (TAXI2_NO_COLPERM), bit for bit."""
+    from bench_secondary import build_config5_task as build_task
+    from taxi2_amd.sequences import Sequences
+
+    n, L = 3000, 400
+
+    def run(sub, perm):
+        if perm:
+            monkeypatch.delenv("TAXI2_NO_COLPERM", raising=False)
+        else:
+            monkeypatch.setenv("TAXI2_NO_COLPERM", "1")
+        task, _, _ = build_task(n, L, engine, tmp_path / sub, 0.02)
+        seqs = list(task.input.sequences)
+        for k in range(0, 60, 3):  # 20 duplicated full tuples (id, sequence, extras)
+            seqs[k + 1] = seqs[k]
+        task.input.sequences = Sequences(seqs)
+        task.start()
+        return task
+
+    a, b = run("perm", True), run("plain", False)
+    ia, da = a.row_minima
+    ib, db = b.row_minima
+    assert np.array_equal(ia, ib)
+    assert np.array_equal(_bits(np.nan_to_num(da, nan=-7.0)), _bits(np.nan_to_num(db, nan=-7.0)))
+    for name in ("genera", "species"):
+        x, y = a.subset_stats[name], b.subset_stats[name]
+        assert np.array_equal(x.count, y.count)
+        for u, v in ((x.mean, y.mean), (x.min, y.min), (x.max, y.max)):
+            assert np.array_equal(_bits(np.nan_to_num(u, nan=-7.0)), _bits(np.nan_to_num(v, nan=-7.0))), name
