@@ -39,6 +39,17 @@ from .common import (Results, console_report, create_parents, fixed_decimals, fo
                      report, seq_key, write_rows_gpu)
 
 
+def self_strings(eng, st, seqs: list, idx, scores: tuple) -> list:
+    """Each sequence idx[k] aligned with itself (versus_all.py:549's diagonal rule, the diagonal pairs
+    of aligned_pairs.txt).  When a match scores > 0 and no gap score is positive the first
+    alignment is the identity -- the diagonal scores len * match and any path with gaps trades at
+    least one match for gaps -- so no alignment is run; otherwise the aligner's own strings."""
+    m, _, io, ie, eo, ee = scores
+    if m > 0 and max(io, ie, eo, ee) <= 0:
+        return [(seqs[i].seq, seqs[i].seq) for i in np.asarray(idx).tolist()]
+    return eng.align_strings(st, st, idx, idx, scores)
+
+
 def walk_strings_ok(scores: tuple, seqs: list) -> bool:
     """Does the packed trace-and-walk aligner (which can write the aligned strings while its walks
     give the metrics) cover this run?  Gotoh scores (not every open == extend), pairs up to 2 048
@@ -270,7 +281,7 @@ class VersusAll:
             dup = [g for g in groups.values()]
             if align:
                 reps = np.array([g[0] for g in dup], dtype=np.int64)
-                strings = eng.align_strings(st, st, reps, reps, scores)
+                strings = self_strings(eng, st, seqs, reps, scores)
                 self_vals = np.empty((len(reps), M))
                 if cidx:
                     self_vals[:, cidx] = eng.list_pairs(st, st, reps, reps, clabels, scores)[:, 0, :]
@@ -356,7 +367,7 @@ class VersusAll:
             lens = torch.as_tensor(lens_h, device=dev)
             # self alignments (x, x) for the diagonal pairs' text
             t_self = perf_counter()
-            strings = eng.align_strings(st, st, np.arange(n), np.arange(n), scores)
+            strings = self_strings(eng, st, seqs, np.arange(n), scores)
             sa = [a.encode("latin-1") for a, _ in strings]
             sb = [b.encode("latin-1") for _, b in strings]
             slen_self = torch.as_tensor(np.array([len(a) for a in sa], dtype=np.int32), device=dev)
@@ -712,7 +723,7 @@ class VersusAll:
         cidx = [k for k, lab in enumerate(labels) if lab != "ncd"]
         nidx = [k for k, lab in enumerate(labels) if lab == "ncd"]
         reps = np.array([g[0] for g in dup], dtype=np.int64)
-        strings = eng.align_strings(st, st, reps, reps, scores)
+        strings = self_strings(eng, st, seqs, reps, scores)
         self_vals = np.empty((len(reps), len(labels)))
         if cidx:
             self_vals[:, cidx] = eng.list_pairs(st, st, reps, reps, [labels[k] for k in cidx], scores)[:, 0, :]
