@@ -91,3 +91,19 @@ def report(progress: Callable | None, caption: str, index: int, total: int) -> N
 def seq_key(s) -> tuple:
     """Full-tuple identity used by the diagonal rule (versus_all.py:549 ``x != y``)."""
     return (s.id, s.seq, tuple(sorted(s.extras.items())) if s.extras else ())
+
+
+def full_tuple_groups(seqs) -> list:
+    """Indices of identical full tuples (seq_key), groups in first-appearance order.  Equal tuples
+    have equal ids, so a sequence whose id occurs once is its own group without hashing its
+    sequence (N = 200 000 x 1 000 bp: 0.5 s of string hashing otherwise)."""
+    from collections import Counter
+
+    ids = [s.id for s in seqs]
+    cnt = Counter(ids)
+    if len(cnt) == len(ids):
+        return [[i] for i in range(len(ids))]
+    groups: dict = {}
+    for i, s in enumerate(seqs):
+        groups.setdefault(seq_key(s) if cnt[ids[i]] > 1 else (i,), []).append(i)
+    return list(groups.values())

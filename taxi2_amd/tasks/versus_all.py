@@ -35,8 +35,8 @@ from ..distances import ENGINE_LABELS, Distance, DistanceHandler, DistanceMetric
 from ..pairs import SequencePair, SequencePairHandler
 from ..sequences import Sequences
 from ..types import AttrDict
-from .common import (Results, console_report, create_parents, fixed_decimals, format_values, gpu_text_ok,
-                     report, seq_key, write_rows_gpu)
+from .common import (Results, console_report, create_parents, fixed_decimals, format_values, full_tuple_groups,
+                     gpu_text_ok, report, write_rows_gpu)
 
 
 def self_strings(eng, st, seqs: list, idx, scores: tuple) -> list:
@@ -275,10 +275,7 @@ class VersusAll:
             t_walk = perf_counter()
             # diagonal rule on full tuples: identical (id, seq, extras) -> None unless the
             # alignment of the sequence with itself is not the identity (non-default scores)
-            groups: dict = {}
-            for i, s in enumerate(seqs):
-                groups.setdefault(seq_key(s), []).append(i)
-            dup = [g for g in groups.values()]
+            dup = full_tuple_groups(seqs)
             if align:
                 reps = np.array([g[0] for g in dup], dtype=np.int64)
                 strings = self_strings(eng, st, seqs, reps, scores)
@@ -714,10 +711,7 @@ class VersusAll:
         """Inputs of the diagonal rule (versus_all.py:549): groups of identical full tuples, and when
         aligning each group's first alignment with itself (strings) and its values -- a sequence
         whose self-alignment is not the identity (non-default scores) keeps its own values."""
-        groups: dict = {}
-        for i, s in enumerate(seqs):
-            groups.setdefault(seq_key(s), []).append(i)
-        dup = list(groups.values())
+        dup = full_tuple_groups(seqs)
         if not align:
             return dup, None, None
         cidx = [k for k, lab in enumerate(labels) if lab != "ncd"]
@@ -1328,11 +1322,18 @@ class _BlockWriters:
             path = self.task.paths.distances_linear.parent / "row_minima.tsv"
             create_parents(path)
             fmt, missing = self.fmt, self.missing
+            from .subsets import _tokens
+
+            # values through the bulk formatter (Python-exact "{:.Nf}"), one join for the file
+            fin = np.isfinite(self.rmin_d)
+            vals = np.full(len(self.ids), missing, dtype=object)
+            if fin.any():
+                vals[fin] = _tokens(self.rmin_d[fin], fmt, self.eng)
+            ids = self.ids
+            close = [ids[j] if j >= 0 else missing for j in self.rmin_idx.tolist()]
             with open(path, "w") as fh:
                 fh.write(f"seqid\tclosest\t{self.metrics[self.rmin_k]}\n")
-                for i, (j, d) in enumerate(zip(self.rmin_idx, self.rmin_d)):
-                    fh.write(f"{self.ids[i]}\t{self.ids[j] if j >= 0 else missing}\t"
-                             f"{fmt.format(float(d)) if np.isfinite(d) else missing}\n")
+                fh.write("".join(f"{a}\t{b}\t{c}\n" for a, b, c in zip(ids, close, vals.tolist())))
         if self.pairs_fh is not None:
             self.pairs_fh.close()
         if self._pair_sets is not None:
