@@ -1017,12 +1017,21 @@ int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const Pa
         const int64_t tiles_x = (nx + PT - 1) / PT, tiles_y = (ny + PT - 1) / PT;
         if (tiles_x * tiles_y > ((int64_t)1 << 31) - 1) return fail(ctx, "pre-aligned tile grid too large");
         const int nwords = (std::max(X.max_len, Y.max_len) + 31) / 32;
-        if (ps.mode == PAIRS_TRI)
-            hipLaunchKernelGGL(k_prealigned_tile<PAIRS_TRI>, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0, st,
-                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out, tb);
-        else
-            hipLaunchKernelGGL(k_prealigned_tile<PAIRS_RECT>, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0, st,
-                               view(X), view(Y), ps, x0, nx, y0, ny, tiles_y, nwords, ms, d_out, tb);
+        bool gap = false;  // p-gaps (or anything but p / jc / k2p) reads the gap counter
+        for (int m = 0; m < ms.n; ++m) gap |= ms.code[m] != TAXI2_METRIC_P && ms.code[m] != TAXI2_METRIC_JC &&
+                                              ms.code[m] != TAXI2_METRIC_K2P;
+        const dim3 g((unsigned)(tiles_x * tiles_y)), b(256);
+        if (ps.mode == PAIRS_TRI) {
+            if (gap) hipLaunchKernelGGL((k_prealigned_tile<PAIRS_TRI, true>), g, b, 0, st, view(X), view(Y), ps, x0, nx, y0,
+                                        ny, tiles_y, nwords, ms, d_out, tb);
+            else hipLaunchKernelGGL((k_prealigned_tile<PAIRS_TRI, false>), g, b, 0, st, view(X), view(Y), ps, x0, nx, y0,
+                                    ny, tiles_y, nwords, ms, d_out, tb);
+        } else {
+            if (gap) hipLaunchKernelGGL((k_prealigned_tile<PAIRS_RECT, true>), g, b, 0, st, view(X), view(Y), ps, x0, nx,
+                                        y0, ny, tiles_y, nwords, ms, d_out, tb);
+            else hipLaunchKernelGGL((k_prealigned_tile<PAIRS_RECT, false>), g, b, 0, st, view(X), view(Y), ps, x0, nx,
+                                    y0, ny, tiles_y, nwords, ms, d_out, tb);
+        }
         HIP_TRY(ctx, hipGetLastError());
         return 0;
     }

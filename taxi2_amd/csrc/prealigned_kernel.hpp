@@ -101,8 +101,9 @@ __device__ __forceinline__ bool rowmin_less(double a, int64_t ya, double b, int6
 
 // Tile grid: x rows [x0, x0 + nx), y columns [y0, y0 + ny); tiles_y tiles per tile row.
 // MODE PAIRS_TRI: pair (a, b) exists for b > a, output slot tri(a, b) - ps.k0 when that lies in
-// [0, ps.count); PAIRS_RECT: output slot (a * ps.R + b) - ps.k0 (b indexes YS).
-template <int MODE>
+// [0, ps.count); PAIRS_RECT: output slot (a * ps.R + b) - ps.k0 (b indexes YS).  GAP: some metric
+// reads the gap counter (p-gaps); without it the gap popcount (4 of ~14 ops per pair-word) is skipped.
+template <int MODE, bool GAP>
 __global__ void __launch_bounds__(256)
 k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, int64_t y0, int64_t ny,
                   int64_t tiles_y, int nwords, MetricSpec ms, double* __restrict__ out, TileBlock tb) {
@@ -159,7 +160,7 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
                     c[i][j][0] += __popc(both);
                     c[i][j][1] += __popc(tsb);
                     c[i][j][2] += __popc(tvb);
-                    c[i][j][3] += __popc((a[i].w & b[j].z) | (b[j].w & a[i].z));
+                    if constexpr (GAP) c[i][j][3] += __popc((a[i].w & b[j].z) | (b[j].w & a[i].z));
                 }
         }
     }

@@ -242,10 +242,10 @@ class SubsetAggregatorDev:
     streamed row blocks in ascending order (taxi2_subset_aggregate_dev): the N x N values never
     exist on the host.  Same result as :func:`aggregate` over the full matrix, bit for bit."""
 
-    def __init__(self, eng, ids: list[str], partition, m: int):
+    def __init__(self, eng, ids: list[str], partition, m: int, codes: tuple | None = None):
         import torch
 
-        code, self.subsets = subset_codes(ids, partition)
+        code, self.subsets = codes if codes is not None else subset_codes(ids, partition)
         ns = len(self.subsets)
         dev = torch.device("cuda", eng.device)
         order = np.argsort(code, kind="stable")  # columns grouped by subset, ascending within one

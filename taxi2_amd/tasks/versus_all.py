@@ -433,6 +433,8 @@ class VersusAll:
                             D[a_h, b_h, kk] = dd[:, 0, q]
                             D[b_h, a_h, kk] = dd[:, 1, q]
                 rows_in()  # the previous block's rows, while this block aligns
+                stream.synchronize()  # the block's alignment (compute) ends here; its text starts
+                t0 = perf_counter()
                 # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
                 # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
                 # and (x, x) from the self alignments
@@ -454,8 +456,6 @@ class VersusAll:
                     py = torch.where(up, sy.data_ptr() + start0, py)
                     ln = torch.where(up, sl[:, 0][q], ln)
                 px, py, ln = px.contiguous(), py.contiguous(), ln.to(torch.int32).contiguous()
-                stream.synchronize()  # the alignment kernel counts as compute, not text
-                t0 = perf_counter()
                 fh.write(eng.format_pairs_ptr_dev(x1 - x0, n, px.data_ptr(), py.data_ptr(), ln.data_ptr(),
                                                   (ids[0], ids[1][x0:x1 + 1]), ids, first=x0 == 0,
                                                   stream=stream.cuda_stream))
@@ -1061,8 +1061,11 @@ class _BlockWriters:
         n = len(seqs)
         self.diag = None
         ex0 = list(seqs[0].extras.keys())
-        self.pre = ["\t".join([s.id, *[v if v is not None else self.missing for v in s.extras.values()]])
-                    for s in seqs]
+        # per-sequence text pieces only when a text writer needs them (N = 200 000: ~0.3 s of Python)
+        want_rows = files and bool(p.distances.write_linear or p.distances.write_matricial)
+        want_summary = files and bool(p.engine.write_summary)
+        self.pre = (["\t".join([s.id, *[v if v is not None else self.missing for v in s.extras.values()]])
+                     for s in seqs] if want_rows else None)
         self.lin = self.mats = None
         # duplicate ids: the reference's handlers merge consecutive lines of equal ids, and such a
         # run can span two row blocks -- the handler-shaped writers (kept open across blocks) and
@@ -1092,13 +1095,17 @@ class _BlockWriters:
         # summary.tsv (always)
         genera, species = task.input.genera, task.input.species
         self.genera, self.species = genera, species
-        gx = [genera.get(i, None) for i in self.ids] if genera else None
-        sx = [species.get(i, None) for i in self.ids] if species else None
-        ext = ["".join("\t" + (v if v is not None else self.missing) for v in s.extras.values()) for s in seqs]
-        gs = ["\t" + ((gx[k] if gx else None) or "-") + "\t" + ((sx[k] if sx else None) or "-") for k in range(n)]
-        self.suf = [t for pair in zip(ext, gs) for t in pair]
-        gcode = subset_codes(self.ids, genera)[0] if genera else np.zeros(n, np.int32)
-        scode = subset_codes(self.ids, species)[0] if species else np.zeros(n, np.int32)
+        self.suf = None
+        if want_summary:
+            gx = [genera.get(i, None) for i in self.ids] if genera else None
+            sx = [species.get(i, None) for i in self.ids] if species else None
+            ext = ["".join("\t" + (v if v is not None else self.missing) for v in s.extras.values()) for s in seqs]
+            gs = ["\t" + ((gx[k] if gx else None) or "-") + "\t" + ((sx[k] if sx else None) or "-") for k in range(n)]
+            self.suf = [t for pair in zip(ext, gs) for t in pair]
+        # subset codes once per partition (summary.tsv and the aggregators)
+        pcodes = {name: subset_codes(self.ids, part) for part, name in ((genera, "genera"), (species, "species")) if part}
+        gcode = pcodes["genera"][0] if genera else np.zeros(n, np.int32)
+        scode = pcodes["species"][0] if species else np.zeros(n, np.int32)
         self.codes = np.stack([gcode, scode], axis=1)
         self.summ = self.summ_runs = None
         if p.engine.write_summary and files:
@@ -1123,7 +1130,7 @@ class _BlockWriters:
             self.rmin_k = labels.index(str(p.engine.row_minima))
             self.rmin_idx = np.full(n, -1, dtype=np.int64)
             self.rmin_d = np.full(n, np.nan)
-        self.aggs = [(name, SubsetAggregatorDev(eng, self.ids, part, len(self.metrics)))
+        self.aggs = [(name, SubsetAggregatorDev(eng, self.ids, part, len(self.metrics), codes=pcodes[name]))
                      for part, name in ((genera, "genera"), (species, "species")) if part]
         self.pairs_fh = None
         self._pair_sets = None
