@@ -2256,8 +2256,9 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     // few subsets: natural-order rows (k_subset_rows_nat), ns x nch chunk slots per row
     const int64_t nch = std::max<int64_t>(1, (ncols + SUB_CH - 1) / SUB_CH);
     const bool nat = ns <= 4 && !getenv("TAXI2_SUB_GATHER");
-    // chunks of ~SUB_LANE_COLS columns or fewer on average: a lane walks each (k_subset_rows_lane)
-    const bool lane_rows = !nat && ncols <= (int64_t)ns * SUB_LANE_COLS && !getenv("TAXI2_SUB_WAVE");
+    // TAXI2_SUB_LANE=1: a lane walks each chunk (k_subset_rows_lane) -- measured slower than the
+    // wave form at config 5 (1.26 s vs 0.83 s for ~200-column species chunks), kept for A/B
+    const bool lane_rows = !nat && getenv("TAXI2_SUB_LANE") != nullptr;
     const int64_t tmax64 = nat ? (int64_t)ns * nch : (int64_t)ns + (ncols + SUB_CH - 1) / SUB_CH;
     if (tmax64 > INT32_MAX / 2) return fail(ctx, "taxi2_subset_aggregate_dev: too many subsets");
     const int tmax = (int)tmax64;

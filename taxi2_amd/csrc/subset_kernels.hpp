@@ -64,7 +64,6 @@ constexpr double SUB_TOP = 9007199254740991.0;  // 2^53 - 1: largest integer mul
 constexpr int SUB_MAX_ROWS = 8192;              // rows per k_subset_groups call (LDS sort)
 constexpr int SUB_CH = 2048;                    // columns per k_subset_rows wave (a subset's chunk)
 constexpr int SUB_FU = 8;                       // fixup: 64-value groups per iteration
-constexpr int SUB_LANE_COLS = 1024;             // mean subset size up to which a lane walks each chunk
 
 // The grid of running sum s: true with s in [2^(e-1), 2^e) when s is a positive normal number.
 __device__ __forceinline__ bool sub_grid(double s, int& e) {
