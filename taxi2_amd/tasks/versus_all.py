@@ -770,6 +770,7 @@ class VersusAll:
 
         t_prep = perf_counter()
         sink = _BlockWriters(self, seqs, eng, files=(rank == 0), walk=walk)
+        times["prepare_sink_s"] = perf_counter() - t_prep
         sink.diag = self._diag_info(seqs, eng, st, bool(p.pairs.align), scores, labels)
         # host-side phases outside the block loop: the set upload, the writers' and aggregators' set-up
         # with the diagonal rule's groups, and the close (subset statistics files, row_minima.tsv)
@@ -804,6 +805,7 @@ class VersusAll:
             for _, agg in sink.aggs:
                 agg.set_storage(inv, col_nat)
             sink.col_map = (order, inv, col_nat)
+        times["prepare_s"] = perf_counter() - t_prep  # + the column view
 
         def block(x0, x1):
             nonlocal pairs_text
