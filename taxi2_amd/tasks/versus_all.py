@@ -403,6 +403,7 @@ class VersusAll:
                         if x0 == 0 and "walker strings need" in str(e):
                             return False
                         raise
+                    rows_in()  # the previous block's rows into D while this block aligns
                     # pair (a, b) of the block: a in [x0, x1), b > a
                     ra = torch.repeat_interleave(torch.arange(x0, x1, device=dev), n - 1 - torch.arange(x0, x1, device=dev))
                     first = torch.cumsum(n - 1 - torch.arange(x0, x1, device=dev), 0) - (n - 1 - torch.arange(x0, x1, device=dev))
@@ -432,7 +433,7 @@ class VersusAll:
                         for q, kk in enumerate(cidx):
                             D[a_h, b_h, kk] = dd[:, 0, q]
                             D[b_h, a_h, kk] = dd[:, 1, q]
-                rows_in()  # the previous block's rows, while this block aligns
+                rows_in()  # (a block without pairs)
                 stream.synchronize()  # the block's alignment (compute) ends here; its text starts
                 t0 = perf_counter()
                 # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
