@@ -218,7 +218,9 @@ class VersusAll:
         align = bool(self.params.pairs.align)
         scores = Scores(**(self.params.pairs.scores or {})).as_tuple()
         n = len(seqs)
-        D = np.full((n, n, M), np.nan)
+        # every entry is written below (each path fills every ordered pair's row, the diagonal rule
+        # every (x, x)): no N^2 NaN fill up front -- the pages are touched as the rows arrive
+        D = np.empty((n, n, M))
         total = M * n * n
         if n == 0:
             return D
