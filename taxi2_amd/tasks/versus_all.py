@@ -332,7 +332,9 @@ class VersusAll:
         launch = int(self.params.engine.launch_pairs or 0)
         slot_budget = max(int(self.params.engine.block_bytes), WALK_BLOCK_BYTES if launch else 0)
         per_pair = 4 * cap + 16 * Mc + 8
-        target = max(1, min(launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
+        # a triangle block fills each pair once for both orientations: twice launch_pairs of them
+        # per launch (fewer launch tails and per-block host steps; the slots still fit slot_budget)
+        target = max(1, min(2 * launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
         stream = torch.cuda.Stream(dev)
         # the counter metrics land in a device copy of D (scattered on the GPU) unless that copy
         # would be large.  Rows [x0, x1) are complete once their block is scattered (the (r, c < r)
