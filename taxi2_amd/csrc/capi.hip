@@ -2269,7 +2269,8 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     const size_t o_part = 0, o_work = al((size_t)rsub * per_row * sizeof(SubPart));
     const size_t o_cpart = o_work + al((size_t)rsub * per_row * sizeof(SubWork));
     const size_t o_cofs = o_cpart + al((size_t)rsub * tmax * m * sizeof(SubPart));
-    const size_t o_ccode = o_cofs + al((size_t)(ns + 1) * 4);
+    const size_t o_t2b = o_cofs + al((size_t)(ns + 1) * 4);
+    const size_t o_ccode = o_t2b + al((size_t)tmax * 4);
     const size_t o_rows = o_ccode + al((size_t)(nat ? ncols : 0) + 1);
     const size_t o_code = o_rows + al((size_t)rsub * 4), o_start = o_code + al((size_t)rsub * 4);
     const size_t o_n = o_start + al((size_t)(rsub + 1) * 4), total = o_n + 256;
@@ -2285,6 +2286,7 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     int32_t* ngrp = (int32_t*)(base + o_n);
     unsigned int* wcount = (unsigned int*)(base + o_n + 64);
     uint8_t* ccode = (uint8_t*)(base + o_ccode);
+    int32_t* t2b = (int32_t*)(base + o_t2b);
     if (nat) {  // cofs[b] = b * nch, on the device (no host staging, no synchronisation)
         hipLaunchKernelGGL(k_subset_natcofs, dim3(1), dim3(64), 0, st, (int)ns, (int)nch, cofs);
         if (ncols > 0)
@@ -2292,6 +2294,8 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
                                d_col_idx, (int)ns, ncols, ccode);
     } else {
         hipLaunchKernelGGL(k_subset_cofs, dim3(1), dim3(1024), 0, st, d_col_start, (int)ns, cofs);
+        hipLaunchKernelGGL(k_subset_t2b, dim3((unsigned)((std::max<int64_t>(tmax, ns) + 255) / 256)), dim3(256), 0, st,
+                           (const int32_t*)cofs, (int)ns, tmax, t2b);
     }
     HIP_TRY(ctx, hipGetLastError());
     for (int64_t r0 = 0; r0 < nrows; r0 += rsub) {
@@ -2316,7 +2320,7 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
         } else {
             hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * tmax + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m,
                                rc, d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum,
-                               cpart);
+                               cpart, (const int32_t*)t2b);
         }
         HIP_TRY(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_subset_rowmerge, dim3((unsigned)((nr * per_row + 255) / 256)), dim3(256), 0, st, nr,

@@ -253,30 +253,35 @@ struct SubAcc {
     }
 };
 
+// chunk t -> its subset b (cofs[b] <= t < cofs[b + 1]), -1 past the last chunk: one load per wave
+// in k_subset_rows instead of a binary search of dependent loads.
+__global__ void __launch_bounds__(256) k_subset_t2b(const int32_t* __restrict__ cofs, int ns, int tmax,
+                                                    int32_t* __restrict__ t2b) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < tmax && i >= cofs[ns]) t2b[i] = -1;  // (every chunk below cofs[ns] has its subset)
+    if (i < ns)
+        for (int t = cofs[i]; t < cofs[i + 1]; ++t) t2b[t] = (int32_t)i;
+}
+
 // One wave per (block row x, chunk t of the row's chunks; tmax >= cofs[ns] bounds the grid), every
 // metric: up to SUB_MG metrics per pass over the chunk, each column's values read together (one
 // gather of m consecutive values per column instead of one per metric).  Chunk t belongs to subset
-// b with cofs[b] <= t < cofs[b + 1].
+// b = t2b[t].
 constexpr int SUB_MG = 4;
 __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ vals, int64_t nrows, int64_t ncols,
                                                      int m, const int32_t* __restrict__ row_code,
                                                      const int64_t* __restrict__ col_start,
                                                      const int32_t* __restrict__ col_idx, int ns,
                                                      const int32_t* __restrict__ cofs, int tmax,
-                                                     const double* __restrict__ sum, SubPart* __restrict__ part) {
+                                                     const double* __restrict__ sum, SubPart* __restrict__ part,
+                                                     const int32_t* __restrict__ t2b) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w >= nrows * tmax) return;
     const int64_t x = w / tmax;
     const int t = (int)(w - x * tmax);
-    if (t >= cofs[ns]) return;
-    int lo = 0, hi = ns;  // the last b with cofs[b] <= t
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (cofs[mid] <= t) lo = mid;
-        else hi = mid;
-    }
-    const int b = lo;
+    const int b = t2b[t];
+    if (b < 0) return;
     const int a = row_code[x];
     const int64_t j0 = col_start[b] + (int64_t)(t - cofs[b]) * SUB_CH;
     const int64_t j1 = min(col_start[b + 1], j0 + SUB_CH);
