@@ -850,12 +850,41 @@ class VersusAll:
             tick("compute_s", t)
             return D
 
+        # Reductions only on one rank (config 5): block b's reductions (row minima, subset partials --
+        # short latency-bound waves) run on a second stream while block b + 1's tile kernel runs;
+        # at most two blocks in flight.  The row minima stay on the device until the end.
+        overlap = (not walk and not p.pairs.align and not text and not sharded and rank == 0
+                   and not os.environ.get("TAXI2_NO_OVERLAP"))
+        red = torch.cuda.Stream(cuda) if overlap else None
+        red_done = []  # events: block b's reductions finished
+        if overlap and sink.rmin_k is not None:
+            sink.rmin_dev = (torch.full((n,), -1, dtype=torch.int64, device=cuda),
+                             torch.full((n,), float("nan"), dtype=torch.float64, device=cuda))
+        t_loop = perf_counter()
         try:
             for x0 in range(r0, r1, B):
                 x1 = min(r1, x0 + B)
                 fused[0] = None
+                if overlap and len(red_done) >= 2:
+                    red_done.pop(0).synchronize()  # block b - 2's D can be reused
                 D = block(x0, x1)
                 t = perf_counter()
+                if overlap:
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    red.wait_event(ev)
+                    with torch.cuda.stream(red):
+                        D.record_stream(red)
+                        for tt in fused[0] or ():
+                            tt.record_stream(red)
+                        sink.row_minima(x0, x1, D, fused[0])
+                        sink.aggregate(x0, x1, D)
+                        done = torch.cuda.Event()
+                        done.record(red)
+                        red_done.append(done)
+                    del D
+                    report(self.progress_handler, "distance.x.id", min(total, M * n * x1), total)
+                    continue
                 sink.row_minima(x0, x1, D, fused[0])
                 if not sharded:
                     sink.aggregate(x0, x1, D)
@@ -894,6 +923,14 @@ class VersusAll:
                     sink.rmin_idx[:] = allr[:, 0].astype(np.int64)
                     sink.rmin_d[:] = allr[:, 1]
                     tick("comm_s", t)
+            if overlap:
+                red.synchronize()
+                stream.synchronize()
+                # the loop's time not spent waiting for the tile kernels: reductions not hidden
+                times["reduce_s"] = max(0.0, perf_counter() - t_loop - times["compute_s"])
+                if sink.rmin_dev is not None:
+                    sink.rmin_idx[:] = sink.rmin_dev[0].cpu().numpy()
+                    sink.rmin_d[:] = sink.rmin_dev[1].cpu().numpy()
             if rank == 0:
                 t_cl = perf_counter()
                 sink.close()
@@ -1151,6 +1188,7 @@ class _BlockWriters:
         self.walk = walk
         self.torch = torch
         self.col_map = None  # (order, inverse, device order) when the blocks' columns are stored permuted
+        self.rmin_dev = None  # (index, value) device arrays of the row minima (overlapped reductions)
 
     def consume(self, x0: int, x1: int, D, scale: float) -> None:
         """D: (x1 - x0, n, M) device tensor of the rows' values, x100 applied, diagonal not yet."""
@@ -1203,8 +1241,13 @@ class _BlockWriters:
         torch = self.torch
         if self.rmin_k is not None and fused is not None:
             idx, val = fused
-            self.rmin_idx[x0:x1] = idx.cpu().numpy()
-            self.rmin_d[x0:x1] = val.cpu().numpy()
+            dev = self.rmin_dev is not None  # kept on the device (no host synchronisation per block)
+            if dev:
+                self.rmin_dev[0][x0:x1].copy_(idx)
+                self.rmin_dev[1][x0:x1].copy_(val)
+            else:
+                self.rmin_idx[x0:x1] = idx.cpu().numpy()
+                self.rmin_d[x0:x1] = val.cpu().numpy()
             lo, hi = np.searchsorted(self._special_rows, [x0, x1])
             rows = np.unique(self._special_rows[lo:hi])
             if rows.size:
@@ -1216,8 +1259,15 @@ class _BlockWriters:
                 d, ix = torch.min(v, dim=1)
                 ok = torch.isfinite(d)
                 d = torch.gather(v, 1, ix[:, None])[:, 0]  # the first minimum's own value (-0.0 / 0.0)
-                self.rmin_idx[rows] = torch.where(ok, ix, torch.full_like(ix, -1)).cpu().numpy()
-                self.rmin_d[rows] = torch.where(ok, d, torch.full_like(d, float("nan"))).cpu().numpy()
+                ri = torch.where(ok, ix, torch.full_like(ix, -1))
+                rv = torch.where(ok, d, torch.full_like(d, float("nan")))
+                if dev:
+                    rr_abs = torch.as_tensor(rows, device=D.device)
+                    self.rmin_dev[0][rr_abs] = ri
+                    self.rmin_dev[1][rr_abs] = rv
+                else:
+                    self.rmin_idx[rows] = ri.cpu().numpy()
+                    self.rmin_d[rows] = rv.cpu().numpy()
             return
         if self.rmin_k is not None:  # first minimum over defined values (-0.0 == 0.0), None skipped
             v = D[:, :, self.rmin_k]
