@@ -776,7 +776,9 @@ class VersusAll:
         t_prep = perf_counter()
         sink = _BlockWriters(self, seqs, eng, files=(rank == 0), walk=walk)
         times["prepare_sink_s"] = perf_counter() - t_prep
+        t_d = perf_counter()
         sink.diag = self._diag_info(seqs, eng, st, bool(p.pairs.align), scores, labels)
+        times["prepare_diag_s"] = perf_counter() - t_d
         # host-side phases outside the block loop: the set upload, the writers' and aggregators' set-up
         # with the diagonal rule's groups, and the close (subset statistics files, row_minima.tsv)
         times["upload_s"] = getattr(self, "_upload_s", 0.0)
@@ -935,6 +937,7 @@ class VersusAll:
                 t_cl = perf_counter()
                 sink.close()
                 times["finish_s"] = perf_counter() - t_cl
+                times["finish_subsets_s"] = sink.subsets_s
         finally:
             if cols_view is not None:
                 cols_view.free()  # before its parent set
@@ -1189,6 +1192,7 @@ class _BlockWriters:
         self.torch = torch
         self.col_map = None  # (order, inverse, device order) when the blocks' columns are stored permuted
         self.rmin_dev = None  # (index, value) device arrays of the row minima (overlapped reductions)
+        self.subsets_s = 0.0
 
     def consume(self, x0: int, x1: int, D, scale: float) -> None:
         """D: (x1 - x0, n, M) device tensor of the rows' values, x100 applied, diagonal not yet."""
@@ -1405,7 +1409,9 @@ class _BlockWriters:
             self._pair_sets = None
         p = self.task.params
         self.task.subset_stats = {}
+        t_sub = perf_counter()
         for name, agg in self.aggs:
             st = self.task.subset_stats[name] = agg.result()
             write_subset_statistics(self.task.paths.subsets / name, st, self.metrics, p.format.float,
                                     p.format.stats_template, eng=self.eng)
+        self.subsets_s = perf_counter() - t_sub
