@@ -97,13 +97,21 @@ def full_tuple_groups(seqs) -> list:
     """Indices of identical full tuples (seq_key), groups in first-appearance order.  Equal tuples
     have equal ids, so a sequence whose id occurs once is its own group without hashing its
     sequence (N = 200 000 x 1 000 bp: 0.5 s of string hashing otherwise)."""
+    import gc
     from collections import Counter
 
     ids = [s.id for s in seqs]
     cnt = Counter(ids)
-    if len(cnt) == len(ids):
-        return [[i] for i in range(len(ids))]
-    groups: dict = {}
-    for i, s in enumerate(seqs):
-        groups.setdefault(seq_key(s) if cnt[ids[i]] > 1 else (i,), []).append(i)
-    return list(groups.values())
+    # (N small lists: the cyclic collector would run several times over them while they are built)
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        if len(cnt) == len(ids):
+            return [[i] for i in range(len(ids))]
+        groups: dict = {}
+        for i, s in enumerate(seqs):
+            groups.setdefault(seq_key(s) if cnt[ids[i]] > 1 else (i,), []).append(i)
+        return list(groups.values())
+    finally:
+        if enabled:
+            gc.enable()

@@ -394,24 +394,31 @@ def _write_subset_statistics_native(path: Path, st: SubsetStats, metrics: list, 
     of Python string joins per partition otherwise."""
     from .._native import format_subset_stats
 
+    from concurrent.futures import ThreadPoolExecutor
+
     lin = Path(path) / "linear"
     mean, mn, mx, cnt = st.mean, st.min, st.max, st.count
+    simple = template == "{mean} ({min}-{max})"
+    # every file's body at once (the library call releases the GIL), then the writes in order
+    parts = [0, 1] + ([2 + k for k in range(len(metrics))] if simple else [])
+    with ThreadPoolExecutor(max_workers=len(parts)) as ex:
+        bodies = dict(zip(parts, ex.map(lambda q: format_subset_stats(mean, mn, mx, cnt, names, dec, q,
+                                                                      threads=12 if q == 0 else 4), parts)))
     with open(lin / "pairs.tsv", "wb") as fp:
-        body = format_subset_stats(mean, mn, mx, cnt, names, dec, 0)
+        body = bodies[0]
         if body:
             fp.write(("\t".join(("target", "query", *labels)) + "\n").encode())
             fp.write(body)
     with open(lin / "identity.tsv", "wb") as fi:
         fi.write(("\t".join(("target", *labels)) + "\n").encode())
-        fi.write(format_subset_stats(mean, mn, mx, cnt, names, dec, 1))
+        fi.write(bodies[1])
     mat = Path(path) / "matricial"
     create_parents(mat)
-    simple = template == "{mean} ({min}-{max})"
     for k, metric in enumerate(metrics):
         with open(mat / f"{metric}.tsv", "wb") as fh:
             fh.write(("\t".join(("", *names)) + "\n").encode())
             if simple:
-                fh.write(format_subset_stats(mean, mn, mx, cnt, names, dec, 2 + k))
+                fh.write(bodies[2 + k])
                 continue
             fmt = "{:.%df}" % dec
             for a in range(len(names)):
