@@ -154,11 +154,17 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+                    // c[1] counts all mismatches (ts + tv; ts = c[1] - c[2] in the epilogue).  Two
+                    // three-input v_bitop3 (truth tables symmetric in the outer operands):
+                    //   tvb  = both & (x.lo ^ y.lo)   (0x48: S1 & (S0 ^ S2))  -- a transversion
+                    //   mism = both & (tvb | dhi)     (0xc8: S1 & (S0 | S2))  -- any base bit differs
                     const uint32_t both = a[i].z & b[j].z;
-                    const uint32_t tvb = both & (a[i].x ^ b[j].x);           // lo bits differ: transversion
-                    const uint32_t tsb = (both ^ tvb) & (a[i].y ^ b[j].y);   // only the hi bit differs
+                    const uint32_t dhi = a[i].y ^ b[j].y;
+                    uint32_t tvb, mism;
+                    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x48" : "=v"(tvb) : "v"(a[i].x), "v"(both), "v"(b[j].x));
+                    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xc8" : "=v"(mism) : "v"(tvb), "v"(both), "v"(dhi));
                     c[i][j][0] += __popc(both);
-                    c[i][j][1] += __popc(tsb);
+                    c[i][j][1] += __popc(mism);
                     c[i][j][2] += __popc(tvb);
                     if constexpr (GAP) c[i][j][3] += __popc((a[i].w & b[j].z) | (b[j].w & a[i].z));
                 }
@@ -191,10 +197,11 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
             }
             ok = ok && slot >= 0 && slot < ps.count;
             const int64_t yn = tb.ynat ? (ok ? tb.ynat[y] : -1) : y;  // the task's column
+            const uint32_t ts = c[i][j][1] - c[i][j][2];
             const bool none = tb.diag && x == yn;
             for (int m = 0; m < nm; ++m) {
                 const double v = none ? __builtin_nan("")
-                                      : metric_value(ms.code[m], c[i][j][0], c[i][j][1], c[i][j][2], c[i][j][3]) * tb.scale;
+                                      : metric_value(ms.code[m], c[i][j][0], ts, c[i][j][2], c[i][j][3]) * tb.scale;
                 if (staged) stg[(tx * PT + ty + 16 * j) * nm + m] = v;
                 else if (ok) out[slot * nm + m] = v;
                 // the first (lowest task column) of equal values stays
