@@ -345,11 +345,13 @@ int taxi2_subset_aggregate(const double* d, int64_t n, int m, const int32_t* cod
  * exactly taxi2_subset_aggregate's (= the reference's x-major) sums.  d_col_nat (optional): the block's
  * columns are stored in another order (taxi2_rect_block_dev's column map) -- d_col_idx then holds
  * stored positions and d_col_nat[c] the task's column of stored column c, which orders ties of the
- * minimum (-0.0 against 0.0).  Asynchronous on `stream`. */
+ * minimum (-0.0 against 0.0).  d_scratch (optional, scratch_bytes; ~300 MB suffice): the call's working
+ * memory instead of the context's, so that two partitions can be aggregated concurrently on two
+ * streams.  Asynchronous on `stream`. */
 int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,
                                const int32_t* d_row_code, const int64_t* d_col_start, const int32_t* d_col_idx,
                                int32_t ns, int init, double* d_sum, double* d_min, double* d_max, int64_t* d_count,
-                               const int64_t* d_col_nat, void* stream);
+                               const int64_t* d_col_nat, void* d_scratch, int64_t scratch_bytes, void* stream);
 
 /* ---- Dereplicate's greedy walk (dereplicate.py:180-196 drop_*_pairs, 289-337 find_replicates,
  * 393-425 the lazily pulled chain that interleaves them) ------------------------------------ *

@@ -136,7 +136,7 @@ _SIGNATURES = {
     "taxi2_format_subset_stats": (_INT, [_I64, _INT, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _I64,
                                          ctypes.POINTER(_I64), _INT]),
     "taxi2_subset_aggregate_dev": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _I32, _INT, _P, _P, _P, _P, _P,
-                                          _P]),
+                                          _P, _I64, _P]),
     "taxi2_dereplicate_walk": (_INT, [_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, ctypes.POINTER(_I64), _P,
                                       _P, _I64, ctypes.POINTER(_I64), _P]),
 }
@@ -406,7 +406,8 @@ class Engine:
 
     def subset_aggregate_dev(self, vals_ptr: int, nrows: int, ncols: int, m: int, row_code_ptr: int,
                              col_start_ptr: int, col_idx_ptr: int, ns: int, init: bool, sum_ptr: int, min_ptr: int,
-                             max_ptr: int, count_ptr: int, stream: int | None = None, col_nat_ptr: int | None = None) -> None:
+                             max_ptr: int, count_ptr: int, stream: int | None = None, col_nat_ptr: int | None = None,
+                             scratch_ptr: int | None = None, scratch_bytes: int = 0) -> None:
         """taxi2_subset_aggregate_dev on device buffers (see taxi2_amd/streaming.py); ``col_nat_ptr``:
         the task column of each stored column when the block is stored permuted."""
         with self._lock:
@@ -416,6 +417,7 @@ class Engine:
                     ctypes.c_void_p(col_start_ptr), ctypes.c_void_p(col_idx_ptr), int(ns), 1 if init else 0,
                     ctypes.c_void_p(sum_ptr), ctypes.c_void_p(min_ptr), ctypes.c_void_p(max_ptr),
                     ctypes.c_void_p(count_ptr), ctypes.c_void_p(col_nat_ptr) if col_nat_ptr else None,
+                    ctypes.c_void_p(scratch_ptr) if scratch_ptr else None, int(scratch_bytes),
                     ctypes.c_void_p(stream) if stream else None,
                 ),
                 "taxi2_subset_aggregate_dev",

@@ -2233,7 +2233,7 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
 int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,
                                const int32_t* d_row_code, const int64_t* d_col_start, const int32_t* d_col_idx,
                                int32_t ns, int init, double* d_sum, double* d_min, double* d_max, int64_t* d_count,
-                               const int64_t* d_col_nat, void* stream) {
+                               const int64_t* d_col_nat, void* d_scratch, int64_t scratch_bytes, void* stream) {
     if (!ctx) return -1;
     if (nrows < 0 || ncols < 0 || m < 1 || ns < 0) return fail(ctx, "invalid sizes to taxi2_subset_aggregate_dev");
     const int64_t nk = (int64_t)ns * ns * m;
@@ -2274,8 +2274,16 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     const size_t o_rows = o_ccode + al((size_t)(nat ? ncols : 0) + 1);
     const size_t o_code = o_rows + al((size_t)rsub * 4), o_start = o_code + al((size_t)rsub * 4);
     const size_t o_n = o_start + al((size_t)(rsub + 1) * 4), total = o_n + 256;
-    if (ensure(ctx, &ctx->d_sub, &ctx->d_sub_bytes, total)) return -1;
-    char* base = (char*)ctx->d_sub;
+    char* base;
+    if (d_scratch) {  // the caller's scratch: aggregations of several partitions on several streams
+        if (scratch_bytes < (int64_t)total)
+            return fail(ctx, "taxi2_subset_aggregate_dev: scratch of %lld bytes, %lld needed", (long long)scratch_bytes,
+                        (long long)total);
+        base = (char*)d_scratch;
+    } else {
+        if (ensure(ctx, &ctx->d_sub, &ctx->d_sub_bytes, total)) return -1;
+        base = (char*)ctx->d_sub;
+    }
     SubPart* part = (SubPart*)(base + o_part);
     SubWork* work = (SubWork*)(base + o_work);
     SubPart* cpart = (SubPart*)(base + o_cpart);

@@ -257,6 +257,7 @@ class SubsetAggregatorDev:
         self.order = order  # the task's columns in subset order (ascending within a subset)
         self.col_idx = torch.as_tensor(order.astype(np.int32), dtype=torch.int32, device=dev)
         self.col_nat = None
+        self.scratch = None  # own working memory (use_own_scratch): concurrent aggregators
         shape = (ns, ns, m)
         self.sum = torch.zeros(shape, dtype=torch.float64, device=dev)
         self.min = torch.full(shape, float("inf"), dtype=torch.float64, device=dev)
@@ -271,6 +272,11 @@ class SubsetAggregatorDev:
         self.col_idx = self.torch.as_tensor(inv[self.order].astype(np.int32), dtype=self.torch.int32,
                                             device=self.col_idx.device)
         self.col_nat = nat
+
+    def use_own_scratch(self, nbytes: int = 384 << 20) -> None:
+        """Give this aggregator its own working memory, so that several can run on separate
+        streams at once (the library's default scratch is one per context)."""
+        self.scratch = self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.col_idx.device)
 
     def add(self, D, x0: int, x1: int) -> None:
         """D: (x1 - x0, n, m) float64 device tensor of the rows' adjusted values (NaN = None),
@@ -289,7 +295,9 @@ class SubsetAggregatorDev:
                                       self.col_start.data_ptr(), self.col_idx.data_ptr(), self.ns, False,
                                       self.sum.data_ptr(), self.min.data_ptr(), self.max.data_ptr(),
                                       self.count.data_ptr(), st,
-                                      col_nat_ptr=self.col_nat.data_ptr() if self.col_nat is not None else None)
+                                      col_nat_ptr=self.col_nat.data_ptr() if self.col_nat is not None else None,
+                                      scratch_ptr=self.scratch.data_ptr() if self.scratch is not None else None,
+                                      scratch_bytes=self.scratch.numel() if self.scratch is not None else 0)
         if side is not None:
             cur.wait_stream(side)
 

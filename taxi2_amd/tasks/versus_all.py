@@ -857,8 +857,14 @@ class VersusAll:
         # at most two blocks in flight.  The row minima stay on the device until the end.
         overlap = (not walk and not p.pairs.align and not text and not sharded and rank == 0
                    and not os.environ.get("TAXI2_NO_OVERLAP"))
-        red = torch.cuda.Stream(cuda) if overlap else None
-        red_done = []  # events: block b's reductions finished
+        # one reduction stream per partition (each aggregator with its own scratch): genus and
+        # species partials of a block run side by side
+        reds = [torch.cuda.Stream(cuda) for _ in range(max(1, len(sink.aggs)))] if overlap else []
+        red = reds[0] if overlap else None
+        if overlap and len(sink.aggs) > 1:
+            for _, agg in sink.aggs:
+                agg.use_own_scratch()
+        red_done = []  # per block: events of its reductions (one per stream)
         if overlap and sink.rmin_k is not None:
             sink.rmin_dev = (torch.full((n,), -1, dtype=torch.int64, device=cuda),
                              torch.full((n,), float("nan"), dtype=torch.float64, device=cuda))
@@ -868,22 +874,28 @@ class VersusAll:
                 x1 = min(r1, x0 + B)
                 fused[0] = None
                 if overlap and len(red_done) >= 2:
-                    red_done.pop(0).synchronize()  # block b - 2's D can be reused
+                    for e in red_done.pop(0):  # block b - 2's D can be reused
+                        e.synchronize()
                 D = block(x0, x1)
                 t = perf_counter()
                 if overlap:
                     ev = torch.cuda.Event()
                     ev.record(stream)
-                    red.wait_event(ev)
-                    with torch.cuda.stream(red):
-                        D.record_stream(red)
-                        for tt in fused[0] or ():
-                            tt.record_stream(red)
-                        sink.row_minima(x0, x1, D, fused[0])
-                        sink.aggregate(x0, x1, D)
-                        done = torch.cuda.Event()
-                        done.record(red)
-                        red_done.append(done)
+                    dones = []
+                    for k, rs in enumerate(reds):
+                        rs.wait_event(ev)
+                        with torch.cuda.stream(rs):
+                            D.record_stream(rs)
+                            if k == 0:
+                                for tt in fused[0] or ():
+                                    tt.record_stream(rs)
+                                sink.row_minima(x0, x1, D, fused[0])
+                            if k < len(sink.aggs):
+                                sink.aggs[k][1].add(D, x0, x1)
+                            done = torch.cuda.Event()
+                            done.record(rs)
+                            dones.append(done)
+                    red_done.append(dones)
                     del D
                     report(self.progress_handler, "distance.x.id", min(total, M * n * x1), total)
                     continue
@@ -926,7 +938,8 @@ class VersusAll:
                     sink.rmin_d[:] = allr[:, 1]
                     tick("comm_s", t)
             if overlap:
-                red.synchronize()
+                for rs in reds:
+                    rs.synchronize()
                 stream.synchronize()
                 # the loop's time not spent waiting for the tile kernels: reductions not hidden
                 times["reduce_s"] = max(0.0, perf_counter() - t_loop - times["compute_s"])
