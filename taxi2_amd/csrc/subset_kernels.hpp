@@ -94,25 +94,41 @@ __global__ void __launch_bounds__(1024) k_subset_groups(const int32_t* __restric
                                                         int32_t* __restrict__ grp_rows, int32_t* __restrict__ grp_code,
                                                         int32_t* __restrict__ grp_start, int32_t* __restrict__ ngrp) {
     __shared__ unsigned long long keys[SUB_MAX_ROWS];
-    int P = 1;
-    while (P < nrows) P <<= 1;
-    for (int i = threadIdx.x; i < P; i += blockDim.x)
-        keys[i] = i < nrows ? ((unsigned long long)(uint32_t)row_code[i] << 32) | (uint32_t)i : ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const unsigned long long a = keys[i], b = keys[l];
-                    if (((i & k) == 0) == (a > b)) {
-                        keys[i] = b;
-                        keys[l] = a;
+    if (nrows <= (int)blockDim.x) {
+        // few rows (a config-5 block holds ~450): each row's rank among the (code, row) keys by
+        // counting, one pass and two barriers instead of the sort's log^2 barrier stages
+        __shared__ uint32_t rc[1024];
+        if ((int)threadIdx.x < nrows) rc[threadIdx.x] = (uint32_t)row_code[threadIdx.x];
+        for (int i = threadIdx.x; i < SUB_MAX_ROWS; i += blockDim.x) keys[i] = ~0ull;
+        __syncthreads();
+        if ((int)threadIdx.x < nrows) {
+            const uint32_t c = rc[threadIdx.x];
+            int rank = 0;
+            for (int j = 0; j < nrows; ++j) rank += rc[j] < c || (rc[j] == c && j < (int)threadIdx.x);
+            keys[rank] = ((unsigned long long)c << 32) | (uint32_t)threadIdx.x;
+        }
+        __syncthreads();
+    } else {
+        int P = 1;
+        while (P < nrows) P <<= 1;
+        for (int i = threadIdx.x; i < P; i += blockDim.x)
+            keys[i] = i < nrows ? ((unsigned long long)(uint32_t)row_code[i] << 32) | (uint32_t)i : ~0ull;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const unsigned long long a = keys[i], b = keys[l];
+                        if (((i & k) == 0) == (a > b)) {
+                            keys[i] = b;
+                            keys[l] = a;
+                        }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
-        }
+    }
     // group index of a boundary = boundaries before it: each thread counts its SUB_MAX_ROWS / 1024
     // consecutive positions, then a scan over the threads' counts (Hillis-Steele in LDS)
     __shared__ int part[1024];
