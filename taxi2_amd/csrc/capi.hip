@@ -2256,9 +2256,6 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     // few subsets: natural-order rows (k_subset_rows_nat), ns x nch chunk slots per row
     const int64_t nch = std::max<int64_t>(1, (ncols + SUB_CH - 1) / SUB_CH);
     const bool nat = ns <= 4 && !getenv("TAXI2_SUB_GATHER");
-    // TAXI2_SUB_LANE=1: a lane walks each chunk (k_subset_rows_lane) -- measured slower than the
-    // wave form at config 5 (1.26 s vs 0.83 s for ~200-column species chunks), kept for A/B
-    const bool lane_rows = !nat && getenv("TAXI2_SUB_LANE") != nullptr;
     const int64_t tmax64 = nat ? (int64_t)ns * nch : (int64_t)ns + (ncols + SUB_CH - 1) / SUB_CH;
     if (tmax64 > INT32_MAX / 2) return fail(ctx, "taxi2_subset_aggregate_dev: too many subsets");
     const int tmax = (int)tmax64;
@@ -2320,11 +2317,6 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
             else
                 hipLaunchKernelGGL(k_subset_rows_nat<4>, g, b, 0, st, v, nr, ncols, m, rc, (const uint8_t*)ccode, (int)ns,
                                    (int)nch, (const double*)d_sum, cpart, d_col_nat);
-        } else if (lane_rows) {  // many small subsets: a lane per chunk
-            const int64_t groups = (tmax + 63) / 64;
-            hipLaunchKernelGGL(k_subset_rows_lane, dim3((unsigned)((nr * groups + 3) / 4)), dim3(256), 0, st, v, nr, ncols,
-                               m, rc, d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum,
-                               cpart);
         } else {
             hipLaunchKernelGGL(k_subset_rows, dim3((unsigned)((nr * tmax + 3) / 4)), dim3(256), 0, st, v, nr, ncols, m,
                                rc, d_col_start, d_col_idx, (int)ns, (const int32_t*)cofs, tmax, (const double*)d_sum,

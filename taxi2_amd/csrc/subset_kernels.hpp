@@ -229,18 +229,6 @@ struct SubAcc {
             }
         }
     }
-    // this lane's partial as it stands (one lane walked the whole chunk)
-    __device__ __forceinline__ SubPart part() const {
-        SubPart P;
-#pragma unroll
-        for (int q = 0; q < SUB_J; ++q) P.rsum[q] = rs[q];
-        P.mn = mn;
-        P.mx = mx;
-        P.cnt = c;
-        P.flags = fl;
-        P.mnp = (int32_t)min(mnp, (long long)INT32_MAX);
-        return P;
-    }
     // the wave's lanes merged; lane 0 holds the partial
     __device__ __forceinline__ SubPart reduce() {
         for (int o = 32; o > 0; o >>= 1) {
@@ -326,50 +314,6 @@ __global__ void __launch_bounds__(256) k_subset_rows(const double* __restrict__ 
 // cofs[b] = b * nch (k_subset_rows_nat's chunk slots: ns subsets x nch chunks per row).
 __global__ void k_subset_natcofs(int ns, int nch, int32_t* __restrict__ cofs) {
     for (int b = threadIdx.x; b <= ns; b += blockDim.x) cofs[b] = b * nch;
-}
-
-// Many small subsets: one LANE per (block row x, chunk t), the chunk's columns walked in order by
-// that lane alone -- no cross-lane reduction per chunk (the wave form above spends most of a ~200-
-// column species chunk on its shuffles), a wave covers 64 consecutive chunks of one row.
-__global__ void __launch_bounds__(256) k_subset_rows_lane(const double* __restrict__ vals, int64_t nrows,
-                                                          int64_t ncols, int m, const int32_t* __restrict__ row_code,
-                                                          const int64_t* __restrict__ col_start,
-                                                          const int32_t* __restrict__ col_idx, int ns,
-                                                          const int32_t* __restrict__ cofs, int tmax,
-                                                          const double* __restrict__ sum, SubPart* __restrict__ part) {
-    const int64_t groups = (tmax + 63) / 64;
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w >= nrows * groups) return;
-    const int64_t x = w / groups;
-    const int t = (int)(w - x * groups) * 64 + (threadIdx.x & 63);
-    if (t >= cofs[ns]) return;
-    int lo = 0, hi = ns;  // the last b with cofs[b] <= t
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (cofs[mid] <= t) lo = mid;
-        else hi = mid;
-    }
-    const int b = lo;
-    const int a = row_code[x];
-    const int64_t j0 = col_start[b] + (int64_t)(t - cofs[b]) * SUB_CH;
-    const int64_t j1 = min(col_start[b + 1], j0 + SUB_CH);
-    const double* row = vals + x * ncols * m;
-    for (int k0 = 0; k0 < m; k0 += SUB_MG) {
-        const int g = min(SUB_MG, m - k0);
-        SubAcc acc[SUB_MG];
-#pragma unroll
-        for (int q = 0; q < SUB_MG; ++q)
-            if (q < g) acc[q].init(sum[((int64_t)a * ns + b) * m + k0 + q]);
-        for (int64_t j = j0; j < j1; ++j) {
-            const double* vp = row + (int64_t)col_idx[j] * m + k0;
-#pragma unroll
-            for (int q = 0; q < SUB_MG; ++q)
-                if (q < g) acc[q].add(vp[q], j);
-        }
-#pragma unroll
-        for (int q = 0; q < SUB_MG; ++q)
-            if (q < g) part[(x * tmax + t) * m + k0 + q] = acc[q].part();
-    }
 }
 
 // Column codes from the sorted layout: code[col_idx[j]] = b for j in [col_start[b], col_start[b+1]).
