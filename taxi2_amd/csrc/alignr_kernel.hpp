@@ -413,10 +413,17 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 int n = 0, rows = 0;
                 while (n == 0) {
                     if (s_qc >= s_qend) {
-                        const int64_t q0 = (int64_t)atomicAdd(next, (unsigned long long)chunk);
+                        // guided: shorter chains once fewer than two rounds of full ones are left, so
+                        // that the workgroups finish closer together (the launch's tail)
+                        int64_t c = chunk;
+                        const int64_t left =
+                            total - (int64_t)__hip_atomic_load(next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (left < (int64_t)gridDim.x * chunk * 2) c = max((int64_t)1, chunk / 2);
+                        if (left < (int64_t)gridDim.x * chunk) c = max((int64_t)1, chunk / 4);
+                        const int64_t q0 = (int64_t)atomicAdd(next, (unsigned long long)c);
                         if (q0 >= total) break;
                         s_qc = q0;
-                        s_qend = min(q0 + chunk, total);
+                        s_qend = min(q0 + c, total);
                         // segment of unit q0 (binary search; units run in segment order)
                         int lo = 0, hi = nseg - 1;
                         while (lo < hi) {
