@@ -51,11 +51,96 @@ def b_pair(L: int, M: int) -> int:
     return 2 * math.ceil(L / 4) + 8 * M
 
 
-def step_block(step: int, rank: int, world: int, batch: int, total_pairs: int) -> int:
-    """First pair of the block rank `rank` runs at `step`: consecutive steps and ranks take
-    consecutive, disjoint blocks of the config-3 pair space (weak scaling: `batch` pairs per rank
-    and step), wrapping before the end of the space."""
-    return ((step * world + rank) * batch) % (total_pairs - batch)
+def step_block(step: int, rank: int, world: int, batch: int, total_pairs: int, nsteps: int = 1) -> int:
+    """First pair of the block rank `rank` runs at timed step `step` (0 .. nsteps - 1; warmup steps
+    reuse them): the nsteps x world blocks (weak scaling: `batch` pairs per rank and step) are spread
+    evenly over the whole config-3 triangle, first pair to last, so that the timed steps sample its
+    long rows (the start) and its short ones (the end, where the row-shared aligner's units pair
+    fewer rows) alike -- versus_all.py:746-769 aligns every pair of the space."""
+    T = nsteps * world
+    i = (step % max(1, nsteps)) * world + rank
+    return 0 if T <= 1 else (i * (total_pairs - batch)) // (T - 1)
+
+
+class StepPipeline:
+    """The bench's steps with N > 1's all-gather of each step's result block (north_star: RCCL
+    all-gather of distance-matrix row blocks over xGMI) on a stream of its own, ordered after the
+    step's kernel by an event, so that step k's gather overlaps step k + 1's kernel (double-buffered
+    results: step k + 1 writes the other slot; step k + 2 waits for step k's gather before it
+    rewrites slot k % 2).  Kernel and gather times are measured separately with events on their own
+    streams (report gather time separately from kernel time).  On CPU (gloo, the
+    tests) the same code runs with no streams and wall-clock timing."""
+
+    def __init__(self, world: int, batch: int, m: int, device):
+        import torch
+
+        self.world, self.device = world, device
+        self.cuda = device.type == "cuda"
+        self.gstream = torch.cuda.Stream(device) if self.cuda and world > 1 else None
+        self.gathered = (torch.empty((world * batch, 2, m), dtype=torch.float64, device=device)
+                         if world > 1 else None)
+        self.done = [None, None]  # per slot: the event after its last gather
+        self.kev, self.gev = [], []
+
+    def _event(self):
+        import torch
+
+        return torch.cuda.Event(enable_timing=True) if self.cuda else time.perf_counter
+
+    def _mark(self, stream):
+        if self.cuda:
+            import torch
+
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            return e
+        return time.perf_counter()
+
+    @staticmethod
+    def _ms(a, b) -> float:
+        return a.elapsed_time(b) if not isinstance(a, float) else (b - a) * 1e3
+
+    def step(self, k: int, kernel, out: list, stream, record: bool) -> None:
+        import torch.distributed as dist
+
+        slot = k % 2
+        if self.cuda and self.done[slot] is not None:
+            stream.wait_event(self.done[slot])  # the gather of step k - 2 has read this slot
+        e0 = self._mark(stream)
+        kernel(k, slot)
+        e1 = self._mark(stream)
+        if record:
+            self.kev.append((e0, e1))
+        if self.world <= 1:
+            return
+        if self.cuda:
+            import torch
+
+            self.gstream.wait_event(e1)
+            with torch.cuda.stream(self.gstream):
+                g0 = self._mark(self.gstream)
+                dist.all_gather_into_tensor(self.gathered, out[slot])
+                g1 = self._mark(self.gstream)
+            self.done[slot] = g1
+        else:
+            g0 = self._mark(None)
+            dist.all_gather_into_tensor(self.gathered, out[slot])
+            g1 = self._mark(None)
+        if record:
+            self.gev.append((g0, g1))
+
+    def drain(self) -> None:
+        if self.cuda and self.gstream is not None:
+            import torch
+
+            torch.cuda.current_stream(self.device).wait_stream(self.gstream)
+            self.gstream.synchronize()
+
+    def kernel_ms(self) -> float:
+        return float(np.mean([self._ms(a, b) for a, b in self.kev])) if self.kev else float("nan")
+
+    def gather_ms(self) -> float | None:
+        return float(np.mean([self._ms(a, b) for a, b in self.gev])) if self.gev else None
 
 
 def max_over_ranks(elapsed: float, world: int, device=None) -> float:
@@ -88,7 +173,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores (max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    ap.add_argument("--secondary", default="allmetrics,config4,task,config5",
+    ap.add_argument("--secondary", default="allmetrics,config4,task,config5,config5_aligned",
                     help="secondary legs after the headline (one GPU only; bench_secondary.py); '' = none")
     return ap.parse_args()
 
@@ -118,46 +203,36 @@ def main() -> None:
     total_pairs = N_SEQS * (N_SEQS - 1) // 2
     B = int(args.batch)
     M = len(METRICS)
-    out = torch.empty((B, 2, M), dtype=torch.float64, device="cuda")
+    # two result slots: step k's kernel writes slot k % 2 while step k - 1's all-gather (N > 1) still
+    # reads the other one on the gather stream
+    out = [torch.empty((B, 2, M), dtype=torch.float64, device="cuda") for _ in range(2)]
     scores = torch.empty((B,), dtype=torch.int32, device="cuda")
-    gathered = torch.empty((world * B, 2, M), dtype=torch.float64, device="cuda") if world > 1 else None
     stream = torch.cuda.Stream()  # a real stream handle: the kernel and its HIP events share it
     torch.cuda.set_stream(stream)
+    pipe = StepPipeline(world, B, M, torch.device("cuda", local))
 
-    def block(step: int) -> int:
-        return step_block(step, rank, world, B, total_pairs)
-
-    ev = []
-
-    def run_step(step: int, record: bool) -> None:
-        if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        eng.all_pairs_dev(seqset, block(step), B, METRICS, out.data_ptr(), None, scores.data_ptr(),
-                          stream.cuda_stream)
-        if record:
-            e1.record(stream)
-            ev.append((e0, e1))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+    def kernel(step: int, slot: int) -> None:
+        eng.all_pairs_dev(seqset, step_block(step, rank, world, B, total_pairs, args.steps), B, METRICS,
+                          out[slot].data_ptr(), None, scores.data_ptr(), stream.cuda_stream)
 
     for w in range(args.warmup):
-        run_step(w, False)
+        pipe.step(w, kernel, out, stream, record=False)
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        run_step(args.warmup + s, True)
+        pipe.step(s, kernel, out, stream, record=True)
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, "cuda")
 
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
+    kern_ms, gather_ms = pipe.kernel_ms(), pipe.gather_ms()
     value = job_value(args.steps, B, world, elapsed)
     bp = b_pair(SEQ_LEN, M)
     achieved_gbs = B * bp / (kern_ms * 1e-3) / 1e9
@@ -213,7 +288,11 @@ def main() -> None:
                 "pairs_per_step_per_gpu": B,
                 "pair_space": total_pairs,
                 "parallelism": f"pair-space shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                "blocks": f"{args.steps} x {world} blocks spread evenly over the whole triangle (first to last pair)",
             },
+            "kernel_ms": kern_ms,
+            "gather_ms": gather_ms,
+            "full_job_eta_s": total_pairs / value,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved_gbs,

@@ -12,12 +12,14 @@ into the same record (bench.py's ``secondary`` key), each on its own synthetic, 
 * ``config5``: VersusAll.start() on 200 000 x 1 000 pre-aligned rows (BASELINE.json configs[4], one
   GPU), p / jc / k2p x100, reductions only (row minima + 2-genus / ~1 000-species subset statistics):
   every one of the 4e10 ordered pairs evaluated and reduced on the GPU.
+* ``config5_aligned``: config 5's aligned form on a stated subset (N = 12 000 of its generator):
+  VersusAll.start() with Gotoh alignment of every pair, four metrics x100, streamed reductions.
 * ``config4``: versusReference slice, 4 096 queries x 10 000 references of 650 bp (seed 0x7A13
   generator), Gotoh align + p, closest reference + extras on the GPU (versus_reference.py:184-188,
   124-129).
 * ``allmetrics``: config 3 with ALL metrics (BASELINE.json configs[2], "+ncd"): p / p-gaps / jc / k2p
-  from the aligner and NCD of the aligned strings (distances.py:351-358, three zlib streams per
-  ordered pair) on a block of config-3 pairs.
+  and NCD of the same alignment's strings (distances.py:351-358) from one fill per pair, on a block
+  of config-3 pairs, split into the fill and the strings + deflate part.
 
 Every leg prints a progress line to stderr and returns a dict (or {"error": ...}: a failing leg never
 takes the headline line with it).
@@ -69,11 +71,11 @@ def build_config5_task(n: int, L: int, eng, out: Path, block_gb: float, aligned:
     from taxi2_amd.sequences import Sequence, Sequences
     from taxi2_amd.tasks import VersusAll
 
-    if aligned:  # the config-3 generator: Gotoh alignment of every pair
+    if aligned:  # config 5's generator (seed 0x7A14) with indels: Gotoh alignment of every pair
         from taxi2_amd.synth import family_sequences
 
         buf = offs = None
-        seqs = [Sequence(f"s{k}", s) for k, s in enumerate(family_sequences(n, L, 0x7A12))]
+        seqs = [Sequence(f"s{k}", s) for k, s in enumerate(family_sequences(n, L, 0x7A14))]
     else:
         buf, offs = prealigned_rows(n, L, 0x7A14)
         raw = buf[:-1].reshape(n, L)
@@ -157,6 +159,36 @@ def leg_config5(eng, n: int = 200_000, L: int = 1000) -> dict:
     }
 
 
+def leg_config5_aligned(eng, n: int = 12_000, L: int = 1000) -> dict:
+    """Config 5's aligned (NW / Gotoh) form on a stated subset ("Run NW on a stated
+    tile subset"): VersusAll.start() on N = 12 000 sequences of the config-5 generator (seed 0x7A14,
+    1 000 bp, with indels), Gotoh align + p / p-gaps / jc / k2p x100, the streamed path's reductions
+    (row minima + 2-genus / ~1 000-species subset statistics), no N x N text -- 1.44e8 ordered pairs,
+    0.36 % of the full 200 000 job, which extrapolates linearly in pairs (the triangle store and the
+    block assembly are per pair)."""
+    import torch
+
+    _log(f"config5_aligned: VersusAll.start() N = {n} x {L} bp, align + 4 metrics, reductions only")
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as tmp:
+        task, _, _ = build_config5_task(n, L, eng, Path(tmp), 2.0, aligned=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = task.start()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    pairs = n * (n - 1) // 2
+    full = 200_000 * 199_999 // 2
+    return {
+        "workload": f"config5 aligned subset: VersusAll.start() on {n} x {L} bp config-5-generator sequences "
+                    f"(seed 0x7A14), Gotoh align + p/p-gaps/jc/k2p x100, row minima + 2-genus / ~1 000-species "
+                    f"subset statistics (streamed reductions, no N x N text), one GPU",
+        "n_seqs": n, "unordered_pairs": pairs, "seconds_taken": res.seconds_taken, "wall_s": wall,
+        "unordered_pairs_per_s": pairs / wall, "phases_s": task.timings,
+        "full_job_200k_hours_1gpu": full / (pairs / wall) / 3600,
+        "full_job_200k_minutes_8gpu": full / (pairs / wall) / 8 / 60,
+    }
+
+
 def leg_config4(eng, q_slice: int = 4096, R: int = 10_000, L: int = 650) -> dict:
     from taxi2_amd.synth import family_sequences
 
@@ -183,34 +215,72 @@ def leg_config4(eng, q_slice: int = 4096, R: int = 10_000, L: int = 650) -> dict
     }
 
 
-def leg_allmetrics(eng, seqset, n_seqs: int, count: int = 1 << 15) -> dict:
-    """p / p-gaps / jc / k2p from the aligner + NCD of the aligned strings for `count` config-3
-    pairs (both orientations), as VersusAll computes them."""
+def leg_allmetrics(eng, seqset, n_seqs: int, count: int = 1 << 17) -> dict:
+    """p / p-gaps / jc / k2p AND NCD for `count` config-3 pairs (both orientations) from ONE fill per
+    pair, as VersusAll computes them (versus_all.py:546-552: one alignment per ordered pair feeds every
+    metric): taxi2_all_pairs_dev with the five metrics -- the walkers write both orientations' aligned
+    strings into HBM slots, NCD deflates them there (distances.py:351-358).  Timed with HIP events on
+    the launch stream, outputs resident in HBM; the four-metric launch of the same block beside it
+    splits the time into the fill and the strings + deflate part."""
     import torch
 
     from taxi2_amd._native import tri_pairs
 
-    _log(f"allmetrics: {count} config-3 pairs, p/p-gaps/jc/k2p + ncd")
-    metrics = ("p", "p-gaps", "jc", "k2p")
+    _log(f"allmetrics: {count} config-3 pairs, p/p-gaps/jc/k2p + ncd, one fill per pair")
+    four, five = ("p", "p-gaps", "jc", "k2p"), ("p", "p-gaps", "jc", "k2p", "ncd")
     k0 = 1 << 20  # a block the headline's first steps do not time
-    a, b = tri_pairs(n_seqs, k0, count)
-    eng.ncd_pairs(seqset, seqset, a[:256], b[:256], aligned=True, both=True)  # warm
-    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()
+    out = torch.empty((count, 2, 5), dtype=torch.float64, device="cuda")
+
+    def timed(metrics, n) -> float:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        eng.all_pairs_dev(seqset, k0, n, metrics, out.data_ptr(), None, None, stream.cuda_stream)
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e-3
+
+    timed(five, 4096)  # warm: scratch, LDS attributes
     t0 = time.perf_counter()
-    four = eng.all_pairs(seqset, k0, count, metrics)
-    t1 = time.perf_counter()
-    ncd = eng.ncd_pairs(seqset, seqset, a, b, aligned=True, both=True)
-    t2 = time.perf_counter()
+    t_all = timed(five, count)
+    wall = time.perf_counter() - t0
+    vals = out.cpu().numpy()
+    t_four = timed(four, count)
+    # deflate input of the block, from a sample of the same pairs' strings (tri_strings_dev): per pair
+    # C(x0), C(y0), C(x0 + y0), C(y1 + x1), and C(y1), C(x1) only when the (b, a) alignment differs
+    S = min(count, 8192)
+    cap = 2 * 1000 + 1
+    sx = torch.empty((S, 2, cap), dtype=torch.uint8, device="cuda")
+    sy = torch.empty((S, 2, cap), dtype=torch.uint8, device="cuda")
+    sl = torch.empty((S, 2), dtype=torch.int32, device="cuda")
+    eng.tri_strings_dev(seqset, k0, S, (), None, cap, sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), None,
+                        stream.cuda_stream)
+    stream.synchronize()
+    a, b = tri_pairs(n_seqs, k0, S)
+    hx, hy, hl = sx.cpu().numpy(), sy.cpu().numpy(), sl.cpu().numpy()
+    end = 2000  # 1 000 bp each
+    dup = 0
+    nbytes = 0
+    for k in range(S):
+        L0, L1 = int(hl[k, 0]), int(hl[k, 1])
+        same = L0 == L1 and np.array_equal(hx[k, 0, end - L0:end], hx[k, 1, end - L1:end]) and \
+            np.array_equal(hy[k, 0, end - L0:end], hy[k, 1, end - L1:end])
+        dup += same
+        nbytes += 4 * L0 + 2 * L1 + (0 if same else 2 * L1)
+    deflate_bytes = nbytes * count / S
     return {
-        "workload": f"config3 all metrics: {count} config-3 pairs (1 000 bp), Gotoh align + p/p-gaps/jc/k2p + NCD of "
-                    f"the aligned strings, both ordered pairs",
-        "pairs": count, "seconds": t2 - t0, "pairs_per_s": count / (t2 - t0),
-        "four_metric_s": t1 - t0, "ncd_s": t2 - t1, "ncd_share": (t2 - t1) / (t2 - t0),
-        "finite": bool(np.isfinite(four).all() and np.isfinite(ncd).all()),
+        "workload": f"config3 all metrics: {count} config-3 pairs (1 000 bp) from pair {k0}, Gotoh align + "
+                    f"p/p-gaps/jc/k2p + NCD of the same alignment's strings, both ordered pairs, one fill per "
+                    f"pair (taxi2_all_pairs_dev), outputs in HBM",
+        "pairs": count, "seconds": t_all, "wall_s": wall, "pairs_per_s": count / t_all,
+        "four_metric_s": t_four, "strings_and_ncd_s": t_all - t_four, "ncd_share": (t_all - t_four) / t_all,
+        "deflate_input_bytes": deflate_bytes, "deflate_input_gb_per_s": deflate_bytes / (t_all - t_four) / 1e9,
+        "same_alignment_both_orders": dup / S,
+        "finite": bool(np.isfinite(vals).all()),
     }
 
 
-def run_all(eng, seqset, n_seqs: int, legs=("allmetrics", "config4", "task", "config5")) -> dict:
+def run_all(eng, seqset, n_seqs: int, legs=("allmetrics", "config4", "task", "config5", "config5_aligned")) -> dict:
     out = {}
     for name in legs:
         t0 = time.perf_counter()
@@ -219,6 +289,8 @@ def run_all(eng, seqset, n_seqs: int, legs=("allmetrics", "config4", "task", "co
                 out[name] = leg_task(eng)
             elif name == "config5":
                 out[name] = leg_config5(eng)
+            elif name == "config5_aligned":
+                out[name] = leg_config5_aligned(eng)
             elif name == "config4":
                 out[name] = leg_config4(eng)
             elif name == "allmetrics":

@@ -51,7 +51,10 @@ typedef struct {
     int32_t end_extend_gap_score;
 } taxi2_scores;
 
-/* distances.py:319-348 metric labels p, p-gaps, jc, k2p.
+/* distances.py:319-348 metric labels p, p-gaps, jc, k2p; distances.py:351-358 ncd.
+ * TAXI2_METRIC_NCD is accepted by taxi2_all_pairs[_dev] on ALIGN sets only: NCD of the same fill's
+ * aligned strings (the walkers write them, one fill per unordered pair for every metric, as
+ * versus_all.py:546-552 feeds one alignment to all metrics); elsewhere use taxi2_ncd_pairs.
  * TAXI2_METRIC_COUNTS is not a metric: accepted ALONE by the pair entry points (all_pairs[_dev],
  * rect_pairs, list_pairs) for sequences of at most 32 767 bp, it writes the four column counters of
  * every ordered pair packed into its 8-byte output slot (uint64: valid | ts << 16 | tv << 32 |
@@ -62,6 +65,7 @@ enum {
     TAXI2_METRIC_P_GAPS = 1,
     TAXI2_METRIC_JC = 2,
     TAXI2_METRIC_K2P = 3,
+    TAXI2_METRIC_NCD = 4,
     TAXI2_METRIC_COUNTS = 16
 };
 
@@ -191,7 +195,8 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
  * outputs on `stream` (asynchronous): d_out[(q - q0) * R + r][nmetrics] as taxi2_rect_pairs_dev,
  * slots d_sx / d_sy [(q - q0) * R + r][cap] (right-aligned as taxi2_align_strings' slot 0, cap >=
  * longest q + longest r) and lengths d_slen[(q - q0) * R + r].  Gotoh scores within int16, pairs up
- * to 2 048 bp (else an error: use taxi2_align_strings). */
+ * to 2 048 bp (else an error: use taxi2_align_strings).  TAXI2_METRIC_NCD may be among the metrics:
+ * NCD of the strings the same fill wrote (taxi2_ncd_slots_dev). */
 int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int64_t q1,
                            const taxi2_scores* sc, const int32_t* metrics, int nmetrics, double* d_out,
                            int32_t cap, uint8_t* d_sx, uint8_t* d_sy, int32_t* d_slen, void* stream);
@@ -203,7 +208,7 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
  * returns for (b, a) written in (a, b) column order (d_sx holds a's aligned string, d_sy b's), each
  * right-aligned at byte len(a) + len(b) of its cap-byte slot, lengths d_slen[k*2 + o].  Replaces
  * versus_all.py:746-750's two alignments of a pair (one per ordered pair) by one fill.  Same
- * shape limits as taxi2_rect_strings_dev.  reserve_cus: the persistent aligner grid leaves that many
+ * shape limits as taxi2_rect_strings_dev; TAXI2_METRIC_NCD as there.  reserve_cus: the persistent aligner grid leaves that many
  * CUs' worth of workgroups unlaunched, so work the caller queues on another stream (the previous
  * block's text) finds room to run beside it; 0 = the whole GPU. */
 int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
@@ -263,6 +268,19 @@ int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, c
 int taxi2_pack_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
                          int nslot, int slot, const int64_t* d_end, const int64_t* d_off, int64_t count, uint8_t* d_dx,
                          uint8_t* d_dy, void* stream);
+
+/* NCD of aligned-string slots already on the device -- taxi2_tri_strings_dev (nslot 2) or
+ * taxi2_rect_strings_dev (nslot 1) output: pair k's alignment of orientation o is the last
+ * d_slen[k * nslot + o] bytes before byte d_end[k] of slot k * nslot + o (cap bytes each).
+ * Orientation 0 is the ordered pair (x = d_sx string, y = d_sy string); orientation 1 (no = 2,
+ * nslot 2) the alignment of (b, a) stored in (a, b) column order, whose metric sees (d_sy, d_sx).
+ * d_out[k * no + o] = NCD (distances.py:351-358) of that ordered pair.  max_len: the longest
+ * sequence of the pairs (sizes the deflate working set; any aligned string is at most twice it);
+ * latin1: some byte >= 0x80 (compressed as its UTF-8 upper case).  Asynchronous on `stream`; uses
+ * the context's NCD staging (one call at a time per context). */
+int taxi2_ncd_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
+                        int nslot, int no, const int64_t* d_end, int64_t count, int32_t max_len, int latin1,
+                        double* d_out, void* stream);
 
 /* ---- compressed length (alfpy ncd.complexity) --------------------------------------------- *
  * out[k] = len(zlib.compress(upper(x[xs[k]]) + upper(y[ys[k]]))), zlib 1.2.11 level 6;

@@ -50,6 +50,7 @@ EXPORTS = (
     "taxi2_closest",
     "taxi2_align_strings",
     "taxi2_ncd_pairs",
+    "taxi2_ncd_slots_dev",
     "taxi2_zlib_lengths",
     "taxi2_format_pairs_dev",
     "taxi2_format_rows",
@@ -69,6 +70,9 @@ METRIC_CODES = {"p": 0, "p-gaps": 1, "jc": 2, "k2p": 3}
 # valid | ts << 16 | tv << 32 | gap << 48); must be the only metric of a call (taxi2_mi355x.h).
 COUNTS = "counts"
 COUNTS_CODE = 16
+# NCD (distances.py:351-358) inside taxi2_all_pairs[_dev] on ALIGN sets: from the same fill's aligned
+# strings (one fill per pair for every metric); other entry points take it through taxi2_ncd_pairs
+NCD_CODE = 4
 MAX_METRICS = 8
 
 
@@ -125,6 +129,7 @@ _SIGNATURES = {
                              _P, _INT, _P, _P, _P, _P]),
     "taxi2_align_strings": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _INT, _I32, _P, _P, _P]),
     "taxi2_ncd_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P, _INT, _P]),
+    "taxi2_ncd_slots_dev": (_INT, [_P, _P, _P, _P, _I64, _INT, _INT, _P, _I64, _I32, _INT, _P, _P]),
     "taxi2_zlib_lengths": (_INT, [_P, _INT, _INT, _P, _P, _I64, _P]),
     "taxi2_format_rows": (_INT, [_P, _INT, _P, _I64, _I64, _INT, _P, _P, _P, _P, _INT, _P, _I32, _P, _I64,
                                  ctypes.POINTER(_I64)]),
@@ -214,12 +219,15 @@ def to_cscores(scores) -> CScores:
     return CScores(*ints)
 
 
-def metric_codes(metrics: Iterable) -> np.ndarray:
+def metric_codes(metrics: Iterable, *, allow_ncd: bool = False) -> np.ndarray:
     codes = []
     for m in metrics:
         label = m if isinstance(m, str) else str(m)
         if label == COUNTS:
             codes.append(COUNTS_CODE)
+            continue
+        if label == "ncd" and allow_ncd:
+            codes.append(NCD_CODE)
             continue
         if label not in METRIC_CODES:
             raise NativeError(f"metric {label!r} is not computed by the MI355X engine")
@@ -357,8 +365,9 @@ class Engine:
 
     # ------------------------------------------------------------------ pair blocks
     def all_pairs(self, s: SeqSet, k0: int, count: int, metrics, scores=None, *, with_scores=False):
-        """Upper-triangle block of ``s``.  ALIGN: (count, 2, M) [(a,b), (b,a)]; else (count, M)."""
-        codes = metric_codes(metrics)
+        """Upper-triangle block of ``s``.  ALIGN: (count, 2, M) [(a,b), (b,a)]; else (count, M).
+        ALIGN sets also take "ncd": every metric of a pair from its one alignment (all_pairs_ncd)."""
+        codes = metric_codes(metrics, allow_ncd=s.aligned)
         shape = (count, 2, len(codes)) if s.aligned else (count, len(codes))
         out = np.empty(shape, dtype=np.float64)
         sc_out = np.empty(count, dtype=np.int32) if (with_scores and s.aligned) else None
@@ -376,7 +385,7 @@ class Engine:
     def all_pairs_dev(self, s: SeqSet, k0: int, count: int, metrics, out_ptr: int, scores=None,
                       scores_ptr: int | None = None, stream: int | None = None) -> None:
         """Asynchronous device-output variant (pointers from e.g. torch tensors on this GPU)."""
-        codes = metric_codes(metrics)
+        codes = metric_codes(metrics, allow_ncd=s.aligned)
         cs = to_cscores(scores)
         with self._lock:
             self._check(
@@ -480,7 +489,7 @@ class Engine:
                          sx_ptr: int, sy_ptr: int, slen_ptr: int, scores=None, stream: int | None = None) -> None:
         """Metrics (may be empty) and aligned strings of rows [q0, q1) x every r, one fill per pair
         (device slots [(q - q0) * R + r][cap], right-aligned; see taxi2_rect_strings_dev)."""
-        codes = metric_codes(metrics) if metrics else np.zeros(0, dtype=np.int32)
+        codes = metric_codes(metrics, allow_ncd=True) if metrics else np.zeros(0, dtype=np.int32)
         cs = to_cscores(scores)
         with self._lock:
             self._check(
@@ -497,7 +506,7 @@ class Engine:
         """Metrics ([count][2][M], may be empty) and BOTH orientations' aligned strings of the
         triangle pairs [k0, k0 + count), one fill per pair (device slots [k][2][cap]; see
         taxi2_tri_strings_dev)."""
-        codes = metric_codes(metrics) if metrics else np.zeros(0, dtype=np.int32)
+        codes = metric_codes(metrics, allow_ncd=True) if metrics else np.zeros(0, dtype=np.int32)
         cs = to_cscores(scores)
         with self._lock:
             self._check(
@@ -685,6 +694,22 @@ class Engine:
                     "taxi2_ncd_pairs",
                 )
         return out
+
+    def ncd_slots_dev(self, sx_ptr: int, sy_ptr: int, slen_ptr: int, cap: int, nslot: int, no: int, end_ptr: int,
+                      count: int, max_len: int, out_ptr: int, *, latin1: bool = False,
+                      stream: int | None = None) -> None:
+        """NCD of walker string slots on the device (taxi2_ncd_slots_dev): out[k * no + o] for pair k's
+        orientation o, from tri_strings_dev (nslot 2) / rect_strings_dev (nslot 1) slots whose strings
+        end at end[k].  Asynchronous on ``stream``."""
+        with self._lock:
+            self._check(
+                self._lib.taxi2_ncd_slots_dev(
+                    self._ctx, ctypes.c_void_p(sx_ptr), ctypes.c_void_p(sy_ptr), ctypes.c_void_p(slen_ptr), int(cap),
+                    int(nslot), int(no), ctypes.c_void_p(end_ptr), int(count), int(max_len), 1 if latin1 else 0,
+                    ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream) if stream else None,
+                ),
+                "taxi2_ncd_slots_dev",
+            )
 
     def zlib_lengths(self, x: SeqSet, xs, y: SeqSet | None = None, ys=None) -> np.ndarray:
         """len(zlib.compress(upper(x[xs[k]]) (+ upper(y[ys[k]])))) per k (zlib 1.2.11, level 6)."""

@@ -195,7 +195,6 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
          uint8_t* __restrict__ trace, int64_t buf_bytes, int cap_rows, unsigned long long* __restrict__ next,
          int band, int64_t* __restrict__ esc_list, unsigned long long* __restrict__ esc_n, StrOut so) {
     static_assert(K % 2 == 0 && K <= 8 && W <= 2, "row-shared shapes: K <= 8 columns per lane, one or two fill waves");
-    constexpr int TB = 4 * K;  // trace bytes per lane and step: (D1 lo, D1 hi, D2 lo, D2 hi) per slot
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
     constexpr int dz = -1;                          // default scores: ie
@@ -206,7 +205,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     __shared__ ArChain chs[2];
     __shared__ int fin[2][AR_UNITS][2];
     __shared__ uint2 ring[(W > 1 ? W - 1 : 1) * AR_RING];
-    __shared__ uint32_t eqt[4][NT][K];  // (s(x0_k, base), s(x1_k, base)) - co_i as pk_int, per lane and slot
+    // (s(x0_k, base), s(x1_k, base)) - co_i as pk_int, per lane and slot, in pieces of EP slots:
+    // eqt[base][k / EP][lane][k % EP], so that the step's vector reads (EP words per lane) are
+    // lane-contiguous -- a lane-major [lane][K] row (32 bytes per lane at K = 8) made every 16-byte
+    // read a 2-way bank conflict (1.64 conflict cycles per LDS instruction)
+    constexpr int EP = ar_pw(K);
+    __shared__ uint32_t eqt[4][K / EP][NT][EP];
     __shared__ int64_t s_qc, s_qend;
     __shared__ int s_n, s_rows, s_seg;
     __shared__ int s_prog[2];  // steps completed by each fill wave in the current chain
@@ -520,7 +524,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 #pragma unroll
                         for (int hh = 0; hh < 2; ++hh)
                             s2[hh] = (jr[hh] < 1 ? 0 : (cb[hh] == (uint32_t)"ACGT"[rb] ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
-                        eqt[rb][tid][k] = ar_pk_int(s2[0], s2[1]);
+                        eqt[rb][k / EP][tid][k % EP] = ar_pk_int(s2[0], s2[1]);
                     }
                 }
             }
@@ -578,19 +582,22 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 }
                 uint32_t eq[K];
                 {
-                    const uint32_t* tp = (const uint32_t*)((const char*)&eqt[0][0][0] + rec.x) + (size_t)tq * K;
-                    if constexpr (K % 4 == 0) {  // 16-byte aligned rows (K * 4 bytes per lane)
+                    // the row base's table, this lane's EP words of each piece (lane-contiguous reads)
+                    const char* tb = (const char*)&eqt[0][0][0][0] + rec.x;
 #pragma unroll
-                        for (int q = 0; q < K / 4; ++q) {
-                            const uint4 v = ((const uint4*)__builtin_assume_aligned(tp, 16))[q];
+                    for (int q = 0; q < K / EP; ++q) {
+                        const char* pq = tb + (size_t)(q * NT + tq) * (EP * 4);
+                        if constexpr (EP == 4) {
+                            const uint4 v = *(const uint4*)__builtin_assume_aligned(pq, 16);
                             eq[4 * q] = v.x;
                             eq[4 * q + 1] = v.y;
                             eq[4 * q + 2] = v.z;
                             eq[4 * q + 3] = v.w;
+                        } else {
+                            const uint2 v = *(const uint2*)__builtin_assume_aligned(pq, 8);
+                            eq[2 * q] = v.x;
+                            eq[2 * q + 1] = v.y;
                         }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < K; ++k) eq[k] = tp[k];
                     }
                 }
                 if (pre) {  // a unit's first or last row, or a byte other than A/C/G/T

@@ -1226,6 +1226,9 @@ __global__ void __launch_bounds__(64 * (W + 1), OCC)
 k_alignt2_queued(SetView XS, SetView YS, PairSrc ps, KScores scin, MetricSpec ms, int chunk_req, int out_mode,
                  double* __restrict__ out, int32_t* __restrict__ sout, uint8_t* __restrict__ trace, int64_t buf_bytes,
                  int cap_rows, int hops, unsigned long long* __restrict__ next, StrOut so) {
+    // nothing queued (the usual case): leave before any set-up -- the full body's prologue over the
+    // resident grid cost ~1 ms per launch (1 % of the config-3 step) with an empty queue
+    if (ps.dcount && *ps.dcount == 0) return;
     alignt2_body<K, W, DEF, false>(XS, YS, ps, scin, ms, chunk_req, out_mode, out, sout, trace, buf_bytes, cap_rows,
                                    hops, next, 0, nullptr, nullptr, so);
 }

@@ -76,6 +76,10 @@ struct taxi2_ctx {
     size_t d_fmt_bytes = 0;
     void* d_sub = nullptr;  // subset aggregation scratch (row partials, groups, worklist)
     size_t d_sub_bytes = 0;
+    void* d_ncd = nullptr;  // NCD from string slots: stream descriptors + compressed lengths
+    size_t d_ncd_bytes = 0;
+    void* d_nslots = nullptr;  // all-metrics versusAll: the walkers' string slots of one chunk
+    size_t d_nslots_bytes = 0;
     void* d_zheads = nullptr;  // NCD: per-thread deflate hash heads (kept zero) and scratch slabs
     void* d_zslabs = nullptr;
     int64_t z_threads = 0;
@@ -149,12 +153,15 @@ SetView view(const DevSet& s) { return SetView{s.bytes, s.offs, s.meta, s.planes
 
 // allow_counts: the pair entry points also accept TAXI2_METRIC_COUNTS, alone, for sequences of at
 // most 32 767 bp (every counter then fits its 16-bit field).
+// allow_ncd: TAXI2_METRIC_NCD too (taxi2_all_pairs[_dev] on ALIGN sets: NCD from the same fill's
+// aligned strings, all_pairs_ncd).
 int check_metrics(taxi2_ctx* ctx, const int32_t* metrics, int nm, MetricSpec& ms, bool allow_counts = false,
-                  int max_len = 0) {
+                  int max_len = 0, bool allow_ncd = false) {
     if (nm < 1 || nm > MAX_METRICS) return fail(ctx, "nmetrics must be in [1, %d]", MAX_METRICS);
     ms.n = nm;
     for (int m = 0; m < nm; ++m) {
-        if (metrics[m] == TAXI2_METRIC_COUNTS && allow_counts) {
+        if (metrics[m] == TAXI2_METRIC_NCD && allow_ncd) {
+        } else if (metrics[m] == TAXI2_METRIC_COUNTS && allow_counts) {
             if (nm != 1) return fail(ctx, "TAXI2_METRIC_COUNTS must be the only metric of a call");
             if (max_len > 32767) return fail(ctx, "TAXI2_METRIC_COUNTS needs sequences of at most 32767 bp");
         } else if (metrics[m] < TAXI2_METRIC_P || metrics[m] > TAXI2_METRIC_K2P) {
@@ -819,8 +826,13 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
         unsigned long long q = 0;
         HIP_TRY(ctx, hipMemcpyAsync(&q, esc_n, sizeof q, hipMemcpyDeviceToHost, st));
         HIP_TRY(ctx, hipStreamSynchronize(st));
+        int64_t single = 0;  // units of one pair (x1 = -1): the other half of every lane idles
+        for (const auto& sg : segs)
+            if (sg.x1 < 0) single += sg.nb;
         fprintf(stderr, "taxi2 band: k_alignr<%d,%d> band %d: %llu of %lld pairs took the full-trace pass (%zu segments, "
-                "%lld units)\n", v.K, v.W, band, q, (long long)ps.count, segs.size(), (long long)units);
+                "%lld units, %lld single-pair units = %.2f %%, grid %lld, chunk %d)\n", v.K, v.W, band, q,
+                (long long)ps.count, segs.size(), (long long)units, (long long)single,
+                units ? 100.0 * (double)single / (double)units : 0.0, (long long)grid, chunk);
     }
 #ifdef AR_PROF
     {  // profiling build: the launch's per-wave phase totals (alignr_kernel.hpp AR_PROF)
@@ -1184,7 +1196,8 @@ struct Tracer {
     }
 };
 
-int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1);
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1,
+                hipStream_t st = nullptr, int likely_n = 0);
 
 // Raw-mode NCD with C(x) computed once per set member (when the pairs outnumber the sequences).
 int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
@@ -1240,20 +1253,31 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
 // zlen_wave.hpp); longer ones, latin-1 text (each byte -> 1-2 UTF-8 bytes) or TAXI2_ZLEN_SERIAL=1:
 // one thread per stream with per-thread HBM scratch slabs kept in the context (the head tables
 // are zeroed once at allocation), any length (the window slides as zlib's does).
-int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1) {
+int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1,
+                hipStream_t st, int likely_n) {
     if (n <= 0) return 0;
-    if (max_n <= zlw::NMAX && !latin1 && !getenv("TAXI2_ZLEN_SERIAL")) {
-        const int nmax = std::max(max_n, 4);
+    if (!st) st = ctx->stream;
+    const bool wave_ok = !latin1 && !getenv("TAXI2_ZLEN_SERIAL");
+    auto wave_pass = [&](int nmax_in, int redo) -> int {
+        const int nmax = std::max(nmax_in, 4);
         const size_t lds = zlw::lds_bytes(nmax);
         if (lds > 64 * 1024)
             HIP_TRY(ctx, hipFuncSetAttribute((const void*)k_zlen_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int per_cu = 0;
         HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave, 64, lds));
         const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
-        hipLaunchKernelGGL(k_zlen_wave, dim3((unsigned)grid), dim3(64), lds, ctx->stream, d_st, n, nmax, d_out);
+        hipLaunchKernelGGL(k_zlen_wave, dim3((unsigned)grid), dim3(64), lds, st, d_st, n, nmax, d_out, redo);
         HIP_TRY(ctx, hipGetLastError());
         return 0;
+    };
+    int redo = 0;
+    if (wave_ok && likely_n > 0 && likely_n < max_n && likely_n <= zlw::NMAX) {
+        // most streams fit `likely_n`: a first pass sized for them (smaller LDS, more waves per CU),
+        // then the pass below over the streams it declined (-1) only
+        if (wave_pass(likely_n, 0)) return -1;
+        redo = 1;
     }
+    if (max_n <= zlw::NMAX && wave_ok) return wave_pass(max_n, redo);
     // waves per SIMD of the one-thread-per-stream parse (TAXI2_ZLEN_WAVES, 1..4: VGPRs cap it at 4);
     // each thread owns 113 KB of HBM scratch
     int wps = 2;
@@ -1268,12 +1292,100 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
         ctx->z_threads = 0;
         HIP_TRY(ctx, hipMalloc(&ctx->d_zheads, (size_t)threads * ZS_HEAD));
         HIP_TRY(ctx, hipMalloc(&ctx->d_zslabs, (size_t)threads * ZS_SLAB));
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_zheads, 0, (size_t)threads * ZS_HEAD, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_zheads, 0, (size_t)threads * ZS_HEAD, st));
         ctx->z_threads = threads;
     }
-    hipLaunchKernelGGL(k_zlen, dim3((unsigned)(threads / 64)), dim3(64), 0, ctx->stream, d_st, n,
-                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out, (int)latin1);
+    hipLaunchKernelGGL(k_zlen, dim3((unsigned)(threads / 64)), dim3(64), 0, st, d_st, n,
+                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out, (int)latin1, redo);
     HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+// Where the aligned strings of `n` pairs sit (the walkers' StrOut slots) and which ordered pairs
+// want NCD: slot p * nslot + o, right-aligned at d_end[p] (or len(a) + len(b) of pair p of `ps`
+// when d_end is null), `no` orientations (1: (a, b) only; 2: and (b, a)).
+struct SlotSrc {
+    const uint8_t* sx;
+    const uint8_t* sy;
+    const int32_t* slen;
+    int64_t cap;
+    int nslot, no;
+    const int64_t* d_end;
+    PairSrc ps;
+};
+
+// NCD (distances.py:351-358) of every (pair, orientation) from the aligned strings already in HBM:
+// k_ncd_slot_streams (4 streams per pair when both orientations hold the same alignment, else 6),
+// one k_zlen_wave launch over all of them, k_ncd_slot_finish into out[(p * no + o) * ostride + ocol].
+// max_str bounds every stream (2 x the longest aligned string); latin1: the set holds bytes >= 0x80
+// (compressed as their UTF-8 upper case, one-thread path).  Stream-ordered on `st`, no host sync.
+int ncd_from_slots(taxi2_ctx* ctx, const SlotSrc& ss, const DevSet& X, const DevSet& Y, int64_t n, int max_str,
+                   bool latin1, double* out, int64_t ostride, int ocol, hipStream_t st) {
+    if (n <= 0) return 0;
+    const int64_t ns = n * 2 * ss.no, nc = n * ss.no;
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_st = al((size_t)(ns + nc) * sizeof(ZStream)), b_c = al((size_t)(ns + nc) * 4);
+    if (ensure(ctx, &ctx->d_ncd, &ctx->d_ncd_bytes, b_st + b_c)) return -1;
+    ZStream* d_st = (ZStream*)ctx->d_ncd;
+    int32_t* d_c = (int32_t*)((char*)ctx->d_ncd + b_st);
+    hipLaunchKernelGGL(k_ncd_slot_streams, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, ss.sx, ss.sy, ss.slen,
+                       ss.cap, ss.nslot, ss.no, ss.d_end, view(X), view(Y), ss.ps, n, d_st, d_st + ns);
+    HIP_TRY(ctx, hipGetLastError());
+    // singles and concatenations in separate launches, each first sized for the likely length (an
+    // aligned string is rarely much longer than the longer sequence: +1/16 + 32 bytes)
+    const int lmax = std::max(X.max_len, Y.max_len);
+    const int likely = std::min(max_str / 2, lmax + lmax / 16 + 32);
+    if (launch_zlen(ctx, d_st, ns, d_c, max_str / 2, latin1, st, likely)) return -1;
+    if (launch_zlen(ctx, d_st + ns, nc, d_c + ns, max_str, latin1, st, 2 * likely)) return -1;
+    hipLaunchKernelGGL(k_ncd_slot_finish, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, d_c, d_c + ns, n,
+                       ss.no, out, ostride, ocol);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+bool has_ncd(const MetricSpec& ms) {
+    for (int m = 0; m < ms.n; ++m)
+        if (ms.code[m] == TAXI2_METRIC_NCD) return true;
+    return false;
+}
+
+// versusAll with every metric incl. NCD from ONE fill per unordered pair (versus_all.py:546-552): the
+// packed aligner writes the counter metrics (NCD's columns get a NaN placeholder) and both
+// orientations' aligned strings of a chunk of pairs into slots; ncd_from_slots overwrites the NCD
+// columns.  d_out[k][2][nm] on the device (h_out == nullptr, stream-ordered on st) or h_out on the
+// host (chunk by chunk through ctx->d_out).  Returns 1 without launching when the packed aligner
+// does not cover the shape (linear scores, past 2 048 bp, scores outside int16).
+int all_pairs_ncd(taxi2_ctx* ctx, const DevSet& S, int64_t k0, int64_t count, const taxi2_scores* sc,
+                  const MetricSpec& ms, double* d_out, double* h_out, int32_t* scores_out, hipStream_t st) {
+    const int cap = std::max(2 * S.max_len, 1);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)2 << 30) / (4 * (int64_t)cap + 16)));
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_slots = al((size_t)chunk * 2 * cap), b_len = al((size_t)chunk * 2 * 4);
+    const size_t b_out = h_out ? al((size_t)chunk * 2 * ms.n * 8) : 0, b_sc = scores_out && h_out ? al((size_t)chunk * 4) : 0;
+    if (ensure(ctx, &ctx->d_nslots, &ctx->d_nslots_bytes, 2 * b_slots + b_len + b_out + b_sc)) return -1;
+    uint8_t* d_sx = (uint8_t*)ctx->d_nslots;
+    uint8_t* d_sy = d_sx + b_slots;
+    int32_t* d_len = (int32_t*)(d_sy + b_slots);
+    double* d_tmp = h_out ? (double*)((char*)d_len + b_len) : nullptr;
+    int32_t* d_stmp = b_sc ? (int32_t*)((char*)d_len + b_len + b_out) : nullptr;
+    for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+        const int64_t n = std::min(chunk, count - c0);
+        PairSrc ps{PAIRS_TRI, k0 + c0, n, S.n, 0, nullptr, nullptr};
+        double* o = h_out ? d_tmp : d_out + c0 * 2 * ms.n;
+        int32_t* so = scores_out ? (h_out ? d_stmp : scores_out + c0) : nullptr;
+        const int rc = launch_packed_strings(ctx, S, S, ps, sc, ms, OUT_BOTH, o, so, st, StrOut{d_sx, d_sy, d_len, cap, 2});
+        if (rc) return rc;
+        SlotSrc ss{d_sx, d_sy, d_len, cap, 2, 2, nullptr, ps};
+        for (int m = 0; m < ms.n; ++m)
+            if (ms.code[m] == TAXI2_METRIC_NCD && ncd_from_slots(ctx, ss, S, S, n, 2 * cap, S.high, o, ms.n, m, st))
+                return -1;
+        if (h_out) {
+            HIP_TRY(ctx, hipMemcpyAsync(h_out + c0 * 2 * ms.n, o, (size_t)n * 2 * ms.n * 8, hipMemcpyDeviceToHost, st));
+            if (scores_out)
+                HIP_TRY(ctx, hipMemcpyAsync(scores_out + c0, so, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(ctx, hipStreamSynchronize(st));
+        }
+    }
     return 0;
 }
 
@@ -1340,6 +1452,8 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_sub) (void)hipFree(ctx->d_sub);
     if (ctx->d_zheads) (void)hipFree(ctx->d_zheads);
     if (ctx->d_zslabs) (void)hipFree(ctx->d_zslabs);
+    if (ctx->d_ncd) (void)hipFree(ctx->d_ncd);
+    if (ctx->d_nslots) (void)hipFree(ctx->d_nslots);
     if (ctx->shared_ev) (void)hipEventDestroy(ctx->shared_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1476,13 +1590,44 @@ int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const ta
     DevSet* s = get_set(ctx, set);
     if (!s) return fail(ctx, "unknown set %d", set);
     MetricSpec ms;
-    if (check_metrics(ctx, metrics, nmetrics, ms, true, s->max_len)) return -1;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, s->max_len, s->mode == TAXI2_MODE_ALIGN)) return -1;
     const int64_t total = s->n * (s->n - 1) / 2;
     if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
     if (s->mode == TAXI2_MODE_ALIGN && !sc) return fail(ctx, "scores required in ALIGN mode");
     if (s->mode == TAXI2_MODE_PREALIGNED && scores_out) return fail(ctx, "no scores in PREALIGNED mode");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     PairSrc ps{PAIRS_TRI, k0, count, s->n, 0, nullptr, nullptr};
+    if (has_ncd(ms)) {
+        if (count == 0) return 0;
+        const int rc = all_pairs_ncd(ctx, *s, k0, count, sc, ms, nullptr, out, scores_out, ctx->stream);
+        if (rc <= 0) return rc;
+        // not the packed aligner's shape: the counter metrics (NCD columns NaN), then NCD of the
+        // trace kernels' strings per chunk of host pair lists (taxi2_ncd_pairs)
+        if (run_pairs(ctx, *s, *s, ps, sc, ms, OUT_BOTH, out, scores_out)) return -1;
+        const int64_t step = (int64_t)1 << 16;
+        std::vector<int64_t> xa, yb;
+        std::vector<double> v;
+        for (int64_t c0 = 0; c0 < count; c0 += step) {
+            const int64_t n = std::min(step, count - c0);
+            xa.resize(n);
+            yb.resize(n);
+            v.resize(2 * n);
+            int64_t a = tri_row_host(k0 + c0, s->n), b = a + 1 + (k0 + c0 - a * (2 * s->n - a - 1) / 2);
+            for (int64_t k = 0; k < n; ++k) {
+                xa[k] = a;
+                yb[k] = b;
+                if (++b == s->n) b = ++a + 1;
+            }
+            if (taxi2_ncd_pairs(ctx, set, set, xa.data(), yb.data(), n, sc, 1, v.data())) return -1;
+            for (int64_t k = 0; k < n; ++k)
+                for (int m = 0; m < ms.n; ++m)
+                    if (ms.code[m] == TAXI2_METRIC_NCD) {
+                        out[((c0 + k) * 2) * ms.n + m] = v[2 * k];
+                        out[((c0 + k) * 2 + 1) * ms.n + m] = v[2 * k + 1];
+                    }
+        }
+        return 0;
+    }
     return run_pairs(ctx, *s, *s, ps, sc, ms, OUT_BOTH, out, scores_out);
 }
 
@@ -1493,7 +1638,7 @@ int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, cons
     DevSet* s = get_set(ctx, set);
     if (!s) return fail(ctx, "unknown set %d", set);
     MetricSpec ms;
-    if (check_metrics(ctx, metrics, nmetrics, ms, true, s->max_len)) return -1;
+    if (check_metrics(ctx, metrics, nmetrics, ms, true, s->max_len, s->mode == TAXI2_MODE_ALIGN)) return -1;
     const int64_t total = s->n * (s->n - 1) / 2;
     if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1501,6 +1646,14 @@ int taxi2_all_pairs_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, cons
     PairSrc ps{PAIRS_TRI, k0, count, s->n, 0, nullptr, nullptr};
     if (s->mode == TAXI2_MODE_ALIGN) {
         if (!sc) return fail(ctx, "scores required in ALIGN mode");
+        if (has_ncd(ms)) {
+            if (count == 0) return 0;
+            const int rc = all_pairs_ncd(ctx, *s, k0, count, sc, ms, d_out, nullptr, d_scores, st);
+            if (rc > 0)
+                return fail(ctx, "NCD on the device path needs the packed aligner (Gotoh scores within int16, "
+                                 "<= 2 048 bp): use taxi2_all_pairs");
+            return rc;
+        }
         return launch_align_pairs(ctx, *s, *s, ps, sc, ms, OUT_BOTH, d_out, d_scores, st);
     }
     return launch_prealigned(ctx, *s, *s, ps, ms, d_out, st);
@@ -1548,7 +1701,8 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
     if (Q->mode != TAXI2_MODE_ALIGN || R->mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need ALIGN sets");
     if (!sc) return fail(ctx, "scores required");
     MetricSpec ms{};
-    if (nmetrics > 0 && check_metrics(ctx, metrics, nmetrics, ms, true, std::max(Q->max_len, R->max_len))) return -1;
+    if (nmetrics > 0 && check_metrics(ctx, metrics, nmetrics, ms, true, std::max(Q->max_len, R->max_len), true))
+        return -1;
     if (q0 < 0 || q1 < q0 || q1 > Q->n) return fail(ctx, "query range out of bounds");
     if ((q1 - q0) * R->n > 0 && (!d_sx || !d_sy || !d_slen || (nmetrics > 0 && !d_out))) return fail(ctx, "null output");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1557,6 +1711,14 @@ int taxi2_rect_strings_dev(taxi2_ctx* ctx, int set_q, int set_r, int64_t q0, int
     const int rc = launch_packed_strings(ctx, *Q, *R, ps, sc, ms, OUT_AB, d_out, nullptr, st,
                                          StrOut{d_sx, d_sy, d_slen, cap, 1});
     if (rc > 0) return fail(ctx, "walker strings need the packed aligner (Gotoh scores within int16, <= 2 048 bp)");
+    if (rc == 0 && has_ncd(ms) && ps.count > 0) {  // NCD of the strings this fill just wrote
+        SlotSrc ss{d_sx, d_sy, d_slen, cap, 1, 1, nullptr, ps};
+        for (int m = 0; m < ms.n; ++m)
+            if (ms.code[m] == TAXI2_METRIC_NCD &&
+                ncd_from_slots(ctx, ss, *Q, *R, ps.count, 2 * (Q->max_len + R->max_len), Q->high || R->high, d_out,
+                               ms.n, m, st))
+                return -1;
+    }
     return rc;
 }
 
@@ -1569,7 +1731,7 @@ int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, co
     if (S->mode != TAXI2_MODE_ALIGN) return fail(ctx, "aligned strings need an ALIGN set");
     if (!sc) return fail(ctx, "scores required");
     MetricSpec ms{};
-    if (nmetrics > 0 && check_metrics(ctx, metrics, nmetrics, ms, true, S->max_len)) return -1;
+    if (nmetrics > 0 && check_metrics(ctx, metrics, nmetrics, ms, true, S->max_len, true)) return -1;
     const int64_t total = S->n * (S->n - 1) / 2;
     if (k0 < 0 || count < 0 || k0 + count > total) return fail(ctx, "pair range out of bounds");
     if (count > 0 && (!d_sx || !d_sy || !d_slen || (nmetrics > 0 && !d_out))) return fail(ctx, "null output");
@@ -1581,6 +1743,13 @@ int taxi2_tri_strings_dev(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, co
                                          StrOut{d_sx, d_sy, d_slen, cap, 2});
     ctx->reserve_cus = 0;
     if (rc > 0) return fail(ctx, "walker strings need the packed aligner (Gotoh scores within int16, <= 2 048 bp)");
+    if (rc == 0 && has_ncd(ms) && count > 0) {  // NCD of both orientations' strings this fill just wrote
+        SlotSrc ss{d_sx, d_sy, d_slen, cap, 2, 2, nullptr, ps};
+        for (int m = 0; m < ms.n; ++m)
+            if (ms.code[m] == TAXI2_METRIC_NCD &&
+                ncd_from_slots(ctx, ss, *S, *S, count, 4 * S->max_len, S->high, d_out, ms.n, m, st))
+                return -1;
+    }
     return rc;
 }
 
@@ -1827,6 +1996,38 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
     const int no = both ? 2 : 1;
     const int cap = X->max_len + Y->max_len;
     if (!aligned && X->n + (X == Y ? 0 : Y->n) <= count * no) return ncd_raw_cached(ctx, *X, *Y, xs, ys, count, both, out);
+    if (aligned && X->mode == TAXI2_MODE_ALIGN && Y->mode == TAXI2_MODE_ALIGN) {
+        // the packed aligner's walkers write the strings (one fill per pair, both orientations),
+        // NCD from those slots (ncd_from_slots); the trace kernels below only for other shapes
+        const int scap = std::max(cap, 1);
+        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)1 << 30) / (4 * (int64_t)scap + 16)));
+        auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+        const size_t b_idx = al((size_t)chunk * 16), b_len = al((size_t)chunk * 8), b_v = al((size_t)chunk * 16);
+        const size_t b_slots = al((size_t)chunk * 2 * scap);
+        if (ensure(ctx, &ctx->d_nslots, &ctx->d_nslots_bytes, b_idx + b_len + b_v + 2 * b_slots)) return -1;
+        int64_t* d_idx = (int64_t*)ctx->d_nslots;
+        int32_t* d_len = (int32_t*)((char*)d_idx + b_idx);
+        double* d_v = (double*)((char*)d_len + b_len);
+        uint8_t* d_sx = (uint8_t*)d_v + b_v;
+        uint8_t* d_sy = d_sx + b_slots;
+        MetricSpec none{};
+        int rc = 1;
+        for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+            const int64_t n = std::min(chunk, count - c0);
+            HIP_TRY(ctx, hipMemcpyAsync(d_idx, xs + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(d_idx + chunk, ys + c0, n * 8, hipMemcpyHostToDevice, ctx->stream));
+            PairSrc ps{PAIRS_LIST, 0, n, 0, 0, d_idx, d_idx + chunk};
+            rc = launch_packed_strings(ctx, *X, *Y, ps, sc, none, both ? OUT_BOTH : OUT_AB, nullptr, nullptr,
+                                       ctx->stream, StrOut{d_sx, d_sy, d_len, scap, 2});
+            if (rc < 0) return -1;
+            if (rc > 0) break;  // not this kernel's shape: the trace kernels below
+            SlotSrc ss{d_sx, d_sy, d_len, scap, 2, no, nullptr, ps};
+            if (ncd_from_slots(ctx, ss, *X, *Y, n, 2 * scap, X->high || Y->high, d_v, 1, 0, ctx->stream)) return -1;
+            HIP_TRY(ctx, hipMemcpyAsync(out + c0 * no, d_v, (size_t)n * no * 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        if (rc == 0) return 0;
+    }
     Tracer tr;
     int64_t chunk = (int64_t)1 << 16;
     if (aligned) {
@@ -1870,6 +2071,23 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     return 0;
+}
+
+int taxi2_ncd_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
+                        int nslot, int no, const int64_t* d_end, int64_t count, int32_t max_len, int latin1,
+                        double* d_out, void* stream) {
+    if (!ctx) return -1;
+    if (count < 0 || cap < 1 || max_len < 0 || (nslot != 1 && nslot != 2) || no < 1 || no > nslot)
+        return fail(ctx, "invalid arguments to taxi2_ncd_slots_dev");
+    if (count == 0) return 0;
+    if (!d_sx || !d_sy || !d_slen || !d_end || !d_out) return fail(ctx, "null argument");
+    if (2 * (int64_t)max_len > cap) return fail(ctx, "slots of %lld bytes < twice the longest sequence", (long long)cap);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    DevSet lens;  // no set: the slot ends come from d_end; only the length bound is read
+    lens.max_len = max_len;
+    SlotSrc ss{d_sx, d_sy, d_slen, cap, nslot, no, d_end, PairSrc{PAIRS_LIST, 0, count, 0, 0, nullptr, nullptr}};
+    return ncd_from_slots(ctx, ss, lens, lens, count, 4 * std::max(max_len, 1), latin1 != 0, d_out, 1, 0, st);
 }
 
 int taxi2_zlib_lengths(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
@@ -2260,7 +2478,18 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     if (tmax64 > INT32_MAX / 2) return fail(ctx, "taxi2_subset_aggregate_dev: too many subsets");
     const int tmax = (int)tmax64;
     const int64_t row_bytes = per_row * (int64_t)(sizeof(SubPart) + sizeof(SubWork)) + tmax64 * m * (int64_t)sizeof(SubPart);
-    const int64_t rows_per = std::max<int64_t>(1, std::min<int64_t>(SUB_MAX_ROWS, ((int64_t)256 << 20) / row_bytes));
+    // the row sub-block fits ~256 MB, or the caller's scratch (its per-block arrays: partials, work,
+    // chunk partials, 3 ints per row; fixed: offsets, chunk map, column codes, 10 x 256 B of alignment)
+    int64_t budget = (int64_t)256 << 20;
+    if (d_scratch) {
+        const int64_t fixed = (int64_t)(ns + 1) * 4 + (int64_t)tmax * 4 + (nat ? ncols : 0) + 1 + 4 + 10 * 256;
+        budget = std::min<int64_t>(budget, scratch_bytes - fixed);
+    }
+    const int64_t rows_fit = budget / (row_bytes + 12);
+    if (d_scratch && rows_fit < 1)
+        return fail(ctx, "taxi2_subset_aggregate_dev: scratch of %lld bytes holds no row (%lld per row)",
+                    (long long)scratch_bytes, (long long)(row_bytes + 12));
+    const int64_t rows_per = std::max<int64_t>(1, std::min<int64_t>(SUB_MAX_ROWS, rows_fit));
     const int64_t rsub = std::min(rows_per, nrows);
     auto al = [](size_t v) { return (v + 255) / 256 * 256; };
     const size_t o_part = 0, o_work = al((size_t)rsub * per_row * sizeof(SubPart));

@@ -18,8 +18,9 @@ namespace taxi2 {
 struct ZStream {
     const uint8_t* a;
     const uint8_t* b;
-    int32_t na, nb;
+    int32_t na, nb;  // na < 0: a skipped stream (its length is ZLEN_SKIPPED)
 };
+constexpr int32_t ZLEN_SKIPPED = -2;
 
 // Per-thread scratch slab after the head tables: [window][prev][Trees]
 constexpr size_t ZS_WIN = ((size_t)zl::WIN_BYTES + 255) / 256 * 256;
@@ -30,27 +31,34 @@ constexpr size_t ZS_HEAD = (size_t)zl::HASH_SIZE * 2;
 
 __global__ void __launch_bounds__(64, 4)
 k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, uint8_t* __restrict__ slabs,
-       int32_t* __restrict__ out, int latin1) {
+       int32_t* __restrict__ out, int latin1, int redo) {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     uint8_t* slab = slabs + tid * ZS_SLAB;
     zl::Scratch z{slab, reinterpret_cast<uint16_t*>(slab + ZS_WIN), heads + tid * zl::HASH_SIZE};
     zl::Trees* t = reinterpret_cast<zl::Trees*>(slab + ZS_WIN + ZS_PREV);
     for (int64_t s = tid; s < n; s += nthreads) {
+        if (redo && out[s] != -1) continue;  // a second pass: only the streams the first one declined
         const ZStream d = st[s];
-        out[s] = zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t, latin1 != 0);
+        out[s] = d.na < 0 ? ZLEN_SKIPPED : zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t, latin1 != 0);
     }
 }
 
 // One wave per stream, all state in LDS (zlen_wave.hpp): for launches whose streams are at most
-// `nmax` bytes (dynamic LDS sized for nmax).  Persistent: each workgroup (one wave) takes streams
-// blockIdx.x, + gridDim.x, ...
+// `nmax` bytes (dynamic LDS sized for nmax); a longer stream gets -1.  Persistent: each workgroup
+// (one wave) takes streams blockIdx.x, + gridDim.x, ...  redo: a second pass with a larger nmax over
+// the streams a first pass (sized for the likely lengths, more waves per CU) left at -1.
 __global__ void __launch_bounds__(64)
-k_zlen_wave(const ZStream* __restrict__ st, int64_t n, int nmax, int32_t* __restrict__ out) {
+k_zlen_wave(const ZStream* __restrict__ st, int64_t n, int nmax, int32_t* __restrict__ out, int redo) {
     extern __shared__ __attribute__((aligned(16))) uint8_t zsm[];
     const int lane = (int)threadIdx.x;
     for (int64_t s = blockIdx.x; s < n; s += gridDim.x) {
+        if (redo && out[s] != -1) continue;  // wave-uniform
         const ZStream d = st[s];
+        if (d.na < 0) {  // skipped (wave-uniform: one wave per workgroup)
+            if (lane == 0) out[s] = ZLEN_SKIPPED;
+            continue;
+        }
         const int r = d.na + d.nb <= nmax ? zlw::compressed_len_wave(d.a, d.na, d.b, d.nb, zsm, nmax, lane) : -1;
         if (lane == 0) out[s] = r;  // -1: longer than the launch promised (the host checks)
         __syncthreads();
@@ -138,6 +146,95 @@ k_ncd_finish_cached(const int32_t* __restrict__ c12, const int32_t* __restrict__
     const double c1 = cx[xs[p]], c2 = cy[ys[p]], c = c12[t];
     const double mn = c1 < c2 ? c1 : c2, mx = c1 < c2 ? c2 : c1;
     out[t] = (c - mn) / mx;
+}
+
+// ---- NCD from the aligners' own string slots (one fill per pair for every metric) ------------
+// versus_all.py:546-552 hands ONE alignment per ordered pair to every metric in the list, NCD
+// included (distances.py:351-358).  The packed aligners' walkers write each alignment while they
+// walk it (StrOut): slot s = p * nslot + o holds it right-aligned at byte end(p) = len(a) + len(b),
+// slen[s] bytes.  Orientation 0 is the ordered pair (a, b): x = sx, y = sy.  Orientation 1 is
+// Biopython's alignment of (b, a) written in (a, b) column order, so its metric sees x = sy, y = sx.
+//
+// Streams per pair: singles[p][4] = C(x0), C(y0), C(x1), C(y1) and concat[p][2] = C(x0 + y0),
+// C(x1 + y1) (x_o, y_o the metric's first and second string of orientation o).  One wave per
+// pair compares the two orientations' strings: when they are the same alignment (no Ix / Iy tie on
+// the path, most pairs) orientation 1's singles ARE orientation 0's (swapped), so those two
+// streams are marked skipped (na = -1) and only the concatenation y0 + x0 is new: 4 streams per
+// pair instead of 6.
+__device__ __forceinline__ void ncd_slot(const uint8_t* sx, const uint8_t* sy, const int32_t* slen, int64_t cap,
+                                         int nslot, int o, int64_t p, int64_t end, const uint8_t*& x,
+                                         const uint8_t*& y, int32_t& len) {
+    const int64_t s = p * nslot + o;
+    len = slen[s];
+    const int64_t off = s * cap + (end - len);
+    x = sx + off;
+    y = sy + off;
+}
+
+__global__ void __launch_bounds__(256)
+k_ncd_slot_streams(const uint8_t* __restrict__ sx, const uint8_t* __restrict__ sy, const int32_t* __restrict__ slen,
+                   int64_t cap, int nslot, int no, const int64_t* __restrict__ d_end, SetView XS, SetView YS,
+                   PairSrc ps, int64_t n, ZStream* __restrict__ singles, ZStream* __restrict__ concat) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (p >= n) return;  // wave-uniform
+    int64_t end;
+    if (d_end != nullptr) {
+        end = d_end[p];
+    } else {
+        int64_t a, b;
+        decode_pair(ps, p, a, b);
+        end = (int64_t)XS.meta[a].x + YS.meta[b].x;
+    }
+    const uint8_t *x0, *y0;
+    int32_t l0;
+    ncd_slot(sx, sy, slen, cap, nslot, 0, p, end, x0, y0, l0);
+    if (no == 1) {
+        if (lane == 0) {
+            singles[p * 2] = ZStream{x0, nullptr, l0, 0};
+            singles[p * 2 + 1] = ZStream{y0, nullptr, l0, 0};
+            concat[p] = ZStream{x0, y0, l0, l0};
+        }
+        return;
+    }
+    const uint8_t *x1, *y1;
+    int32_t l1;
+    ncd_slot(sx, sy, slen, cap, nslot, 1, p, end, x1, y1, l1);
+    bool diff = l1 != l0;
+    if (!diff) {
+        bool d = false;
+        for (int i = lane; i < l0; i += 64) d |= (x0[i] != x1[i]) | (y0[i] != y1[i]);
+        diff = __ballot(d) != 0;
+    }
+    if (lane == 0) {
+        singles[p * 4] = ZStream{x0, nullptr, l0, 0};
+        singles[p * 4 + 1] = ZStream{y0, nullptr, l0, 0};
+        // orientation 1: x = b's string (sy), y = a's (sx)
+        singles[p * 4 + 2] = ZStream{y1, nullptr, diff ? l1 : -1, 0};
+        singles[p * 4 + 3] = ZStream{x1, nullptr, diff ? l1 : -1, 0};
+        concat[p * 2] = ZStream{x0, y0, l0, l0};
+        concat[p * 2 + 1] = ZStream{y1, x1, l1, l1};
+    }
+}
+
+// out[(p * no + o) * ostride + ocol] = NCD of orientation o; a skipped single (-2) is orientation 0's
+// (swapped: min / max do not care).
+__global__ void __launch_bounds__(256)
+k_ncd_slot_finish(const int32_t* __restrict__ cs, const int32_t* __restrict__ cc, int64_t n, int no,
+                  double* __restrict__ out, int64_t ostride, int ocol) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * no) return;
+    const int64_t p = t / no;
+    const int o = (int)(t - p * no);
+    const int32_t* c = cs + p * 2 * no;
+    int32_t c1 = c[2 * o], c2 = c[2 * o + 1];
+    if (c1 == ZLEN_SKIPPED) {
+        c1 = c[0];
+        c2 = c[1];
+    }
+    const double d1 = c1, d2 = c2, d12 = cc[t];
+    const double mn = d1 < d2 ? d1 : d2, mx = d1 < d2 ? d2 : d1;
+    out[t * ostride + ocol] = (d12 - mn) / mx;
 }
 
 // Raw-mode streams for taxi2_zlib_lengths: upper(x_a) (+ upper(y_b) when ys != nullptr).

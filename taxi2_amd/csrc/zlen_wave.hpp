@@ -44,12 +44,16 @@ __host__ __device__ inline int pow2_at_least(int v) {
     return p;
 }
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) / 16 * 16; }
-// LDS layout for streams of at most nmax bytes: [window nmax + 274][key region: P2 x u32][Trees].
-// The key region holds the (hash << 16 | position) sort keys; after the sort it is reused as the
-// sorted positions (u16, first half) and each position's sorted index (u16, second half).
+// LDS layout for streams of at most nmax bytes: [window nmax + 274][key region: npmax x u32][Trees],
+// npmax = nmax - 2 inserted positions at most.  The key region holds the (hash << 16 | position)
+// sort keys; after the sort it is reused as the sorted positions (u16, first half) and each
+// position's sorted index (u16, second half).  The sort network never moves a key past npos (below),
+// so the region is sized by the positions, not by the next power of two (2 050-byte streams, e.g.
+// two 1 025-column aligned strings, would otherwise need a 4 096-key region).
+__host__ __device__ inline int npos_max(int nmax) { return nmax > 4 ? nmax - 2 : 2; }
 __host__ __device__ inline size_t off_keys(int nmax) { return al16((size_t)nmax + zl::MAX_MATCH + 16); }
-__host__ __device__ inline size_t off_idx(int nmax) { return off_keys(nmax) + (size_t)pow2_at_least(nmax) * 2; }
-__host__ __device__ inline size_t off_trees(int nmax) { return al16(off_keys(nmax) + (size_t)pow2_at_least(nmax) * 4); }
+__host__ __device__ inline size_t off_idx(int nmax) { return off_keys(nmax) + (size_t)npos_max(nmax) * 2; }
+__host__ __device__ inline size_t off_trees(int nmax) { return al16(off_keys(nmax) + (size_t)npos_max(nmax) * 4); }
 __host__ __device__ inline size_t lds_bytes(int nmax) { return al16(off_trees(nmax) + sizeof(zl::Trees)); }
 
 __device__ __forceinline__ uint32_t hash3(const uint8_t* w, int p) {
@@ -150,21 +154,38 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     __syncthreads();
     ZLW_T(tw1);
     ZLW_ADD(0, tw1 - tw0);
-    // sorted (hash, position) keys of the inserted positions 0 .. n - 3
+    // sorted (hash, position) keys of the inserted positions 0 .. n - 3.  Bitonic network in its
+    // all-ascending form (each merge starts with a flip: i against the mirror of its block), padded
+    // to P2 with virtual +inf keys: every comparator puts the minimum at the lower index, so a
+    // comparator touching a pad (hi >= npos) never swaps and the pads are never stored.
     const int npos = n >= MIN_MATCH ? n - (MIN_MATCH - 1) : 0;
     const int P2 = pow2_at_least(npos > 1 ? npos : 2);
-    for (int i = lane; i < P2; i += 64) keys[i] = i < npos ? (hash3(win, i) << 16) | (uint32_t)i : 0xFFFFFFFFu;
+    for (int i = lane; i < npos; i += 64) keys[i] = (hash3(win, i) << 16) | (uint32_t)i;
     __syncthreads();
     for (int size = 2; size <= P2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = lane; i < P2 / 2; i += 64) {  // flip: lo and its mirror in the size-block
+            const int half = size >> 1;
+            const int lo = (i / half) * size + (i & (half - 1));
+            const int hi = (lo | (size - 1)) - (i & (half - 1));
+            if (hi < npos) {
+                const uint32_t x = keys[lo], y = keys[hi];
+                if (x > y) {
+                    keys[lo] = y;
+                    keys[hi] = x;
+                }
+            }
+        }
+        __syncthreads();
+        for (int stride = size >> 2; stride > 0; stride >>= 1) {
             for (int i = lane; i < P2 / 2; i += 64) {
                 const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));  // stride is a power of 2
                 const int hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const uint32_t x = keys[lo], y = keys[hi];
-                if ((x > y) == up) {
-                    keys[lo] = y;
-                    keys[hi] = x;
+                if (hi < npos) {
+                    const uint32_t x = keys[lo], y = keys[hi];
+                    if (x > y) {
+                        keys[lo] = y;
+                        keys[hi] = x;
+                    }
                 }
             }
             __syncthreads();

@@ -41,11 +41,13 @@ from .common import (Results, console_report, create_parents, fixed_decimals, fo
 
 def self_strings(eng, st, seqs: list, idx, scores: tuple) -> list:
     """Each sequence idx[k] aligned with itself (versus_all.py:549's diagonal rule, the diagonal pairs
-    of aligned_pairs.txt).  When a match scores > 0 and no gap score is positive the first
-    alignment is the identity -- the diagonal scores len * match and any path with gaps trades at
-    least one match for gaps -- so no alignment is run; otherwise the aligner's own strings."""
-    m, _, io, ie, eo, ee = scores
-    if m > 0 and max(io, ie, eo, ee) <= 0:
+    of aligned_pairs.txt).  When a match scores > 0, no mismatch scores more than a match and no gap
+    score is positive, the first alignment is the identity -- the diagonal scores len * match, a
+    path with gaps trades at least one match for gaps and a shifted diagonal pairs mismatching bytes
+    at most -- so no alignment is run; otherwise the aligner's own strings (e.g. mismatch > match:
+    a one-column shift of a 10-base sequence can outscore the identity)."""
+    m, mi, io, ie, eo, ee = scores
+    if m > 0 and mi <= m and max(io, ie, eo, ee) <= 0:
         return [(seqs[i].seq, seqs[i].seq) for i in np.asarray(idx).tolist()]
     return eng.align_strings(st, st, idx, idx, scores)
 
@@ -237,38 +239,31 @@ class VersusAll:
                 out = np.empty((count, 2, M))
                 step = (1 << 20) if align else (1 << 24)
                 if nidx:
-                    step = min(step, 1 << 16)
+                    step = min(step, 1 << 18 if align else 1 << 16)
                 for c0 in range(0, count, step):
                     c = min(step, count - c0)
-                    if cidx:
-                        blk = eng.all_pairs(st, k0 + c0, c, clabels, scores)
-                        if align:
-                            out[c0 : c0 + c][:, :, cidx] = blk
-                        else:  # counters are symmetric: one value serves both ordered rows
+                    if align:  # every metric, NCD included, from the one alignment of each ordered pair
+                        out[c0 : c0 + c] = eng.all_pairs(st, k0 + c0, c, labels, scores)
+                    else:
+                        if cidx:  # counters are symmetric: one value serves both ordered rows
+                            blk = eng.all_pairs(st, k0 + c0, c, clabels, scores)
                             out[c0 : c0 + c][:, 0, cidx] = blk
                             out[c0 : c0 + c][:, 1, cidx] = blk
-                    if nidx:
-                        a, b = tri_pairs(n, k0 + c0, c)
-                        v = eng.ncd_pairs(st, st, a, b, scores, aligned=align, both=True)
-                        for k in nidx:
-                            out[c0 : c0 + c][:, :, k] = v
+                        if nidx:
+                            a, b = tri_pairs(n, k0 + c0, c)
+                            v = eng.ncd_pairs(st, st, a, b, scores, aligned=False, both=True)
+                            for k in nidx:
+                                out[c0 : c0 + c][:, :, k] = v
                     report(self.progress_handler, "distance.x.id", min(total, 2 * M * (k0 + c0 + c)), total)
                 return out.reshape(count, 2 * M)
 
             walked = False
-            if pairs_fh is not None and cidx and walk_strings_ok(scores, seqs):
-                walked = (self._tri_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh)
-                          or self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, pairs_fh))
-            if walked:  # counter metrics and aligned_pairs.txt done; NCD (if any) from the triangle
-                if nidx:
-                    for k0 in range(0, npairs, 1 << 16):
-                        c = min(1 << 16, npairs - k0)
-                        a, b = tri_pairs(n, k0, c)
-                        v = eng.ncd_pairs(st, st, a, b, scores, aligned=True, both=True)
-                        for k in nidx:
-                            D[a, b, k] = v[:, 0]
-                            D[b, a, k] = v[:, 1]
-            else:
+            if pairs_fh is not None and walk_strings_ok(scores, seqs):
+                # every metric (NCD from the same walks' strings) and aligned_pairs.txt from one fill
+                every = list(range(M))
+                walked = (self._tri_with_pairs(seqs, eng, st, D, every, labels, scores, pairs_fh)
+                          or self._rows_with_pairs(seqs, eng, st, D, every, labels, scores, pairs_fh))
+            if not walked:
                 res = self._run_pairs(n, npairs, compute)
                 a, b = tri_pairs(n)
                 D[a, b] = res[:, :M]
@@ -342,7 +337,8 @@ class VersusAll:
         # text, and into D while the GPU aligns the next block
         Dd = None
         if n * n * Mc * 8 <= DEVICE_D_BYTES:
-            Dd = torch.full((n, n, Mc), float("nan"), dtype=torch.float64, device=dev)
+            with torch.cuda.stream(stream):  # filled on `stream`, ahead of the scatters queued there
+                Dd = torch.full((n, n, Mc), float("nan"), dtype=torch.float64, device=dev)
         stage = [None, None, None]  # pinned buffer, its event, the rows (x0, x1) it holds
 
         def rows_out(x0: int, x1: int) -> None:  # queue rows [x0, x1) of Dd to the staging buffer

@@ -23,13 +23,30 @@ WORKER = textwrap.dedent(
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     total, B, steps, warm = bench.N_SEQS * (bench.N_SEQS - 1) // 2, 1 << 19, 6, 2
-    mine = [bench.step_block(s, rank, world, B, total) for s in range(warm + steps)]
+    mine = [bench.step_block(s, rank, world, B, total, steps) for s in range(steps)]
     got = [None] * world
     dist.all_gather_object(got, mine)
     elapsed = bench.max_over_ranks(1.0 + rank, world)    # rank 1 is the slow one
     value = bench.job_value(steps, B, world, elapsed)
+    # the step pipeline on CPU: each step's result block names (rank, step); the gather of every
+    # step must hold every rank's block of that step, and the line's two times are reported
+    b, m = 64, 4
+    pipe = bench.StepPipeline(world, b, m, torch.device("cpu"))
+    out = [torch.empty((b, 2, m), dtype=torch.float64) for _ in range(2)]
+    seen = []
+
+    def kernel(k, slot):
+        out[slot].fill_(1000.0 * rank + k)
+
+    for k in range(warm + steps):
+        pipe.step(k, kernel, out, None, record=k >= warm)
+        g = pipe.gathered.view(world, b, 2, m)
+        seen.append([float(g[r].min()) for r in range(world)] + [float(g[r].max()) for r in range(world)])
+    pipe.drain()
     with open(os.environ["OUT"] + f".{{rank}}", "w") as fh:
-        json.dump({{"blocks": got, "elapsed": elapsed, "value": value}}, fh)
+        json.dump({{"blocks": got, "elapsed": elapsed, "value": value, "seen": seen,
+                   "kernel_ms": pipe.kernel_ms(), "gather_ms": pipe.gather_ms(), "nk": len(pipe.kev),
+                   "ng": len(pipe.gev)}}, fh)
     dist.destroy_process_group()
     """
 )
@@ -48,10 +65,16 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     res = [json.loads((tmp_path / f"res.{k}").read_text()) for k in range(2)]
     B = 1 << 19
+    total = 50_000 * 49_999 // 2
     starts = [b for blocks in res[0]["blocks"] for b in blocks]
     assert len(set(starts)) == len(starts)
     spans = sorted(starts)
     assert all(b - a >= B for a, b in zip(spans, spans[1:]))  # no two blocks overlap
+    assert spans[0] == 0 and spans[-1] == total - B             # the whole triangle, first to last pair
     for rec in res:
         assert rec["elapsed"] == 2.0                        # the slower rank's time on both
         assert rec["value"] == 6 * B * 2 / 2.0              # all ranks' pairs / that time
+        assert rec["nk"] == 6 and rec["ng"] == 6            # timed steps only, kernel and gather apart
+        assert rec["kernel_ms"] >= 0 and rec["gather_ms"] >= 0
+        for k, row in enumerate(rec["seen"]):               # step k's gather: rank r's block = 1000 r + k
+            assert row == [float(k), 1000.0 + k, float(k), 1000.0 + k]

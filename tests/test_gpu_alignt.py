@@ -1,7 +1,11 @@
-"""GPU parity of the trace-and-walk aligners (taxi2_amd/csrc/alignt_kernel.hpp and its packed
-two-pairs-per-lane form alignt2_kernel.hpp, the default for Gotoh scores up to 1 024 columns):
-the fill stores one byte of tie information per cell and a walker wave traces both Biopython
-first paths (priority M>Ix>Iy for (a, b), M>Iy>Ix for (b, a)).
+"""GPU parity of the trace-and-walk aligners: the fill stores the tie information of every cell and
+a walker wave traces both Biopython first paths (priority M>Ix>Iy for (a, b), M>Iy>Ix for (b, a)).
+Which kernel runs a case: with the DEFAULT scores and every sequence <= 1 024 columns, the
+row-shared packed aligner k_alignr (alignr_kernel.hpp, the headline kernel) for the triangle, the
+rectangle and the string-emitting launches; other Gotoh score sets within int16, and 1 025 - 2 048
+columns, the packed k_alignt2 (alignt2_kernel.hpp); TAXI2_NO_PACKED=1 the 32-bit k_alignt
+(alignt_kernel.hpp); TAXI2_NO_ALIGNR=1 keeps default scores on k_alignt2
+(test_alignr_off_matches_default pins that k_alignt2 default-score path bit for bit).
 
 Every case is checked against the C restatement (oracle/taxi2_oracle.c, scores bit-exact,
 p / p-gaps bit-exact, jc / k2p within 1e-12) AND against the forward-carry kernels
@@ -147,4 +151,28 @@ def test_alignt2_value_range_extremes(engine, oracle_c):
     # the identical full-length pair scores its length (the largest value the fill holds)
     k = int(np.flatnonzero((a == 0) & (b == 1))[0])
     assert int(gsc[k]) == L
+    st.free()
+
+
+def test_alignr_off_matches_default(engine, oracle_c):
+    """TAXI2_NO_ALIGNR=1 runs the default scores on k_alignt2 instead of k_alignr: both must give the
+    same scores and metrics bit for bit (triangle and rectangle, tie-heavy ragged sets up to the
+    1 024-column capacity), and the oracle's."""
+    from taxi2_amd._native import tri_pairs
+
+    seqs = _tie_heavy(20, 1000, 0x6A) + ["ACGT" * 256, "A", "", "N" * 40]
+    seqs.append(seqs[0])
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    sc = SCORE_SETS["default"]
+    got, gsc = engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True)
+    off, osc = _with_env({"TAXI2_NO_ALIGNR": "1"},
+                         lambda: engine.all_pairs(st, 0, len(a), METRICS, sc, with_scores=True))
+    assert np.array_equal(got.view(np.int64), off.view(np.int64)) and np.array_equal(gsc, osc)
+    exp, esc = oracle_c.batch(seqs, a, b, align=True, scores=sc)
+    assert np.array_equal(gsc, esc)
+    assert_metrics_equal(got, exp)
+    r_on = engine.rect_pairs(st, st, 3, 9, METRICS, sc)
+    r_off = _with_env({"TAXI2_NO_ALIGNR": "1"}, lambda: engine.rect_pairs(st, st, 3, 9, METRICS, sc))
+    assert np.array_equal(r_on.view(np.int64), r_off.view(np.int64))
     st.free()

@@ -1,4 +1,6 @@
-"""GPU parity of the packed aligner's trace band (taxi2_amd/csrc/alignt2_kernel.hpp a2_band_blocks):
+"""GPU parity of the packed aligners' trace band (the row-shared k_alignr, alignr_kernel.hpp, for the
+default scores up to 1 024 columns; k_alignt2, alignt2_kernel.hpp a2_band_blocks, for the other
+score sets and shapes; both requeue escapes to k_alignt2_queued's full-trace pass):
 the fill stores only the diagonal strip j - i in [min(0, nB - nA) - band, max(0, nB - nA) + band]
 of each pair's trace, a walk that would leave it queues the pair, and a second launch redoes the
 queued pairs with the full trace.  Results must not depend on the band: every case against the

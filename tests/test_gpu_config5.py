@@ -114,3 +114,46 @@ def test_column_view_matches_task_order(tmp_path, engine, monkeypatch):
         assert np.array_equal(x.count, y.count)
         for u, v in ((x.mean, y.mean), (x.min, y.min), (x.max, y.max)):
             assert np.array_equal(_bits(np.nan_to_num(u, nan=-7.0)), _bits(np.nan_to_num(v, nan=-7.0))), name
+
+
+@pytest.mark.timeout(600)
+def test_aligned_streamed_reductions_vs_dense_and_oracle(tmp_path, engine, oracle_c):
+    """Config 5's aligned form (NW / Gotoh on a stated subset) through the streamed
+    reductions path at N = 2 000 x 600 bp of its generator: every subset statistic equals the dense
+    path's sequential host aggregation bit for bit, the row minima equal the dense matrix's first
+    minima (x100, diagonal None), and sampled rows equal the C restatement's alignments."""
+    from bench_secondary import build_config5_task as build_task
+
+    n, L = 2000, 600
+    streamed, _, _ = build_task(n, L, engine, tmp_path / "stream", 0.05, aligned=True)  # many blocks
+    streamed.start()
+    dense, _, _ = build_task(n, L, engine, tmp_path / "dense", 0.05, aligned=True)
+    dense.params.engine.stream = False
+    dense.params.engine.row_minima = None
+    dense.start()
+    for name in ("genera", "species"):
+        a, b = dense.subset_stats[name], streamed.subset_stats[name]
+        assert a.subsets == b.subsets
+        assert np.array_equal(a.count, b.count)
+        for x, y in ((a.mean, b.mean), (a.min, b.min), (a.max, b.max)):
+            assert np.array_equal(_bits(np.nan_to_num(x, nan=-7.0)), _bits(np.nan_to_num(y, nan=-7.0))), name
+    D = dense.distances
+    v = D[:, :, 0] * 100.0
+    v[np.arange(n), np.arange(n)] = np.nan
+    v = np.where(np.isfinite(v), v, np.inf)
+    j = np.argmin(v, axis=1)
+    idx, d = streamed.row_minima
+    fin = np.isfinite(v[np.arange(n), j])
+    assert np.array_equal(idx[fin], j[fin]) and (idx[~fin] == -1).all()
+    assert np.array_equal(_bits(d[fin]), _bits(v[np.arange(n), j][fin]))
+    seqs = [s.normalize().seq for s in streamed.input.sequences]
+    for x in (0, 777, n - 1):
+        pa = np.full(n, x, dtype=np.int64)
+        pb = np.arange(n, dtype=np.int64)
+        exp, _ = oracle_c.batch(seqs, pa, pb, align=True, scores=(1, -1, -8, -1, -1, -1), metrics=("p",),
+                                threads=16)
+        e = exp[:, 0, 0]
+        got = D[x, :, 0]
+        m = np.arange(n) != x
+        assert np.array_equal(np.isfinite(e[m]), np.isfinite(got[m]))
+        assert np.array_equal(_bits(e[m][np.isfinite(e[m])]), _bits(got[m][np.isfinite(got[m])]))

@@ -1,0 +1,217 @@
+"""GPU: NCD from the aligners' own string slots -- every metric of a pair from ONE fill, as
+versus_all.py:546-552 feeds one alignment per ordered pair to p / p-gaps / jc / k2p AND ncd
+(distances.py:351-358).
+
+The oracle is the Python restatement (oracle/restatement.py: the first Biopython alignment of each
+ordered pair + alfpy's NCD over Python's zlib 1.2.11).  The packed walkers' strings
+(all_pairs / tri_strings_dev / rect_strings_dev with "ncd", taxi2_ncd_slots_dev) are also checked
+against the round-1 trace kernels' strings (TAXI2_NO_WALK_STRINGS=1 forces them), bit for bit.
+"""
+
+from __future__ import annotations
+
+import os
+import random
+
+import numpy as np
+import pytest
+
+from tests.seqgen import family_sequences, mutate, random_sequences
+
+pytestmark = pytest.mark.gpu
+
+DEFAULT = (1, -1, -8, -1, -1, -1)
+GENERIC1 = (2, -3, -5, -2, -3, -2)  # best-open fill, one extend for internal and end gaps
+GENERIC = (2, -3, -5, -2, -1, -1)   # tagged sign-digit fill
+FOUR = ("p", "p-gaps", "jc", "k2p")
+
+
+def tie_heavy(seed: int) -> list[str]:
+    """Two-letter runs, families with indels, N runs, one short / one long sequence whose alignment
+    is mostly end gaps (its concatenation exceeds the first zlen pass's likely length: the redo
+    pass), and an empty sequence."""
+    from oracle import restatement as R
+
+    rng = random.Random(seed)
+    fam = family_sequences(4, 300, seed, ancestors=2)
+    two = ["".join(rng.choice("AC") for _ in range(rng.randrange(40, 160))) for _ in range(4)]
+    base = random_sequences(3, 60, 260, seed + 1, "ACGTN", n_rate=0.05)
+    seqs = fam + two + base + mutate(base[:2], seed + 2, rate=0.2)
+    seqs += ["A" * 150 + "C" * 150, "C" * 150 + "G" * 150, ""]
+    return [R.normalize(s) for s in seqs]
+
+
+def oracle_ncd(seqs, a, b, scores):
+    from oracle import restatement as R
+
+    sc = R.Scores(*scores)
+    out = np.empty((len(a), 2))
+    for k, (i, j) in enumerate(zip(a, b)):
+        ax, ay, _ = R.align(seqs[i], seqs[j], sc)
+        by, bx, _ = R.align(seqs[j], seqs[i], sc)
+        out[k, 0] = R.ncd(ax, ay)
+        out[k, 1] = R.ncd(by, bx)
+    return out
+
+
+def same(x, y) -> bool:
+    """Bit-identical, NaN positions included."""
+    return np.array_equal(np.asarray(x).view(np.int64), np.asarray(y).view(np.int64))
+
+
+@pytest.mark.parametrize("scores", [DEFAULT, GENERIC1, GENERIC])
+def test_all_pairs_with_ncd_one_fill(engine, scores):
+    from taxi2_amd._native import tri_pairs
+
+    seqs = tie_heavy(3)
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    npairs = n * (n - 1) // 2
+    five = engine.all_pairs(st, 0, npairs, FOUR + ("ncd",), scores)
+    four = engine.all_pairs(st, 0, npairs, FOUR, scores)
+    assert same(five[..., :4], four), "the counter metrics change when NCD rides the same fill"
+    a, b = tri_pairs(n)
+    exp = oracle_ncd(seqs, a, b, scores)
+    assert np.array_equal(five[..., 4], exp), "NCD differs from the restatement"
+    # NCD first in the list, twice: every NCD column is written, the others stay the counters
+    mixed = engine.all_pairs(st, 0, npairs, ("ncd", "p", "ncd"), scores)
+    assert np.array_equal(mixed[..., 0], exp) and np.array_equal(mixed[..., 2], exp)
+    assert same(mixed[..., 1], four[..., 0])
+    st.free()
+
+
+def test_walker_ncd_equals_trace_kernel_ncd(engine):
+    """ncd_pairs on the packed walkers' strings == on the trace kernels' strings (TAXI2_NO_WALK_STRINGS),
+    both orientations, tie-heavy pairs; and the host all_pairs fallback (trace strings) agrees too."""
+    seqs = tie_heavy(5)
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    rng = random.Random(7)
+    xs = np.array([rng.randrange(n) for _ in range(300)])
+    ys = np.array([rng.randrange(n) for _ in range(300)])
+    npairs = n * (n - 1) // 2
+    for scores in (DEFAULT, GENERIC1):
+        walk = engine.ncd_pairs(st, st, xs, ys, scores, aligned=True, both=True)
+        os.environ["TAXI2_NO_WALK_STRINGS"] = "1"
+        try:
+            trace = engine.ncd_pairs(st, st, xs, ys, scores, aligned=True, both=True)
+            fb = engine.all_pairs(st, 0, npairs, FOUR + ("ncd",), scores)
+        finally:
+            del os.environ["TAXI2_NO_WALK_STRINGS"]
+        assert np.array_equal(walk, trace)
+        assert same(fb, engine.all_pairs(st, 0, npairs, FOUR + ("ncd",), scores))
+    st.free()
+
+
+def test_all_pairs_dev_with_ncd_and_slots_entry(engine):
+    """The device form (caller's stream) and taxi2_ncd_slots_dev on tri_strings_dev slots give the
+    host path's values; rect_strings_dev with "ncd" gives the (q, r) orientation."""
+    import torch
+
+    from taxi2_amd._native import tri_pairs
+
+    seqs = family_sequences(12, 700, 9, ancestors=3) + tie_heavy(11)[:6]
+    st = engine.upload(seqs, align=True)
+    n = len(seqs)
+    npairs = n * (n - 1) // 2
+    host = engine.all_pairs(st, 0, npairs, FOUR + ("ncd",), DEFAULT)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        out = torch.empty((npairs, 2, 5), dtype=torch.float64, device=dev)
+        engine.all_pairs_dev(st, 0, npairs, FOUR + ("ncd",), out.data_ptr(), DEFAULT, None, s.cuda_stream)
+        cap = 2 * max(len(x) for x in seqs) + 1
+        d = torch.empty((npairs, 2, 2), dtype=torch.float64, device=dev)
+        sx = torch.empty((npairs, 2, cap), dtype=torch.uint8, device=dev)
+        sy = torch.empty((npairs, 2, cap), dtype=torch.uint8, device=dev)
+        sl = torch.empty((npairs, 2), dtype=torch.int32, device=dev)
+        engine.tri_strings_dev(st, 0, npairs, ("p", "ncd"), d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
+                               sl.data_ptr(), DEFAULT, s.cuda_stream)
+        a, b = tri_pairs(n)
+        lens = np.array([len(x) for x in seqs])
+        end = torch.as_tensor(lens[a] + lens[b], device=dev)
+        v = torch.empty((npairs, 2), dtype=torch.float64, device=dev)
+        engine.ncd_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 2, end.data_ptr(), npairs,
+                             int(lens.max()), v.data_ptr(), stream=s.cuda_stream)
+        v1 = torch.empty((npairs,), dtype=torch.float64, device=dev)
+        engine.ncd_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 1, end.data_ptr(), npairs,
+                             int(lens.max()), v1.data_ptr(), stream=s.cuda_stream)
+        R_ = n
+        rc = torch.empty((3 * R_, 2), dtype=torch.float64, device=dev)
+        rsx = torch.empty((3 * R_, cap), dtype=torch.uint8, device=dev)
+        rsy = torch.empty((3 * R_, cap), dtype=torch.uint8, device=dev)
+        rsl = torch.empty((3 * R_,), dtype=torch.int32, device=dev)
+        engine.rect_strings_dev(st, st, 2, 5, ("ncd", "k2p"), rc.data_ptr(), cap, rsx.data_ptr(), rsy.data_ptr(),
+                                rsl.data_ptr(), DEFAULT, s.cuda_stream)
+    s.synchronize()
+    assert same(out.cpu().numpy(), host)
+    assert same(d.cpu().numpy()[..., 1], host[..., 4]) and same(d.cpu().numpy()[..., 0], host[..., 0])
+    assert same(v.cpu().numpy(), host[..., 4])
+    assert same(v1.cpu().numpy(), host[:, 0, 4])
+    exp = oracle_ncd(seqs, np.repeat(np.arange(2, 5), R_), np.tile(np.arange(R_), 3), DEFAULT)
+    assert np.array_equal(rc.cpu().numpy()[:, 0], exp[:, 0])
+    st.free()
+
+
+@pytest.mark.parametrize("scores", [DEFAULT, GENERIC1])
+def test_task_ncd_with_aligned_pairs_walked(tmp_path, engine, scores):
+    """VersusAll with aligned_pairs.txt on (the walked one-fill path) and p + ncd: the NCD values come
+    from the walks' own strings and equal the restatement; the files equal the non-walked path's."""
+    from oracle import restatement as R
+    from taxi2_amd.distances import DistanceMetric
+    from taxi2_amd.sequences import Sequence, Sequences
+    from taxi2_amd.tasks import VersusAll
+
+    raw = tie_heavy(13)[:12]
+    seqs = [Sequence(f"s{k}", s) for k, s in enumerate(raw)]
+
+    def run(out, env):
+        if env:
+            os.environ["TAXI2_PAIRS_RECT"] = "1"
+        try:
+            t = VersusAll()
+            t.engine, t.progress_handler, t.work_dir = engine, None, out
+            t.input.sequences = Sequences(seqs)
+            t.params.pairs.scores = dict(zip(("match_score", "mismatch_score", "internal_open_gap_score",
+                                              "internal_extend_gap_score", "end_open_gap_score",
+                                              "end_extend_gap_score"), scores))
+            t.params.distances.metrics = [DistanceMetric.Uncorrected(), DistanceMetric.NCD()]
+            t.start()
+            return t
+        finally:
+            os.environ.pop("TAXI2_PAIRS_RECT", None)
+
+    t1 = run(tmp_path / "tri", False)
+    t2 = run(tmp_path / "rect", True)
+    assert t1.pairs_walked and t2.pairs_walked
+    sc = R.Scores(*scores)
+    n = len(raw)
+    for i in range(n):
+        for j in range(n):
+            if i == j:
+                continue
+            ax, ay, _ = R.align(R.normalize(raw[i]), R.normalize(raw[j]), sc)
+            assert t1.distances[i, j, 1] == R.ncd(ax, ay), (i, j)
+    for f in ("distances/linear.tsv", "distances/matricial/ncd.tsv", "align/aligned_pairs.txt", "summary.tsv"):
+        assert (tmp_path / "tri" / f).read_bytes() == (tmp_path / "rect" / f).read_bytes(), f
+
+
+def test_self_strings_mismatch_above_match(engine):
+    """with mismatch > match the self alignment need not be the identity (a one-column
+    shift of a 10-base sequence scores 9 * 5 - 2 = 43 against 10): self_strings must align."""
+    from oracle import restatement as R
+    from taxi2_amd.tasks.versus_all import self_strings
+    from taxi2_amd.sequences import Sequence
+
+    scores = (1, 5, -1, -1, -1, -1)
+    raw = ["ACGTACGTAC", "AAAACCCCGG", "ACGT" * 20, "A"]
+    seqs = [Sequence(f"s{k}", s) for k, s in enumerate(raw)]
+    st = engine.upload(raw, align=True)
+    got = self_strings(engine, st, seqs, np.arange(len(raw)), scores)
+    ref = engine.align_strings(st, st, np.arange(len(raw)), np.arange(len(raw)), scores)
+    assert got == ref
+    for k, s in enumerate(raw):
+        ax, ay, _ = R.align(s, s, R.Scores(*scores))
+        assert got[k] == (ax, ay)
+    assert got[0] != (raw[0], raw[0])  # the shifted alignment, not the identity
+    st.free()

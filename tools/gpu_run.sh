@@ -31,16 +31,20 @@ export TMPDIR=/tmp
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 BENCH="python3 $R/bench.py --secondary= --no-cpu-baseline"
 PMC_OPTS="--kernel-include-regex k_align --output-format csv"
+# the library's baked-in source hash beside the tree's, first line of every test log
+BUILD_LINE="from taxi2_amd._native import build_info; print('engine build:', build_info())"
 
 run_step() {
     local s=$1
     case "$s" in
     suite)
-        (cd "$R" && timeout -k 10 1000 $PYT tests -m gpu > "$OUT/suite.log" 2>&1) ;;
+        (cd "$R" && python3 -c "$BUILD_LINE" > "$OUT/suite.log" 2>&1 && \
+            timeout -k 10 1000 $PYT tests -m gpu >> "$OUT/suite.log" 2>&1) ;;
     tests:*)
         local files=""
         for f in $(echo "${s#tests:}" | tr ',' ' '); do files="$files tests/$f.py"; done
-        (cd "$R" && timeout -k 10 900 $PYT $files > "$OUT/tests_$(echo "${s#tests:}" | tr ',' '_').log" 2>&1) ;;
+        local log="$OUT/tests_$(echo "${s#tests:}" | tr ',' '_').log"
+        (cd "$R" && python3 -c "$BUILD_LINE" > "$log" 2>&1 && timeout -k 10 900 $PYT $files >> "$log" 2>&1) ;;
     smoke)
         (cd "$R" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1) ;;
     bench)
