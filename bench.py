@@ -173,7 +173,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores (max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    ap.add_argument("--secondary", default="allmetrics,config4,task,config5,config5_aligned",
+    ap.add_argument("--secondary", default="allmetrics,config4,task,config5,config5_aligned,prealigned",
                     help="secondary legs after the headline (one GPU only; bench_secondary.py); '' = none")
     return ap.parse_args()
 

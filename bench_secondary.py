@@ -14,6 +14,8 @@ into the same record (bench.py's ``secondary`` key), each on its own synthetic, 
   every one of the 4e10 ordered pairs evaluated and reduced on the GPU.
 * ``config5_aligned``: config 5's aligned form on a stated subset (N = 12 000 of its generator):
   VersusAll.start() with Gotoh alignment of every pair, four metrics x100, streamed reductions.
+* ``prealigned``: the pre-aligned path alone: config 2 on the ca2000 stand-in file and config 5's
+  tile kernel over all 2.0e10 pairs, with its VALU-issue and traffic rooflines.
 * ``config4``: versusReference slice, 4 096 queries x 10 000 references of 650 bp (seed 0x7A13
   generator), Gotoh align + p, closest reference + extras on the GPU (versus_reference.py:184-188,
   124-129).
@@ -189,6 +191,91 @@ def leg_config5_aligned(eng, n: int = 12_000, L: int = 1000) -> dict:
     }
 
 
+PREALIGNED_CEILING_JSON = ROOT / "profiles" / "prealigned_ceiling.json"
+
+
+def leg_prealigned(eng) -> dict:
+    """The pre-aligned path (params.pairs.align = False, versus_all.py:546-552 on the raw rows):
+    config 2 on BASELINE.md's stand-in file (samples/Taxi2test1_ca2000.tab, 1 999 rows, the full
+    pair space, p / jc / k2p) and config 5's tile kernel alone over all 2.0e10 unordered pairs of
+    200 000 x 1 000 synthetic rows (2^26-pair launches, outputs overwritten in HBM), kernel time from
+    HIP events on the launch stream.  With profiles/prealigned_ceiling.json (tools/tile_ceiling.py:
+    the tile kernel's PMC VALU count per pair-word and its instruction mix priced with the measured
+    issue costs) the kernel's VALU-issue fraction and its real-traffic fraction are attached."""
+    import json
+
+    import torch
+
+    from taxi2_amd.sequences import SequenceHandler, Sequences
+
+    _log("prealigned: config2 (ca2000 stand-in) and config5's tile kernel at full size")
+    out = {}
+    path = ROOT / "tests" / "golden" / "samples" / "Taxi2test1_ca2000.tab"
+    # TAXI2_PREALIGNED_PARTS=config5: the tile kernel alone (a PMC pass of just its launches)
+    parts = os.environ.get("TAXI2_PREALIGNED_PARTS", "config2,config5").split(",")
+    if path.exists() and "config2" in parts:
+        seqs = [x.seq for x in Sequences.fromPath(path, SequenceHandler.Tabfile, idHeader="seqid",
+                                                   seqHeader="sequence")]
+        st = eng.upload(seqs, align=False)
+        n = len(seqs)
+        total = n * (n - 1) // 2
+        o = torch.empty((total, 3), dtype=torch.float64, device="cuda")
+        stream = torch.cuda.Stream()
+        eng.all_pairs_dev(st, 0, total, ("p", "jc", "k2p"), o.data_ptr(), None, None, stream.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record(stream)
+        for _ in range(reps):
+            eng.all_pairs_dev(st, 0, total, ("p", "jc", "k2p"), o.data_ptr(), None, None, stream.cuda_stream)
+        e1.record(stream)
+        e1.synchronize()
+        dt = e0.elapsed_time(e1) * 1e-3 / reps
+        st.free()
+        del o
+        out["config2_ca2000"] = {
+            "workload": f"config 2 stand-in: samples/Taxi2test1_ca2000.tab ({n} rows, 416-618 columns), pre-aligned "
+                        f"p/jc/k2p over all {total} unordered pairs, outputs in HBM",
+            "pairs": total, "seconds": dt, "pairs_per_s": total / dt}
+    n, L = 200_000, 1000
+    buf, offs = prealigned_rows(n, L, 0x7A14)
+    st = eng.upload_packed(buf, offs, align=False)
+    del buf
+    total = n * (n - 1) // 2
+    B = 1 << 26
+    o = torch.empty((B, 3), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.Stream()
+    eng.all_pairs_dev(st, 0, B, ("p", "jc", "k2p"), o.data_ptr(), None, None, stream.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    launches = 0
+    for k0 in range(0, total, B):
+        eng.all_pairs_dev(st, k0, min(B, total - k0), ("p", "jc", "k2p"), o.data_ptr(), None, None, stream.cuda_stream)
+        launches += 1
+    e1.record(stream)
+    e1.synchronize()
+    dt = e0.elapsed_time(e1) * 1e-3
+    st.free()
+    words = (L + 31) // 32
+    rec = {"workload": f"config 5 pre-aligned, tile kernel alone: {n} x {L} synthetic rows (seed 0x7A14), p/jc/k2p, "
+                       f"all {total} unordered pairs in {launches} launches of 2^26, outputs overwritten in HBM",
+           "pairs": total, "seconds": dt, "pairs_per_s": total / dt, "ms_per_launch": dt * 1e3 / launches,
+           "pair_words_per_s": total * words / dt, "output_GBps": total * 24 / dt / 1e9}
+    if PREALIGNED_CEILING_JSON.exists():
+        c = json.loads(PREALIGNED_CEILING_JSON.read_text())
+        instr_rate = total * words * c["valu_instr_per_pair_word"] / dt  # wave-instructions / s
+        ach = instr_rate / (1024 * c["clock_ghz"] * 1e9)
+        rec["compute_roofline"] = {
+            "bound": "valu-issue", "unit": "wave64 VALU instructions per SIMD-cycle", "achieved": ach,
+            "peak": c["ceiling_instr_per_simd_clk"], "frac": ach / c["ceiling_instr_per_simd_clk"],
+            "full_rate_peak": 1 / 2.28, "frac_of_full_rate": ach * 2.28, "source": c["source"]}
+        if c.get("hbm_bytes_per_pair"):
+            gbps = c["hbm_bytes_per_pair"] * total / dt / 1e9
+            rec["traffic_roofline"] = {"bound": "hbm", "achieved": gbps, "peak": 8000.0, "unit": "GB/s",
+                                       "frac": gbps / 8000.0, "bytes_per_pair": c["hbm_bytes_per_pair"]}
+    out["config5_tile"] = rec
+    return out
+
+
 def leg_config4(eng, q_slice: int = 4096, R: int = 10_000, L: int = 650) -> dict:
     from taxi2_amd.synth import family_sequences
 
@@ -280,7 +367,8 @@ def leg_allmetrics(eng, seqset, n_seqs: int, count: int = 1 << 17) -> dict:
     }
 
 
-def run_all(eng, seqset, n_seqs: int, legs=("allmetrics", "config4", "task", "config5", "config5_aligned")) -> dict:
+def run_all(eng, seqset, n_seqs: int,
+            legs=("allmetrics", "config4", "task", "config5", "config5_aligned", "prealigned")) -> dict:
     out = {}
     for name in legs:
         t0 = time.perf_counter()
@@ -291,6 +379,8 @@ def run_all(eng, seqset, n_seqs: int, legs=("allmetrics", "config4", "task", "co
                 out[name] = leg_config5(eng)
             elif name == "config5_aligned":
                 out[name] = leg_config5_aligned(eng)
+            elif name == "prealigned":
+                out[name] = leg_prealigned(eng)
             elif name == "config4":
                 out[name] = leg_config4(eng)
             elif name == "allmetrics":

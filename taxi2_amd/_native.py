@@ -728,7 +728,7 @@ class Engine:
         return out
 
     def format_rows(self, vals: np.ndarray, row_pre, col_pre=None, *, decimals: int = 4,
-                    missing: str = "NA") -> bytes:
+                    missing: str = "NA", view: bool = False):
         """Writer text (taxi2_format_rows): ``vals`` (nrows, ncols, nm) -> linear rows
         ``row_pre TAB col_pre (TAB value){nm} LF`` per cell; (nrows, ncols) with ``col_pre=None``
         -> matrix rows ``row_pre (TAB value){ncols} LF``.  Values as Python "%.{decimals}f"."""
@@ -739,10 +739,10 @@ class Engine:
         if v.ndim != 3:
             raise ValueError("vals must be (nrows, ncols, nm) (linear) or (nrows, ncols) (matrix)")
         nrows, ncols, nm = v.shape
-        return self._format(mode, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing)
+        return self._format(mode, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing, view=view)
 
     def format_ragged(self, vals: np.ndarray, row_start, cols, row_pre, col_pre=None, *, ncols: int | None = None,
-                      decimals: int = 4, missing: str = "NA") -> bytes:
+                      decimals: int = 4, missing: str = "NA", view: bool = False):
         """Writer text for ragged rows (taxi2_format_ragged): row r formats tokens
         [row_start[r], row_start[r+1]) of ``vals`` (ntok, nm) / (ntok,), token g at column cols[g];
         linear with ``col_pre``, matrix rows otherwise (``ncols`` bounds cols then)."""
@@ -757,10 +757,11 @@ class Engine:
         mode = 0 if col_pre is not None else 1
         if ncols is None:
             ncols = len(col_pre) if col_pre is not None else (int(cs.max()) + 1 if len(cs) else 0)
-        return self._format(mode, v, nrows, rs, cs, ncols, v.shape[1], row_pre, col_pre, decimals, missing)
+        return self._format(mode, v, nrows, rs, cs, ncols, v.shape[1], row_pre, col_pre, decimals, missing, view=view)
 
     def format_summary(self, vals: np.ndarray, row_pre, col_pre, row_suf, col_suf, row_codes, col_codes, *,
-                       has_genera: bool, has_species: bool, decimals: int = 4, missing: str = "NA") -> bytes:
+                       has_genera: bool, has_species: bool, decimals: int = 4, missing: str = "NA",
+                       view: bool = False):
         """summary.tsv lines (taxi2_format_summary) for ``vals`` (nrows, ncols, nm): row_suf / col_suf
         = 2 strings per row / column (extras with leading TABs; TAB genus TAB species),
         row_codes / col_codes (n, 2) = (genus, species) subset codes."""
@@ -775,10 +776,14 @@ class Engine:
         lb, lo = pack_strings(COMPARISON_LABELS)
         extra = (rsb, rso, csb, cso, rc_, cc_, int(bool(has_genera)), int(bool(has_species)), lb, lo)
         sfx = int(rso[-1]) * ncols + int(cso[-1]) * nrows + nrows * ncols * 16
-        return self._format(2, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing, extra, sfx)
+        return self._format(2, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing, extra, sfx,
+                            view=view)
 
     def _format(self, mode, v, nrows, rs, cs, ncols, nm, row_pre, col_pre, decimals, missing, summary=None,
-                extra_cap: int = 0) -> bytes:
+                extra_cap: int = 0, view: bool = False):
+        """The formatter call; the text as bytes, or with ``view`` as a memoryview of the engine's
+        pinned formatter buffer (valid until the next ``view`` call: write it out at once) -- the
+        D2H then runs at full link rate into page-locked memory and no bytes copy is made."""
         pack = pack_strings
         rb, ro = pack(row_pre)
         if len(ro) != nrows + 1:
@@ -794,7 +799,14 @@ class Engine:
                   + (int(np.diff(co).max(initial=0)) * ntok if mode == 0 and rs is not None else 0) + extra_cap)
         name = "taxi2_format_summary" if summary else "taxi2_format_rows" if rs is None else "taxi2_format_ragged"
         for _ in range(2):
-            out = np.empty(cap, dtype=np.uint8)
+            if view:
+                buf = getattr(self, "_fmt_buf", None)
+                if buf is None or buf.size < cap:
+                    self._fmt_buf = None
+                    buf = self._fmt_buf = self._pinned(max(cap, 1 << 24))
+                out = buf[:cap]
+            else:
+                out = np.empty(cap, dtype=np.uint8)
             cpre = (cb.ctypes.data if cb is not None else None, co.ctypes.data if co is not None else None)
             with self._lock:
                 if summary is not None:
@@ -820,7 +832,7 @@ class Engine:
                 cap = int(need.value)
                 continue
             self._check(rc, name)
-            return out[: need.value].tobytes()
+            return memoryview(out[: need.value]) if view else out[: need.value].tobytes()
         raise NativeError(f"{name}: output size changed between calls")
 
     def align_strings(self, x: SeqSet, y: SeqSet, xs, ys, scores=None, *, both: bool = False):

@@ -56,6 +56,11 @@ constexpr int AR_UNITS = TAXI2_AR_UNITS;  // units (row sequences, up to two pai
 #define TAXI2_AR_TS 0
 #endif
 constexpr int AR_TS = TAXI2_AR_TS;
+// wave-uniform skip of the trace VALU on steps with no lane in the band (see the step's cells)
+#ifndef TAXI2_AR_SKIP
+#define TAXI2_AR_SKIP 1
+#endif
+constexpr bool AR_SKIP = TAXI2_AR_SKIP != 0;
 __host__ __device__ constexpr int ar_pw(int K) { return K % 4 == 0 ? 4 : 2; }
 // byte offset of (step, lane, column k) in a chain's trace buffer (NT lanes)
 // (AR_TS = 0: the plain [step][lane][4K bytes] layout, for comparison)
@@ -583,10 +588,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 uint32_t eq[K];
                 {
                     // the row base's table, this lane's EP words of each piece (lane-contiguous reads)
-                    const char* tb = (const char*)&eqt[0][0][0][0] + rec.x;
+                    // (lane-first base: the other address forms cost the allocator a 129th VGPR, i.e.
+                    // one wave per SIMD at the 128-register budget)
+                    const char* tb = (const char*)&eqt[0][0][tq][0] + rec.x;
 #pragma unroll
                     for (int q = 0; q < K / EP; ++q) {
-                        const char* pq = tb + (size_t)(q * NT + tq) * (EP * 4);
+                        const char* pq = tb + (size_t)(q * NT) * (EP * 4);
                         if constexpr (EP == 4) {
                             const uint4 v = *(const uint4*)__builtin_assume_aligned(pq, 16);
                             eq[4 * q] = v.x;
@@ -627,26 +634,37 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 at_s2 F1 = as_s2(inF), Y = as_s2(inY);
                 uint32_t acc[K];
                 // Best-open fill on open-shifted cells (alignt2_kernel.hpp cells, RAW): M = G(i-1, j-1) +
-                // (s - co_i), X = max(G_up, X_up), Y = max(G_left, Y_left), B = maximum3(M, X, Y), G = B + o_i
-                at_s2 Mk = padd32(as_s2(carry), eq[0]);
+                // (s - co_i), X = max(G_up, X_up), Y = max(G_left, Y_left), B = maximum3(M, X, Y), G = B + o_i.
+                // TR: also the trace words (D1 = M - Ix, D2 = M - Iy of both halves, one v_perm)
+                auto cells = [&](auto TRC) {
+                    constexpr bool TR = decltype(TRC)::value;
+                    at_s2 Mk = padd32(as_s2(carry), eq[0]);
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const at_s2 Gu = as_s2(stG[k]), Xu = as_s2(stX[k]);
-                    const at_s2 M = Mk;
-                    if (k + 1 < K) Mk = padd32(Gu, eq[k + 1]);
-                    const at_s2 Xn = pmax(k == K - 1 ? padd32(Gu, cadj) : Gu, Xu);
-                    const at_s2 Yn = pmax(F1, Y);
-                    uint32_t b3;
-                    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(b3) : "v"(as_u32(M)), "v"(as_u32(Xn)), "v"(as_u32(Yn)));
-                    const uint32_t dD = as_u32(M) - as_u32(Xn);
-                    const uint32_t dE = as_u32(M) - as_u32(Yn);
-                    acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
-                    const at_s2 Gn = padd32(as_s2(b3), orow);
-                    stG[k] = as_u32(Gn);
-                    stX[k] = as_u32(Xn);
-                    F1 = Gn;
-                    Y = Yn;
-                }
+                    for (int k = 0; k < K; ++k) {
+                        const at_s2 Gu = as_s2(stG[k]), Xu = as_s2(stX[k]);
+                        const at_s2 M = Mk;
+                        if (k + 1 < K) Mk = padd32(Gu, eq[k + 1]);
+                        const at_s2 Xn = pmax(k == K - 1 ? padd32(Gu, cadj) : Gu, Xu);
+                        const at_s2 Yn = pmax(F1, Y);
+                        uint32_t b3;
+                        asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(b3) : "v"(as_u32(M)), "v"(as_u32(Xn)), "v"(as_u32(Yn)));
+                        if constexpr (TR) {
+                            const uint32_t dD = as_u32(M) - as_u32(Xn);
+                            const uint32_t dE = as_u32(M) - as_u32(Yn);
+                            acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
+                        }
+                        const at_s2 Gn = padd32(as_s2(b3), orow);
+                        stG[k] = as_u32(Gn);
+                        stX[k] = as_u32(Xn);
+                        F1 = Gn;
+                        Y = Yn;
+                    }
+                };
+                // AR_SKIP: a wave with no lane in the trace band this step (~36 % of (fill wave, step)
+                // pairs at config 3) runs the cells without the trace's 3 VALU per cell pair; the
+                // branch is wave-uniform (the band ballot in an SGPR)
+                if (AR_SKIP && bmask == 0) cells(std::false_type{});
+                else cells(std::true_type{});
                 if (in_band) {
                     constexpr uint32_t PSTRIDE = ar_piece_stride<K, NT>();  // bytes between pieces
                     // uniform step offset (SGPR) + the lane's constant: one VALU add, saddr stores per piece

@@ -71,7 +71,7 @@ def write_rows_gpu(fh, eng, vals: np.ndarray, row_pre: list, col_pre, decimals: 
     step = max(1, max_values // per_row)
     for r0 in range(0, vals.shape[0], step):
         r1 = min(vals.shape[0], r0 + step)
-        fh.write(eng.format_rows(vals[r0:r1], row_pre[r0:r1], col_pre, decimals=decimals, missing=missing))
+        fh.write(eng.format_rows(vals[r0:r1], row_pre[r0:r1], col_pre, decimals=decimals, missing=missing, view=True))
 
 
 def _brace_to_percent(fmt: str) -> str | None:

@@ -271,5 +271,5 @@ def _ragged_chunks(fh, eng, vals, row_kept, cols, row_pre, col_pre, decimals, mi
         r1 = int(np.searchsorted(starts, starts[r0] + max_values, side="right")) - 1
         r1 = min(n, max(r1, r0 + 1))
         fh.write(eng.format_ragged(vals, starts[r0 : r1 + 1], cols, row_pre[r0:r1], col_pre, ncols=len(row_pre),
-                                   decimals=decimals, missing=missing))
+                                   decimals=decimals, missing=missing, view=True))
         r0 = r1

@@ -93,7 +93,7 @@ def write_summary(path: Path, seqs: list, A: np.ndarray, metrics: list, genera, 
                 r1 = min(n, r0 + step)
                 fh.write(eng.format_summary(A[r0:r1], ids[r0:r1], ids, suf[2 * r0 : 2 * r1], suf, codes[r0:r1], codes,
                                             has_genera=bool(genera), has_species=bool(species), decimals=dec,
-                                            missing=missing))
+                                            missing=missing, view=True))
         return
     # line grouping of DistanceHandler.Linear (distances.py:96-111): runs of equal (x.id, y.id)
     text = _values_text(A, fmt, missing)

@@ -346,10 +346,10 @@ class VersusAll:
                 return
             if stage[0] is None or stage[0].shape[0] < x1 - x0:
                 stage[0] = torch.empty((x1 - x0, n, Mc), dtype=torch.float64, pin_memory=True)
-            with torch.cuda.stream(stream):
+            with torch.cuda.stream(tstream):  # after the block's event (post() waits on it)
                 stage[0][: x1 - x0].copy_(Dd[x0:x1], non_blocking=True)
                 stage[1] = torch.cuda.Event()
-                stage[1].record(stream)
+                stage[1].record(tstream)
             stage[2] = (x0, x1)
 
         def rows_in() -> None:  # the staged rows into D (waits for their copy only)
@@ -360,6 +360,12 @@ class VersusAll:
             D[x0:x1, :, cidx] = stage[0][: x1 - x0].numpy()
             stage[2] = None
 
+        # Two streams: block k + 1 aligns on `stream` while block k's post-processing -- compaction of
+        # its kept (b, a) strings, the text kernel, the text's D2H and file write, the staging of its
+        # complete rows -- runs on `tstream` after block k's event.  Tensors of a block are
+        # record_stream()'d on tstream before they are dropped, so the caching allocator never hands
+        # their memory to the next block while the text still reads it.
+        tstream = torch.cuda.Stream(dev)
         with torch.cuda.stream(stream):
             lens = torch.as_tensor(lens_h, device=dev)
             # self alignments (x, x) for the diagonal pairs' text
@@ -381,61 +387,65 @@ class VersusAll:
             kpx = torch.zeros(npairs, dtype=torch.int64, device=dev)
             kpy = torch.zeros(npairs, dtype=torch.int64, device=dev)
             klen = torch.zeros(npairs, dtype=torch.int32, device=dev)
-            kept = []
-            x0 = 0
-            while x0 < n:
-                # rows [x0, x1): about `target` triangle pairs, at most 2 * target ordered pairs of text
-                x1, cnt = x0, 0
-                while x1 < n and (x1 == x0 or (cnt + (n - 1 - x1) <= target and (x1 + 1 - x0) * n <= 2 * target)):
-                    cnt += n - 1 - x1
-                    x1 += 1
-                k0 = x0 * (2 * n - x0 - 1) // 2
-                blk = None
+        tstream.wait_stream(stream)  # the tables above
+        kept = []
+        kept_b = [0]
+
+        def launch(x0: int, x1: int, cnt: int):
+            """Block rows [x0, x1) (cnt triangle pairs) on `stream`: the fill (metrics + both
+            orientations' strings) and the metrics' scatter into Dd; returns the block record."""
+            k0 = x0 * (2 * n - x0 - 1) // 2
+            with torch.cuda.stream(stream):
+                d = torch.empty((cnt, 2, Mc), dtype=torch.float64, device=dev)
+                sx = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
+                sy = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
+                sl = torch.empty((cnt, 2), dtype=torch.int32, device=dev)
+                eng.tri_strings_dev(st, k0, cnt, clabels, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
+                                    sl.data_ptr(), scores, stream.cuda_stream)
+                # pair (a, b) of the block: a in [x0, x1), b > a
+                rows = torch.arange(x0, x1, device=dev)
+                per = n - 1 - rows
+                ra = torch.repeat_interleave(rows, per)
+                first = torch.cumsum(per, 0) - per
+                rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(first, per)
+                if Dd is not None:
+                    Dd[ra, rb] = d[:, 0, :]
+                    Dd[rb, ra] = d[:, 1, :]
+                ev = torch.cuda.Event()
+                ev.record(stream)
+            return dict(x0=x0, x1=x1, k0=k0, cnt=cnt, d=d, sx=sx, sy=sy, sl=sl, ra=ra, rb=rb, ev=ev)
+
+        def post(b) -> None:
+            """Block b's compaction, text and rows on tstream (after its fill)."""
+            x0, x1, k0, cnt = b["x0"], b["x1"], b["k0"], b["cnt"]
+            t0 = perf_counter()
+            with torch.cuda.stream(tstream):
                 if cnt:
-                    d = torch.empty((cnt, 2, Mc), dtype=torch.float64, device=dev)
-                    sx = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
-                    sy = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
-                    sl = torch.empty((cnt, 2), dtype=torch.int32, device=dev)
-                    try:
-                        eng.tri_strings_dev(st, k0, cnt, clabels, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
-                                            sl.data_ptr(), scores, stream.cuda_stream)
-                    except NativeError as e:
-                        if x0 == 0 and "walker strings need" in str(e):
-                            return False
-                        raise
-                    rows_in()  # the previous block's rows into D while this block aligns
-                    # pair (a, b) of the block: a in [x0, x1), b > a
-                    ra = torch.repeat_interleave(torch.arange(x0, x1, device=dev), n - 1 - torch.arange(x0, x1, device=dev))
-                    first = torch.cumsum(n - 1 - torch.arange(x0, x1, device=dev), 0) - (n - 1 - torch.arange(x0, x1, device=dev))
-                    rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(first, n - 1 - torch.arange(x0, x1, device=dev))
+                    tstream.wait_event(b["ev"])
+                    for key in ("d", "sx", "sy", "sl", "ra", "rb"):
+                        b[key].record_stream(tstream)
+                    sx, sy, sl, ra, rb = b["sx"], b["sy"], b["sl"], b["ra"], b["rb"]
+                    if Dd is None:
+                        dd = b["d"].cpu().numpy()
+                        a_h, b_h = ra.cpu().numpy(), rb.cpu().numpy()
+                        for q, kk in enumerate(cidx):
+                            D[a_h, b_h, kk] = dd[:, 0, q]
+                            D[b_h, a_h, kk] = dd[:, 1, q]
                     end = (lens[ra] + lens[rb]).to(torch.int64)
                     # keep the (b, a) orientation compacted (taxi2_pack_slots_dev: each slot's
                     # right-aligned bytes to a running offset)
                     L1 = sl[:, 1].to(torch.int64)
                     off = torch.cumsum(L1, 0) - L1
-                    tot = int(L1.sum().item())
+                    tot = int(L1.sum().item())  # waits for tstream only (this block's fill is done)
                     kx = torch.empty(max(1, tot), dtype=torch.uint8, device=dev)
                     ky = torch.empty(max(1, tot), dtype=torch.uint8, device=dev)
                     eng.pack_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 1, end.data_ptr(),
-                                       off.data_ptr(), cnt, kx.data_ptr(), ky.data_ptr(), stream.cuda_stream)
+                                       off.data_ptr(), cnt, kx.data_ptr(), ky.data_ptr(), tstream.cuda_stream)
                     kpx[k0:k0 + cnt] = kx.data_ptr() + off
                     kpy[k0:k0 + cnt] = ky.data_ptr() + off
                     klen[k0:k0 + cnt] = sl[:, 1]
                     kept.append((kx, ky))
-                    kept_bytes += 2 * tot
-                    blk = (sx, sy, sl, end, d, ra, rb)
-                    if Dd is not None:
-                        Dd[ra, rb] = d[:, 0, :]
-                        Dd[rb, ra] = d[:, 1, :]
-                    else:
-                        dd = d.cpu().numpy()
-                        a_h, b_h = ra.cpu().numpy(), rb.cpu().numpy()
-                        for q, kk in enumerate(cidx):
-                            D[a_h, b_h, kk] = dd[:, 0, q]
-                            D[b_h, a_h, kk] = dd[:, 1, q]
-                rows_in()  # (a block without pairs)
-                stream.synchronize()  # the block's alignment (compute) ends here; its text starts
-                t0 = perf_counter()
+                    kept_b[0] += 2 * tot
                 # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
                 # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
                 # and (x, x) from the self alignments
@@ -448,8 +458,7 @@ class VersusAll:
                 px = torch.where(lo, kpy[pl.clamp(0, npairs - 1)], px_self[xs_.expand(-1, n)])
                 py = torch.where(lo, kpx[pl.clamp(0, npairs - 1)], py_self[xs_.expand(-1, n)])
                 ln = torch.where(lo, klen[pl.clamp(0, npairs - 1)], slen_self[xs_.expand(-1, n)])
-                if blk is not None:
-                    sx, sy, sl, end, _, _, _ = blk
+                if cnt:
                     q = (pu - k0).clamp(0, max(0, cnt - 1))
                     L0 = sl[:, 0].to(torch.int64)
                     start0 = q * 2 * cap + end[q] - L0[q]
@@ -459,25 +468,49 @@ class VersusAll:
                 px, py, ln = px.contiguous(), py.contiguous(), ln.to(torch.int32).contiguous()
                 fh.write(eng.format_pairs_ptr_dev(x1 - x0, n, px.data_ptr(), py.data_ptr(), ln.data_ptr(),
                                                   (ids[0], ids[1][x0:x1 + 1]), ids, first=x0 == 0,
-                                                  stream=stream.cuda_stream))
-                if isinstance(self.timings, dict):
-                    self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
-                del blk, px, py, ln
+                                                  stream=tstream.cuda_stream))
+                rows_in()  # the previous block's staged rows into D
                 rows_out(x0, x1)
-                report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
-                       total)
-                x0 = x1
-                if x0 < n and kept_bytes > keep_limit:
-                    # the kept strings outgrew their budget: the remaining rows align every ordered
-                    # pair once (row blocks of the rect path), nothing kept
-                    rows_in()
-                    del kept, kpx, kpy, klen, Dd
-                    return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
-            rows_in()
-            stream.synchronize()
-            del kept
-        return True
+            if isinstance(self.timings, dict):
+                self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
+            report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
+                   total)
 
+        pending = None
+        x0 = 0
+        while x0 < n:
+            # rows [x0, x1): about `target` triangle pairs, at most 2 * target ordered pairs of text
+            x1, cnt = x0, 0
+            while x1 < n and (x1 == x0 or (cnt + (n - 1 - x1) <= target and (x1 + 1 - x0) * n <= 2 * target)):
+                cnt += n - 1 - x1
+                x1 += 1
+            try:
+                blk = launch(x0, x1, cnt) if cnt else dict(x0=x0, x1=x1, k0=0, cnt=0)
+            except NativeError as e:
+                if x0 == 0 and "walker strings need" in str(e):
+                    return False
+                raise
+            if pending is not None:
+                post(pending)  # block k - 1's text while block k aligns
+            pending = blk
+            x0 = x1
+            if x0 < n and kept_b[0] > keep_limit:
+                # the kept strings outgrew their budget: the remaining rows align every ordered pair
+                # once (row blocks of the rect path), nothing kept
+                post(pending)
+                pending = None
+                rows_in()
+                tstream.synchronize()
+                stream.synchronize()
+                del kept, kpx, kpy, klen, Dd
+                return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
+        if pending is not None:
+            post(pending)
+        rows_in()
+        tstream.synchronize()
+        stream.synchronize()
+        del kept
+        return True
 
     def _rows_with_pairs(self, seqs, eng, st, D, cidx, clabels, scores, fh, x_start: int = 0) -> bool:
         """versus_all.py:746-750 as the reference runs it: each ORDERED pair aligned once, its aligned
@@ -1357,7 +1390,7 @@ class _BlockWriters:
                 self.summ.write(self.eng.format_summary(
                     A[r0:r1], ids[x0 + r0 : x0 + r1], ids, self.suf[2 * (x0 + r0) : 2 * (x0 + r1)], self.suf,
                     self.codes[x0 + r0 : x0 + r1], self.codes, has_genera=bool(self.genera),
-                    has_species=bool(self.species), decimals=self.dec, missing=self.missing))
+                    has_species=bool(self.species), decimals=self.dec, missing=self.missing, view=True))
         else:
             from .subsets import summary_lines
 

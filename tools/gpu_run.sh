@@ -21,6 +21,8 @@
 #   tool:SCRIPT      python tools/SCRIPT.py (bench tools), e.g. tool:bench_long
 #   sec:LEG          one bench_secondary.py leg alone (task, config5, config4, allmetrics)
 #   sectrace:LEG     rocprofv3 --kernel-trace --stats of that leg
+#   pmcsec:LEG:SET   one rocprofv3 --pmc pass (valu | lds | fetch | write) over that leg's kernels
+#                    matching PMC_SEC_RE (default k_prealigned|k_subset|k_rowmin)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:?tag}
@@ -85,6 +87,22 @@ run_step() {
     pmc_write)
         (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE $PMC_OPTS -d "$OUT/pmc_write" -o run -- \
             $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_write.err") ;;
+    pmcsec:*)  # pmcsec:LEG:SET -- one PMC pass (SET valu | lds | fetch | write) over a bench_secondary leg,
+        # kernels matching PMC_SEC_RE (default: the pre-aligned tile and subset kernels)
+        local rest=${s#pmcsec:}
+        local leg=${rest%%:*} set=${rest#*:}
+        local re=${PMC_SEC_RE:-k_prealigned|k_subset|k_rowmin}
+        local ctr
+        case "$set" in
+            valu) ctr="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" ;;
+            lds) ctr="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE" ;;
+            fetch) ctr="FETCH_SIZE" ;;
+            write) ctr="WRITE_SIZE" ;;
+            *) echo "unknown pmc set $set" >&2; return 2 ;;
+        esac
+        (cd /tmp && timeout -s KILL 400 rocprofv3 --pmc $ctr --kernel-include-regex "$re" --output-format csv \
+            -d "$OUT/pmcsec_${leg}_$set" -o run -- python3 $R/bench_secondary.py "$leg" \
+            > "$OUT/pmcsec_${leg}_$set.json" 2> "$OUT/pmcsec_${leg}_$set.err") ;;
     guard)
         (cd "$R" && TAXI2_LIB=libtaxi2_mi355x_guard.so timeout -k 10 900 $PYT tests/test_gpu_alignt.py \
             tests/test_gpu_band.py tests/test_gpu_regress.py > "$OUT/guard.log" 2>&1) ;;

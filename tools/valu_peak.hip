@@ -61,7 +61,17 @@ constexpr int UNROLL = 32;  // asm blocks per loop iteration (256 measured instr
                  : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]) \
                  : "v"(c))
 
-// instruction table: name, form (2 = dst,src0,src1; 3 = three sources; 1 = mov; v = with vcc; 6 = 64-bit pair)
+// three-source bit operation with its truth table (the pre-aligned tile kernel's v_bitop3 0x48)
+#define CH8_B(INS)                                                                                               \
+    asm volatile(INS " %0, %0, %8, %9 bitop3:0x48\n\t" INS " %1, %1, %8, %9 bitop3:0x48\n\t" INS             \
+                     " %2, %2, %8, %9 bitop3:0x48\n\t" INS " %3, %3, %8, %9 bitop3:0x48\n\t" INS              \
+                     " %4, %4, %8, %9 bitop3:0x48\n\t" INS " %5, %5, %8, %9 bitop3:0x48\n\t" INS              \
+                     " %6, %6, %8, %9 bitop3:0x48\n\t" INS " %7, %7, %8, %9 bitop3:0x48"                        \
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]) \
+                 : "v"(c), "v"(d))
+
+// instruction table: name, form (2 = dst,src0,src1; 3 = three sources; 1 = mov; v = with vcc; 6 = 64-bit pair;
+// b = bitop3 with a truth table)
 #define VALU_LIST(X)                                                                                             \
     X(0, "v_add_f32", 2) X(1, "v_add_u32", 2) X(2, "v_sub_u32", 2) X(3, "v_max_i32", 2) X(4, "v_min_u32", 2)     \
     X(5, "v_max_f32", 2) X(6, "v_min_f32", 2) X(7, "v_and_b32", 2) X(8, "v_or_b32", 2) X(9, "v_xor_b32", 2)      \
@@ -73,13 +83,15 @@ constexpr int UNROLL = 32;  // asm blocks per loop iteration (256 measured instr
     X(30, "v_bfe_u32", 3) X(31, "v_lshl_add_u32", 3) X(32, "v_and_or_b32", 3) X(33, "v_pk_mad_u16", 3)          \
     X(34, "v_pk_fma_f16", 3) X(35, "v_mad_u32_u24", 3) X(36, "v_pk_add_f32", 6) X(37, "v_pk_mul_f32", 6)       \
     X(38, "v_max_u16", 2) X(39, "v_add_u16", 2) X(40, "v_max_f16", 2) X(41, "v_cvt_f32_i32", 1)               \
-    X(42, "v_add_u32_sdwa", s) X(43, "v_pk_maximum3_f16", 3) X(44, "v_pk_max_u16", 2)
+    X(42, "v_add_u32_sdwa", s) X(43, "v_pk_maximum3_f16", 3) X(44, "v_pk_max_u16", 2)                        \
+    X(45, "v_bcnt_u32_b32", 2) X(46, "v_bitop3_b32", b) X(47, "v_add_f64", 6) X(48, "v_mul_f64", 6)
 #define FORM_2(INS) CH8(INS)
 #define FORM_3(INS) CH8_3(INS)
 #define FORM_1(INS) CH8_1(INS)
 #define FORM_v(INS) CH8_V(INS)
 #define FORM_6(INS) CH4_64(INS)
 #define FORM_s(INS) CH8_S(INS)
+#define FORM_b(INS) CH8_B(INS)
 
 template <int MODE>
 __global__ void __launch_bounds__(256) k_valu(unsigned* out, unsigned long long* cyc, int iters, unsigned seed) {
