@@ -89,9 +89,52 @@ __device__ __forceinline__ int base_code(unsigned c) {
     return u == 'A' ? 0 : u == 'C' ? 1 : u == 'G' ? 2 : u == 'T' ? 3 : 4;
 }
 
+// Natural log for the jc / k2p transforms: ~50 VALU (31 of them f64) instead of the ~98 (76 f64) of
+// the library's f64 log (ocml), which dominated the pre-aligned tile kernel's epilogue (three logs
+// per pair; an f64 op issues at a quarter of the f32 rate).  x = 2^e m,
+// m in [sqrt(1/2), sqrt(2)); log m = 2 atanh(s) = 2 s + 2 s (s^2 / 3 + s^4 / 5 + ... + s^20 / 21),
+// s = (m - 1) / (m + 1), |s| <= 0.1716 (the first omitted term is < 1e-19 relative); log x = e ln2_hi +
+// (2 s + (2 s R + e ln2_lo)) with ln2 split so that e ln2_hi is exact.  Within a few ulp of a correctly
+// rounded log (absolute error < 1e-15 on every argument the metrics form, which are >= ~1e-17): the
+// 1e-12 bound north_star sets for jc / k2p against the reference's glibc log holds with a wide
+// margin (tests/test_gpu_parity.py, tests/test_gpu_prealigned.py).  Special values as log's:
+// log(1) = +0 (so -0.75 log(1) is -0.0, "-0.0000"), log(0) = -inf, log(x < 0) = log(NaN) = NaN.
+__device__ __forceinline__ double metric_log(double x) {
+    if (!(x > 0.0)) return x == 0.0 ? -__builtin_inf() : __builtin_nan("");
+    int e = __builtin_amdgcn_frexp_exp(x);
+    double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        e -= 1;
+    }
+    // s = (m - 1) / (m + 1) from the hardware reciprocal, one Newton step and one residual
+    // correction (a few ulp at most; the division's exact rounding is not needed here)
+    const double d = m + 1.0, n1 = m - 1.0;
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = fma(rc, fma(-d, rc, 1.0), rc);
+    double s = n1 * rc;
+    s = fma(rc, fma(-d, s, n1), s);
+    const double t = s * s;
+    double r = 1.0 / 21.0;
+    r = fma(r, t, 1.0 / 19.0);
+    r = fma(r, t, 1.0 / 17.0);
+    r = fma(r, t, 1.0 / 15.0);
+    r = fma(r, t, 1.0 / 13.0);
+    r = fma(r, t, 1.0 / 11.0);
+    r = fma(r, t, 1.0 / 9.0);
+    r = fma(r, t, 1.0 / 7.0);
+    r = fma(r, t, 1.0 / 5.0);
+    r = fma(r, t, 1.0 / 3.0);
+    const double s2 = 2.0 * s;
+    const double de = (double)e;
+    constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+    return fma(de, LN2_HI, s2 + fma(s2 * t, r, de * LN2_LO));
+}
+
 // f64 metric from the four column counters (itaxotools.calculate_distances semantics,
 // restated in oracle/restatement.py metric_value).  Compiled with -ffp-contract=off so the
-// operation sequence matches the C restatement exactly; NaN / inf = undefined (None).
+// operation sequence matches the C restatement exactly (p / p-gaps bit for bit; jc / k2p through
+// metric_log); NaN / inf = undefined (None).
 __device__ __forceinline__ double metric_value(int code, uint32_t valid, uint32_t ts, uint32_t tv,
                                                uint32_t gap) {
     const double v = (double)valid;
@@ -104,13 +147,13 @@ __device__ __forceinline__ double metric_value(int code, uint32_t valid, uint32_
         case 2: {
             if (!valid) return __builtin_nan("");
             const double p = mism / v;
-            return -0.75 * log(1.0 - (4.0 / 3.0) * p);
+            return -0.75 * metric_log(1.0 - (4.0 / 3.0) * p);
         }
         case 3: {
             if (!valid) return __builtin_nan("");
             const double P = (double)ts / v;
             const double Q = (double)tv / v;
-            return -0.5 * log(1.0 - 2.0 * P - Q) - 0.25 * log(1.0 - 2.0 * Q);
+            return -0.5 * metric_log(1.0 - 2.0 * P - Q) - 0.25 * metric_log(1.0 - 2.0 * Q);
         }
         case METRIC_COUNTS:  // the counters themselves, 16 bits each (max_len <= 32767 checked by the host)
             return __longlong_as_double((long long)((uint64_t)valid | (uint64_t)ts << 16 | (uint64_t)tv << 32 |

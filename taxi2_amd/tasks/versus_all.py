@@ -390,6 +390,22 @@ class VersusAll:
         tstream.wait_stream(stream)  # the tables above
         kept = []
         kept_b = [0]
+        # linear.tsv, the matricial files, summary.tsv and the subset statistics per row block, while
+        # the next blocks align and their aligned_pairs.txt text is written: the writers' own engine
+        # context (formatting on its own stream, its own lock) in a worker thread, fed each block's
+        # adjusted rows (x100, diagonal rule) once they are complete
+        sink = writers = None
+        futs = []
+        if Dd is not None and not os.environ.get("TAXI2_NO_BLOCK_WRITERS") and n > 1:
+            from concurrent.futures import ThreadPoolExecutor
+
+            from .._native import Engine
+
+            sink = _BlockWriters(self, seqs, Engine(eng.device), files=True, walk=False, pairs=False)
+            sink.rmin_k = None  # (row minima: the streamed path's extra, not the dense path's)
+            sink.diag = self._diag_info(seqs, eng, st, True, scores, [str(m) for m in self.params.distances.metrics])
+            writers = ThreadPoolExecutor(1, thread_name_prefix="taxi2-writers")
+            scale = 100.0 if self.params.format.percentage_multiply else 1.0
 
         def launch(x0: int, x1: int, cnt: int):
             """Block rows [x0, x1) (cnt triangle pairs) on `stream`: the fill (metrics + both
@@ -471,6 +487,16 @@ class VersusAll:
                                                   stream=tstream.cuda_stream))
                 rows_in()  # the previous block's staged rows into D
                 rows_out(x0, x1)
+                if sink is not None:  # rows [x0, x1) are complete: adjusted on the GPU, text in the thread
+                    A = Dd[x0:x1].clone()
+                    if scale != 1.0:
+                        A *= scale
+                    sink.diagonal(x0, x1, A, scale)
+                    sink.aggregate(x0, x1, A)
+                    Ah = A.cpu().numpy()
+                    while len(futs) >= 2:  # at most two blocks queued for the thread
+                        futs.pop(0).result()
+                    futs.append(writers.submit(sink.write_text_host, x0, x1, Ah))
             if isinstance(self.timings, dict):
                 self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
             report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
@@ -503,6 +529,11 @@ class VersusAll:
                 tstream.synchronize()
                 stream.synchronize()
                 del kept, kpx, kpy, klen, Dd
+                if sink is not None:  # the end-of-task writers redo every file from the full matrix
+                    for f in futs:
+                        f.result()
+                    writers.shutdown()
+                    sink.abandon()
                 return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
         if pending is not None:
             post(pending)
@@ -510,6 +541,15 @@ class VersusAll:
         tstream.synchronize()
         stream.synchronize()
         del kept
+        if sink is not None:
+            t0 = perf_counter()
+            for f in futs:
+                f.result()
+            writers.shutdown()
+            sink.close()
+            self._written_by_blocks = True
+            if isinstance(self.timings, dict):
+                self.timings["writers_drain_s"] = perf_counter() - t0
         return True
 
     def _rows_with_pairs(self, seqs, eng, st, D, cidx, clabels, scores, fh, x_start: int = 0) -> bool:
@@ -1096,6 +1136,7 @@ class VersusAll:
             create_parents(self.paths.aligned_pairs)
             pairs_fh = open(self.paths.aligned_pairs, "wb")
         self.pairs_walked = False
+        self._written_by_blocks = False
         self.timings = times = {"compute_s": 0.0, "pairs_text_s": 0.0}
         t0 = perf_counter()
         try:
@@ -1112,7 +1153,9 @@ class VersusAll:
             rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
         except Exception:
             pass
-        if rank0:
+        if rank0 and self._written_by_blocks:  # linear / matricial / summary / subsets per row block
+            pass
+        elif rank0:
             A = self._adjusted(D)
             for name, fn in (("pairs_s", None if self.pairs_walked else self.write_pairs),
                              ("linear_s", lambda s_: self.write_distances_linear(s_, A)),
@@ -1135,7 +1178,8 @@ class _BlockWriters:
     taxi2_subset_aggregate_dev), each fed the rows [x0, x1) in x-major order -- the file contents
     are those of the dense path (tests/test_gpu_streaming.py)."""
 
-    def __init__(self, task: VersusAll, seqs: list, eng, files: bool = True, walk: bool = False):
+    def __init__(self, task: VersusAll, seqs: list, eng, files: bool = True, walk: bool = False,
+                 pairs: bool = True):
         import torch
 
         from .subsets import SubsetAggregatorDev, subset_codes
@@ -1223,7 +1267,7 @@ class _BlockWriters:
                      for part, name in ((genera, "genera"), (species, "species")) if part]
         self.pairs_fh = None
         self._pair_sets = None
-        if p.pairs.write and files:
+        if p.pairs.write and files and pairs:  # (pairs False: the caller writes aligned_pairs.txt)
             create_parents(task.paths.aligned_pairs)
             if walk:  # text from the metric kernel's walks, handed over per block (write_text)
                 self.pairs_fh = open(task.paths.aligned_pairs, "wb")
@@ -1343,7 +1387,10 @@ class _BlockWriters:
     def write_text(self, x0: int, x1: int, D, pairs_text: bytes | None = None) -> None:
         if not self.has_text:  # reductions only: the block never leaves HBM
             return
-        A = D.cpu().numpy()
+        self.write_text_host(x0, x1, D.cpu().numpy(), pairs_text)
+
+    def write_text_host(self, x0: int, x1: int, A: np.ndarray, pairs_text: bytes | None = None) -> None:
+        """write_text on the block's values already on the host (a writer thread's entry)."""
         seqs, ids = self.seqs, self.ids
         if self.walk and self.pairs_fh is not None:
             self.pairs_fh.write(pairs_text)
@@ -1415,6 +1462,13 @@ class _BlockWriters:
                             self.mats[m].write(d)
         if self.summ_runs is not None:
             self.summ_runs.feed(A, x0)
+
+    def abandon(self) -> None:
+        """Close the files without finishing them (the caller rewrites every one of them)."""
+        for fh in [self.lin, self.summ, *(self.mats or [])]:
+            if fh is not None:
+                fh.close()
+        self.lin = self.summ = self.mats = self.summ_runs = None
 
     def close(self) -> None:
         from .subsets import write_subset_statistics
