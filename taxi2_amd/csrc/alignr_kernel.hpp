@@ -58,7 +58,7 @@ constexpr int AR_UNITS = TAXI2_AR_UNITS;  // units (row sequences, up to two pai
 constexpr int AR_TS = TAXI2_AR_TS;
 // wave-uniform skip of the trace VALU on steps with no lane in the band (see the step's cells)
 #ifndef TAXI2_AR_SKIP
-#define TAXI2_AR_SKIP 1
+#define TAXI2_AR_SKIP 0
 #endif
 constexpr bool AR_SKIP = TAXI2_AR_SKIP != 0;
 __host__ __device__ constexpr int ar_pw(int K) { return K % 4 == 0 ? 4 : 2; }

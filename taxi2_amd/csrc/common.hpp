@@ -163,4 +163,14 @@ __device__ __forceinline__ double metric_value(int code, uint32_t valid, uint32_
     }
 }
 
+// metric_value with the pair's p-distance (mism / valid, NaN without valid columns) already formed:
+// the p and jc metrics share its division (the pre-aligned tile kernel's epilogue evaluates every
+// requested metric of 16 pairs per thread).  Same values as metric_value, bit for bit.
+__device__ __forceinline__ double metric_value_p(int code, uint32_t valid, uint32_t ts, uint32_t tv, uint32_t gap,
+                                                 double p) {
+    if (code == 0) return p;
+    if (code == 2) return valid ? -0.75 * metric_log(1.0 - (4.0 / 3.0) * p) : __builtin_nan("");
+    return metric_value(code, valid, ts, tv, gap);
+}
+
 }  // namespace taxi2

@@ -199,9 +199,10 @@ k_prealigned_tile(SetView XS, SetView YS, PairSrc ps, int64_t x0, int64_t nx, in
             const int64_t yn = tb.ynat ? (ok ? tb.ynat[y] : -1) : y;  // the task's column
             const uint32_t ts = c[i][j][1] - c[i][j][2];
             const bool none = tb.diag && x == yn;
+            const double pd = c[i][j][0] ? (double)c[i][j][1] / (double)c[i][j][0] : __builtin_nan("");
             for (int m = 0; m < nm; ++m) {
                 const double v = none ? __builtin_nan("")
-                                      : metric_value(ms.code[m], c[i][j][0], ts, c[i][j][2], c[i][j][3]) * tb.scale;
+                                      : metric_value_p(ms.code[m], c[i][j][0], ts, c[i][j][2], c[i][j][3], pd) * tb.scale;
                 if (staged) stg[(tx * PT + ty + 16 * j) * nm + m] = v;
                 else if (ok) out[slot * nm + m] = v;
                 // the first (lowest task column) of equal values stays

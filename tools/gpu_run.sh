@@ -18,6 +18,7 @@
 #                    does not split counters over passes)
 #   guard            the poisoning guard build (make guard) on the packed aligner suites
 #   peak             tools/valu_peak (SIMD cycles per wave64 instruction)
+#   d2h              tools/d2h_probe (device -> host text bandwidth: memcpy, 4 streams, kernel stores)
 #   tool:SCRIPT      python tools/SCRIPT.py (bench tools), e.g. tool:bench_long
 #   sec:LEG          one bench_secondary.py leg alone (task, config5, config4, allmetrics)
 #   sectrace:LEG     rocprofv3 --kernel-trace --stats of that leg
@@ -100,14 +101,17 @@ run_step() {
             write) ctr="WRITE_SIZE" ;;
             *) echo "unknown pmc set $set" >&2; return 2 ;;
         esac
-        (cd /tmp && timeout -s KILL 400 rocprofv3 --pmc $ctr --kernel-include-regex "$re" --output-format csv \
-            -d "$OUT/pmcsec_${leg}_$set" -o run -- python3 $R/bench_secondary.py "$leg" \
+        # (the prealigned leg: config 5's tile launches alone, TAXI2_PREALIGNED_PARTS=config5)
+        (cd /tmp && TAXI2_PREALIGNED_PARTS=config5 timeout -s KILL 400 rocprofv3 --pmc $ctr --kernel-include-regex "$re" \
+            --output-format csv -d "$OUT/pmcsec_${leg}_$set" -o run -- python3 $R/bench_secondary.py "$leg" \
             > "$OUT/pmcsec_${leg}_$set.json" 2> "$OUT/pmcsec_${leg}_$set.err") ;;
     guard)
         (cd "$R" && TAXI2_LIB=libtaxi2_mi355x_guard.so timeout -k 10 900 $PYT tests/test_gpu_alignt.py \
             tests/test_gpu_band.py tests/test_gpu_regress.py > "$OUT/guard.log" 2>&1) ;;
     peak)
         timeout -k 10 180 "$R/tools/valu_peak" > "$OUT/valu_peak.txt" 2>&1 ;;
+    d2h)
+        timeout -k 10 120 "$R/tools/d2h_probe" > "$OUT/d2h_probe.txt" 2>&1 ;;
     tool:*)
         (cd "$R" && timeout -k 10 900 python3 -u "tools/${s#tool:}.py" > "$OUT/${s#tool:}.json" 2> "$OUT/${s#tool:}.err") ;;
     sec:*)

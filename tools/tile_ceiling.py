@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU issue roofline of the pre-aligned tile kernel (prealigned_kernel.hpp k_prealigned_tile): the
 instruction mix of its word loop (gfx950 ISA) priced with the measured per-instruction issue costs
-(tools/valu_peak -> profiles/r2/valu_peak.txt, as tools/issue_ceiling.py does for the aligner),
+(tools/valu_peak -> profiles/r5/valu_peak.txt, which adds v_bcnt, v_bitop3 and the f64 ops; as tools/issue_ceiling.py does for the aligner),
 combined with rocprofv3 PMC passes of the bench's `prealigned` leg (config 5's tile launches alone,
 TAXI2_PREALIGNED_PARTS=config5) into profiles/prealigned_ceiling.json, which bench_secondary.py's
 leg reads for its compute_roofline / traffic_roofline.
@@ -75,7 +75,7 @@ def main() -> None:
     ap.add_argument("--write")
     ap.add_argument("--pairs", type=float, required=True, help="unordered pairs over the profiled launches")
     ap.add_argument("--words", type=int, required=True, help="32-column plane words per pair")
-    ap.add_argument("--costs", default=str(ROOT / "profiles/r2/valu_peak.txt"))
+    ap.add_argument("--costs", default=str(ROOT / "profiles/r5/valu_peak.txt"))
     ap.add_argument("--out", default=str(ROOT / "profiles/prealigned_ceiling.json"))
     a = ap.parse_args()
     costs = valu_costs(Path(a.costs))
