@@ -1196,8 +1196,9 @@ struct Tracer {
     }
 };
 
+// first_only: the one-thread path compresses each descriptor's first part alone (launch_zlen2)
 int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1,
-                hipStream_t st = nullptr, int likely_n = 0);
+                hipStream_t st = nullptr, int likely_n = 0, int first_only = 0);
 
 // Raw-mode NCD with C(x) computed once per set member (when the pairs outnumber the sequences).
 int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64_t* xs, const int64_t* ys,
@@ -1254,10 +1255,10 @@ int ncd_raw_cached(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const int64
 // one thread per stream with per-thread HBM scratch slabs kept in the context (the head tables
 // are zeroed once at allocation), any length (the window slides as zlib's does).
 int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1,
-                hipStream_t st, int likely_n) {
+                hipStream_t st, int likely_n, int first_only) {
     if (n <= 0) return 0;
     if (!st) st = ctx->stream;
-    const bool wave_ok = !latin1 && !getenv("TAXI2_ZLEN_SERIAL");
+    bool wave_ok = !latin1 && !getenv("TAXI2_ZLEN_SERIAL");
     auto wave_pass = [&](int nmax_in, int redo) -> int {
         const int nmax = std::max(nmax_in, 4);
         const size_t lds = zlw::lds_bytes(nmax);
@@ -1271,6 +1272,7 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
         return 0;
     };
     int redo = 0;
+    if (first_only) wave_ok = false;  // (only the fused fallback asks for it)
     if (wave_ok && likely_n > 0 && likely_n < max_n && likely_n <= zlw::NMAX) {
         // most streams fit `likely_n`: a first pass sized for them (smaller LDS, more waves per CU),
         // then the pass below over the streams it declined (-1) only
@@ -1296,9 +1298,39 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
         ctx->z_threads = threads;
     }
     hipLaunchKernelGGL(k_zlen, dim3((unsigned)(threads / 64)), dim3(64), 0, st, d_st, n,
-                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out, (int)latin1, redo);
+                       (uint16_t*)ctx->d_zheads, (uint8_t*)ctx->d_zslabs, d_out, (int)latin1, redo, first_only);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
+}
+
+// The fused lengths of `n` descriptors: d_out[s] = C(a + b), d_out_a[s] = C(a) (k_zlen_wave2: one sort
+// and a shared parse prefix, zlen_wave.hpp); where the one-wave path does not apply, two one-thread
+// passes (a + b, then a alone).
+int launch_zlen2(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int32_t* d_out_a, int max_n,
+                 bool latin1, hipStream_t st, int likely_n) {
+    if (n <= 0) return 0;
+    if (!st) st = ctx->stream;
+    if (latin1 || getenv("TAXI2_ZLEN_SERIAL") || max_n > zlw::NMAX) {
+        if (launch_zlen(ctx, d_st, n, d_out, max_n, latin1, st)) return -1;
+        return launch_zlen(ctx, d_st, n, d_out_a, max_n, latin1, st, 0, 1);
+    }
+    auto wave_pass = [&](int nmax_in, int redo) -> int {
+        const int nmax = std::max(nmax_in, 4);
+        const size_t lds = zlw::lds_bytes(nmax);
+        if (lds > 64 * 1024)
+            HIP_TRY(ctx, hipFuncSetAttribute((const void*)k_zlen_wave2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int per_cu = 0;
+        HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave2, 64, lds));
+        const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
+        hipLaunchKernelGGL(k_zlen_wave2, dim3((unsigned)grid), dim3(64), lds, st, d_st, n, nmax, d_out, d_out_a, redo);
+        HIP_TRY(ctx, hipGetLastError());
+        return 0;
+    };
+    if (likely_n > 0 && likely_n < max_n) {
+        if (wave_pass(likely_n, 0)) return -1;
+        return wave_pass(max_n, 1);
+    }
+    return wave_pass(max_n, 0);
 }
 
 // Where the aligned strings of `n` pairs sit (the walkers' StrOut slots) and which ordered pairs
@@ -1315,29 +1347,34 @@ struct SlotSrc {
 };
 
 // NCD (distances.py:351-358) of every (pair, orientation) from the aligned strings already in HBM:
-// k_ncd_slot_streams (4 streams per pair when both orientations hold the same alignment, else 6),
-// one k_zlen_wave launch over all of them, k_ncd_slot_finish into out[(p * no + o) * ostride + ocol].
-// max_str bounds every stream (2 x the longest aligned string); latin1: the set holds bytes >= 0x80
+// k_ncd_slot_streams (per pair one fused job per orientation -- C(x + y) and C(x) in one pass -- and
+// C(y0), C(x1) only where the two orientations' alignments differ), k_zlen_wave2 over the fused jobs,
+// k_zlen_wave over the singles, k_ncd_slot_finish into out[(p * no + o) * ostride + ocol].  max_str
+// bounds every stream (2 x the longest aligned string); latin1: the set holds bytes >= 0x80
 // (compressed as their UTF-8 upper case, one-thread path).  Stream-ordered on `st`, no host sync.
 int ncd_from_slots(taxi2_ctx* ctx, const SlotSrc& ss, const DevSet& X, const DevSet& Y, int64_t n, int max_str,
                    bool latin1, double* out, int64_t ostride, int ocol, hipStream_t st) {
     if (n <= 0) return 0;
-    const int64_t ns = n * 2 * ss.no, nc = n * ss.no;
+    const int64_t nf = n * ss.no, ns = n * 2;
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-    const size_t b_st = al((size_t)(ns + nc) * sizeof(ZStream)), b_c = al((size_t)(ns + nc) * 4);
-    if (ensure(ctx, &ctx->d_ncd, &ctx->d_ncd_bytes, b_st + b_c)) return -1;
-    ZStream* d_st = (ZStream*)ctx->d_ncd;
-    int32_t* d_c = (int32_t*)((char*)ctx->d_ncd + b_st);
+    const size_t b_f = al((size_t)nf * sizeof(ZStream)), b_s = al((size_t)ns * sizeof(ZStream));
+    const size_t b_c = al((size_t)(2 * nf + ns) * 4);
+    if (ensure(ctx, &ctx->d_ncd, &ctx->d_ncd_bytes, b_f + b_s + b_c)) return -1;
+    ZStream* d_fused = (ZStream*)ctx->d_ncd;
+    ZStream* d_single = (ZStream*)((char*)ctx->d_ncd + b_f);
+    int32_t* d_cab = (int32_t*)((char*)ctx->d_ncd + b_f + b_s);
+    int32_t* d_ca = d_cab + nf;
+    int32_t* d_cs = d_ca + nf;
     hipLaunchKernelGGL(k_ncd_slot_streams, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, ss.sx, ss.sy, ss.slen,
-                       ss.cap, ss.nslot, ss.no, ss.d_end, view(X), view(Y), ss.ps, n, d_st, d_st + ns);
+                       ss.cap, ss.nslot, ss.no, ss.d_end, view(X), view(Y), ss.ps, n, d_fused, d_single);
     HIP_TRY(ctx, hipGetLastError());
-    // singles and concatenations in separate launches, each first sized for the likely length (an
-    // aligned string is rarely much longer than the longer sequence: +1/16 + 32 bytes)
+    // each launch first sized for the likely length (an aligned string is rarely much longer than
+    // the longer sequence: +1/16 + 32 bytes), a second pass over the streams that did not fit
     const int lmax = std::max(X.max_len, Y.max_len);
     const int likely = std::min(max_str / 2, lmax + lmax / 16 + 32);
-    if (launch_zlen(ctx, d_st, ns, d_c, max_str / 2, latin1, st, likely)) return -1;
-    if (launch_zlen(ctx, d_st + ns, nc, d_c + ns, max_str, latin1, st, 2 * likely)) return -1;
-    hipLaunchKernelGGL(k_ncd_slot_finish, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, d_c, d_c + ns, n,
+    if (launch_zlen2(ctx, d_fused, nf, d_cab, d_ca, max_str, latin1, st, 2 * likely)) return -1;
+    if (launch_zlen(ctx, d_single, ns, d_cs, max_str / 2, latin1, st, likely)) return -1;
+    hipLaunchKernelGGL(k_ncd_slot_finish, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, d_cab, d_ca, d_cs, n,
                        ss.no, out, ostride, ocol);
     HIP_TRY(ctx, hipGetLastError());
     return 0;

@@ -31,7 +31,7 @@ constexpr size_t ZS_HEAD = (size_t)zl::HASH_SIZE * 2;
 
 __global__ void __launch_bounds__(64, 4)
 k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, uint8_t* __restrict__ slabs,
-       int32_t* __restrict__ out, int latin1, int redo) {
+       int32_t* __restrict__ out, int latin1, int redo, int first_only) {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     uint8_t* slab = slabs + tid * ZS_SLAB;
@@ -40,7 +40,8 @@ k_zlen(const ZStream* __restrict__ st, int64_t n, uint16_t* __restrict__ heads, 
     for (int64_t s = tid; s < n; s += nthreads) {
         if (redo && out[s] != -1) continue;  // a second pass: only the streams the first one declined
         const ZStream d = st[s];
-        out[s] = d.na < 0 ? ZLEN_SKIPPED : zl::compressed_len(d.a, d.na, d.b, d.nb, z, *t, latin1 != 0);
+        out[s] = d.na < 0 ? ZLEN_SKIPPED
+                          : zl::compressed_len(d.a, d.na, d.b, first_only ? 0 : d.nb, z, *t, latin1 != 0);
     }
 }
 
@@ -61,6 +62,26 @@ k_zlen_wave(const ZStream* __restrict__ st, int64_t n, int nmax, int32_t* __rest
         }
         const int r = d.na + d.nb <= nmax ? zlw::compressed_len_wave(d.a, d.na, d.b, d.nb, zsm, nmax, lane) : -1;
         if (lane == 0) out[s] = r;  // -1: longer than the launch promised (the host checks)
+        __syncthreads();
+    }
+}
+
+// The fused form (zlen_wave.hpp compressed_len_wave2): out[s] = C(a + b) and out_a[s] = C(a) of the
+// same stream descriptor, one sort and a shared parse prefix.
+__global__ void __launch_bounds__(64)
+k_zlen_wave2(const ZStream* __restrict__ st, int64_t n, int nmax, int32_t* __restrict__ out, int32_t* __restrict__ out_a,
+             int redo) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t zsm[];
+    const int lane = (int)threadIdx.x;
+    for (int64_t s = blockIdx.x; s < n; s += gridDim.x) {
+        if (redo && out[s] != -1) continue;  // wave-uniform
+        const ZStream d = st[s];
+        int ca = -1, r = -1;
+        if (d.na + d.nb <= nmax) r = zlw::compressed_len_wave2(d.a, d.na, d.b, d.nb, zsm, nmax, lane, &ca);
+        if (lane == 0) {
+            out[s] = r;  // -1: longer than the launch promised (a redo pass takes it)
+            out_a[s] = ca;
+        }
         __syncthreads();
     }
 }
@@ -155,12 +176,12 @@ k_ncd_finish_cached(const int32_t* __restrict__ c12, const int32_t* __restrict__
 // slen[s] bytes.  Orientation 0 is the ordered pair (a, b): x = sx, y = sy.  Orientation 1 is
 // Biopython's alignment of (b, a) written in (a, b) column order, so its metric sees x = sy, y = sx.
 //
-// Streams per pair: singles[p][4] = C(x0), C(y0), C(x1), C(y1) and concat[p][2] = C(x0 + y0),
-// C(x1 + y1) (x_o, y_o the metric's first and second string of orientation o).  One wave per
-// pair compares the two orientations' strings: when they are the same alignment (no Ix / Iy tie on
-// the path, most pairs) orientation 1's singles ARE orientation 0's (swapped), so those two
-// streams are marked skipped (na = -1) and only the concatenation y0 + x0 is new: 4 streams per
-// pair instead of 6.
+// Jobs per pair: fused[p][o] = (x_o, y_o), o < no, each giving C(x_o + y_o) and C(x_o) in one pass
+// (k_zlen_wave2), and singles[p][2] = C(y0), C(x1) (x_o, y_o: the metric's first and second string of
+// orientation o).  One wave per pair compares the two orientations' strings: when they are the same
+// alignment (no Ix / Iy tie on the path, most pairs) x1 = y0 and y1 = x0, so C(y0) and C(x1) ARE the
+// fused jobs' C(x1) and C(x0) and both singles are marked skipped (na = -1): two fused jobs per pair
+// instead of six separate streams.
 __device__ __forceinline__ void ncd_slot(const uint8_t* sx, const uint8_t* sy, const int32_t* slen, int64_t cap,
                                          int nslot, int o, int64_t p, int64_t end, const uint8_t*& x,
                                          const uint8_t*& y, int32_t& len) {
@@ -174,7 +195,7 @@ __device__ __forceinline__ void ncd_slot(const uint8_t* sx, const uint8_t* sy, c
 __global__ void __launch_bounds__(256)
 k_ncd_slot_streams(const uint8_t* __restrict__ sx, const uint8_t* __restrict__ sy, const int32_t* __restrict__ slen,
                    int64_t cap, int nslot, int no, const int64_t* __restrict__ d_end, SetView XS, SetView YS,
-                   PairSrc ps, int64_t n, ZStream* __restrict__ singles, ZStream* __restrict__ concat) {
+                   PairSrc ps, int64_t n, ZStream* __restrict__ fused, ZStream* __restrict__ singles) {
     const int lane = (int)(threadIdx.x & 63);
     const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (p >= n) return;  // wave-uniform
@@ -191,9 +212,9 @@ k_ncd_slot_streams(const uint8_t* __restrict__ sx, const uint8_t* __restrict__ s
     ncd_slot(sx, sy, slen, cap, nslot, 0, p, end, x0, y0, l0);
     if (no == 1) {
         if (lane == 0) {
-            singles[p * 2] = ZStream{x0, nullptr, l0, 0};
-            singles[p * 2 + 1] = ZStream{y0, nullptr, l0, 0};
-            concat[p] = ZStream{x0, y0, l0, l0};
+            fused[p] = ZStream{x0, y0, l0, l0};
+            singles[p * 2] = ZStream{y0, nullptr, l0, 0};
+            singles[p * 2 + 1] = ZStream{y0, nullptr, -1, 0};
         }
         return;
     }
@@ -207,32 +228,27 @@ k_ncd_slot_streams(const uint8_t* __restrict__ sx, const uint8_t* __restrict__ s
         diff = __ballot(d) != 0;
     }
     if (lane == 0) {
-        singles[p * 4] = ZStream{x0, nullptr, l0, 0};
-        singles[p * 4 + 1] = ZStream{y0, nullptr, l0, 0};
-        // orientation 1: x = b's string (sy), y = a's (sx)
-        singles[p * 4 + 2] = ZStream{y1, nullptr, diff ? l1 : -1, 0};
-        singles[p * 4 + 3] = ZStream{x1, nullptr, diff ? l1 : -1, 0};
-        concat[p * 2] = ZStream{x0, y0, l0, l0};
-        concat[p * 2 + 1] = ZStream{y1, x1, l1, l1};
+        fused[p * 2] = ZStream{x0, y0, l0, l0};      // (a, b): x = a's string, y = b's
+        fused[p * 2 + 1] = ZStream{y1, x1, l1, l1};  // (b, a): x = b's string (sy), y = a's (sx)
+        singles[p * 2] = ZStream{y0, nullptr, diff ? l0 : -1, 0};
+        singles[p * 2 + 1] = ZStream{x1, nullptr, diff ? l1 : -1, 0};
     }
 }
 
-// out[(p * no + o) * ostride + ocol] = NCD of orientation o; a skipped single (-2) is orientation 0's
-// (swapped: min / max do not care).
+// out[(p * no + o) * ostride + ocol] = NCD of orientation o from the fused jobs' C(x_o + y_o) (cab) and
+// C(x_o) (ca) and C(y_o): the single's, or -- skipped: both orientations hold the same alignment -- the
+// other orientation's fused C(x).
 __global__ void __launch_bounds__(256)
-k_ncd_slot_finish(const int32_t* __restrict__ cs, const int32_t* __restrict__ cc, int64_t n, int no,
-                  double* __restrict__ out, int64_t ostride, int ocol) {
+k_ncd_slot_finish(const int32_t* __restrict__ cab, const int32_t* __restrict__ ca, const int32_t* __restrict__ cs,
+                  int64_t n, int no, double* __restrict__ out, int64_t ostride, int ocol) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n * no) return;
     const int64_t p = t / no;
     const int o = (int)(t - p * no);
-    const int32_t* c = cs + p * 2 * no;
-    int32_t c1 = c[2 * o], c2 = c[2 * o + 1];
-    if (c1 == ZLEN_SKIPPED) {
-        c1 = c[0];
-        c2 = c[1];
-    }
-    const double d1 = c1, d2 = c2, d12 = cc[t];
+    const int32_t c1 = ca[t];
+    int32_t c2 = cs[p * 2 + o];
+    if (c2 == ZLEN_SKIPPED) c2 = ca[p * no + (o ^ 1)];
+    const double d1 = c1, d2 = c2, d12 = cab[t];
     const double mn = d1 < d2 ? d1 : d2, mx = d1 < d2 ? d2 : d1;
     out[t * ostride + ocol] = (d12 - mn) / mx;
 }

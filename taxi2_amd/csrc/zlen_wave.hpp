@@ -135,8 +135,19 @@ __device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint
 }
 
 // len(zlib.compress(upper(a) + upper(b))); n = na + nb <= nmax (the caller's LDS layout).
-__device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_t* b, int nb, uint8_t* lds, int nmax,
-                                          int lane) {
+//
+// With c_a (nb > 0): len(zlib.compress(upper(a))) too, from the same sort and a shared parse prefix.
+// deflate_slow's decisions at position s read the window only below s + MAX_MATCH (the match scan,
+// capped at MAX_MATCH; candidates and the inserted hashes lie below s) and its lookahead caps
+// (nice_match, the returned length) bind only within MAX_MATCH of the end, so while s + MIN_LOOKAHEAD
+// <= na the parse of a + b and the parse of a alone are the same sequence of states.  The parse of
+// a + b snapshots its state (tallies, match state, block position) at the first step past that
+// point, runs to its end, and the parse of a alone resumes from the snapshot with the window zeroed
+// past na (what the one-stream form loads there).  The sorted keys of a + b serve a alone: a chain
+// walks only earlier positions of the same hash, and those lie below na - 2.  NCD needs C(x) and
+// C(x + y) of the same x (distances.py:351-358): one sort and ~three quarters of C(x)'s parse saved.
+__device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8_t* b, int nb, uint8_t* lds, int nmax,
+                                           int lane, int* c_a) {
     using namespace zl;
     const int n = na + nb;
     uint8_t* win = lds;
@@ -209,7 +220,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     int64_t bits = 0;
     int block_start = 0, last_lit = 0;
     int strstart = 0, lookahead = n;
-    int match_length = MIN_MATCH - 1, prev_length, match_start = 0, prev_match;
+    int match_length = MIN_MATCH - 1, prev_length = 0, match_start = 0, prev_match = 0;
     bool match_available = false;
     auto flush = [&](bool last) {  // FLUSH_BLOCK_ONLY, lane 0; bits broadcast
         __syncthreads();
@@ -227,6 +238,7 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
     // it (the literal a step there tallies); the serial parse then reads them with v_readlane.
     int pb = -64;
     uint32_t pinf = 0, phash = 0, pbyte = 0;
+    int nn = n;  // the stream being parsed ends here (na for a alone after the fork)
     auto prefetch = [&](int s0) {
         pb = s0;
         const int p = s0 + lane;
@@ -243,60 +255,126 @@ __device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_
         }
         pinf = v;
         phash = hq;
-        pbyte = (p >= 1 && p <= n) ? win[p - 1] : 0u;
+        pbyte = (p >= 1 && p <= nn) ? win[p - 1] : 0u;
     };
     // tallies: no-return LDS atomics on the u16 frequency pairs (lane 0), nothing waits on them
     auto tally = [&](uint16_t* f, int c) {
         if (lane == 0) atomicAdd(reinterpret_cast<uint32_t*>(f + (c & ~1)), 1u << (16 * (c & 1)));
     };
-    while (lookahead != 0) {
-        if (strstart - pb >= 64) prefetch(strstart);
-        const int sl = strstart - pb;
-        int hash_head = 0, i0 = 0;
-        uint32_t hq = 0;
-        if (lookahead >= MIN_MATCH) {  // insert(strstart): hash_head = the newest earlier same-hash position
-            const uint32_t inf = __builtin_amdgcn_readlane(pinf, sl);
-            i0 = (int)(inf & 0xFFFFu);
-            hash_head = (int)(inf >> 16);
-            hq = __builtin_amdgcn_readlane(phash, sl);
-        }
-        prev_length = match_length;
-        prev_match = match_start;
-        match_length = MIN_MATCH - 1;
-        if (hash_head != 0 && prev_length < LAZY && strstart - hash_head <= MAX_DIST) {
-            match_length = coop_longest_match(win, spos, i0, hq, strstart, lookahead, prev_length, match_start, lane);
-            if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > TOO_FAR)
-                match_length = MIN_MATCH - 1;
-        }
-        if (prev_length >= MIN_MATCH && match_length <= prev_length) {
-            tally(t.lfc, length_code(prev_length - MIN_MATCH) + LITERALS + 1);  // _tr_tally_dist
-            tally(t.dfc, dist_code(strstart - 1 - prev_match - 1));
-            const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
-            lookahead -= prev_length - 1;
-            strstart += prev_length - 2;  // the match's other positions (inserted by the sort)
-            match_available = false;
+    // the fork (c_a): the state at the first step with strstart + MIN_LOOKAHEAD > na
+    const bool fork = c_a != nullptr && nb > 0;
+    const int fork_at = na - MIN_LOOKAHEAD;
+    bool snapped = !fork;
+    int64_t f_bits = 0;
+    int f_block_start = 0, f_last_lit = 0, f_strstart = 0, f_match_length = MIN_MATCH - 1, f_match_start = 0;
+    bool f_match_available = false;
+    uint32_t f_tal[3] = {0u, 0u, 0u};  // lfc[0..286) + dfc[0..30) as 158 u16 pairs, three per lane
+    constexpr int TAL_L = L_CODES / 2, TAL_W = L_CODES / 2 + D_CODES / 2;
+    auto tal_word = [&](int w) -> uint32_t* {
+        return w < TAL_L ? reinterpret_cast<uint32_t*>(t.lfc) + w : reinterpret_cast<uint32_t*>(t.dfc) + (w - TAL_L);
+    };
+    auto parse = [&]() {
+        while (lookahead != 0) {
+            if (!snapped && strstart > fork_at) {  // a alone parses the same up to here: keep the state
+                snapped = true;
+                __syncthreads();  // lane 0's tallies are in LDS
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int w = lane + 64 * q;
+                    f_tal[q] = w < TAL_W ? *tal_word(w) : 0u;
+                }
+                f_bits = bits;
+                f_block_start = block_start;
+                f_last_lit = last_lit;
+                f_strstart = strstart;
+                f_match_length = match_length;
+                f_match_start = match_start;
+                f_match_available = match_available;
+            }
+            if (strstart - pb >= 64) prefetch(strstart);
+            const int sl = strstart - pb;
+            int hash_head = 0, i0 = 0;
+            uint32_t hq = 0;
+            if (lookahead >= MIN_MATCH) {  // insert(strstart): hash_head = the newest earlier same-hash position
+                const uint32_t inf = __builtin_amdgcn_readlane(pinf, sl);
+                i0 = (int)(inf & 0xFFFFu);
+                hash_head = (int)(inf >> 16);
+                hq = __builtin_amdgcn_readlane(phash, sl);
+            }
+            prev_length = match_length;
+            prev_match = match_start;
             match_length = MIN_MATCH - 1;
-            strstart++;
-            if (bflush) flush(false);
-        } else if (match_available) {
-            tally(t.lfc, (int)__builtin_amdgcn_readlane(pbyte, sl));
-            const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
-            if (bflush) flush(false);
-            strstart++;
-            lookahead--;
-        } else {
-            match_available = true;
-            strstart++;
-            lookahead--;
+            if (hash_head != 0 && prev_length < LAZY && strstart - hash_head <= MAX_DIST) {
+                match_length = coop_longest_match(win, spos, i0, hq, strstart, lookahead, prev_length, match_start, lane);
+                if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > TOO_FAR)
+                    match_length = MIN_MATCH - 1;
+            }
+            if (prev_length >= MIN_MATCH && match_length <= prev_length) {
+                tally(t.lfc, length_code(prev_length - MIN_MATCH) + LITERALS + 1);  // _tr_tally_dist
+                tally(t.dfc, dist_code(strstart - 1 - prev_match - 1));
+                const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
+                lookahead -= prev_length - 1;
+                strstart += prev_length - 2;  // the match's other positions (inserted by the sort)
+                match_available = false;
+                match_length = MIN_MATCH - 1;
+                strstart++;
+                if (bflush) flush(false);
+            } else if (match_available) {
+                tally(t.lfc, (int)__builtin_amdgcn_readlane(pbyte, sl));
+                const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
+                if (bflush) flush(false);
+                strstart++;
+                lookahead--;
+            } else {
+                match_available = true;
+                strstart++;
+                lookahead--;
+            }
         }
-    }
-    if (match_available) tally(t.lfc, win[strstart - 1]);
+        if (match_available) tally(t.lfc, win[strstart - 1]);
+        flush(true);
+        return 2 + (int)(bits >> 3) + 4;
+    };
     ZLW_T(tw3);
-    ZLW_ADD(2, tw3 - tw2);
-    flush(true);
+    const int c_ab = parse();
     ZLW_T(tw4);
-    ZLW_ADD(3, tw4 - tw3);
-    return 2 + (int)(bits >> 3) + 4;
+    ZLW_ADD(2, tw4 - tw3);
+    if (fork) {  // a alone from the snapshot: the window past na as the one-stream form has it (zeros)
+        if (!snapped) {  // (a + b ended before the fork point: a is too short to share anything)
+            f_strstart = 0;
+            f_match_length = MIN_MATCH - 1;
+        }
+        for (int i = na + lane; i < n + MAX_MATCH + 12; i += 64) win[i] = 0;
+        __syncthreads();
+        if (lane == 0) init_block(t);
+        __syncthreads();
+        if (snapped) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int w = lane + 64 * q;
+                if (w < TAL_W) *tal_word(w) = f_tal[q];
+            }
+        }
+        __syncthreads();
+        bits = snapped ? f_bits : 0;
+        block_start = snapped ? f_block_start : 0;
+        last_lit = snapped ? f_last_lit : 0;
+        strstart = f_strstart;
+        lookahead = na - strstart;
+        match_length = f_match_length;
+        match_start = snapped ? f_match_start : 0;
+        match_available = snapped && f_match_available;
+        nn = na;
+        pb = -64;  // the prefetched literals past na changed
+        *c_a = parse();
+    }
+    return c_ab;
+}
+
+// len(zlib.compress(upper(a) + upper(b))); n = na + nb <= nmax (the caller's LDS layout).
+__device__ inline int compressed_len_wave(const uint8_t* a, int na, const uint8_t* b, int nb, uint8_t* lds, int nmax,
+                                          int lane) {
+    return compressed_len_wave2(a, na, b, nb, lds, nmax, lane, nullptr);
 }
 
 }  // namespace zlw

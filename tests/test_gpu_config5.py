@@ -157,3 +157,25 @@ def test_aligned_streamed_reductions_vs_dense_and_oracle(tmp_path, engine, oracl
         m = np.arange(n) != x
         assert np.array_equal(np.isfinite(e[m]), np.isfinite(got[m]))
         assert np.array_equal(_bits(e[m][np.isfinite(e[m])]), _bits(got[m][np.isfinite(got[m])]))
+
+
+@pytest.mark.timeout(900)
+def test_streamed_subsets_exact_vs_dense_16000(tmp_path, engine):
+    """the streamed subset statistics (exact parallel sums) against the dense
+    path's sequential host aggregation at N = 16 000 (2.56e8 ordered pairs, 6 GB dense), bit for bit
+    -- 16x the pairs of the N = 4 000 check, every block boundary and binade change of a long run."""
+    from bench_secondary import build_config5_task as build_task
+
+    n, L = 16_000, 300
+    dense, _, _ = build_task(n, L, engine, tmp_path / "dense", 0.5)
+    dense.params.engine.stream = False
+    dense.params.engine.row_minima = None
+    dense.start()
+    streamed, _, _ = build_task(n, L, engine, tmp_path / "stream", 0.5)
+    streamed.start()
+    for name in ("genera", "species"):
+        a, b = dense.subset_stats[name], streamed.subset_stats[name]
+        assert a.subsets == b.subsets
+        assert np.array_equal(a.count, b.count)
+        for x, y in ((a.mean, b.mean), (a.min, b.min), (a.max, b.max)):
+            assert np.array_equal(_bits(np.nan_to_num(x, nan=-7.0)), _bits(np.nan_to_num(y, nan=-7.0))), name

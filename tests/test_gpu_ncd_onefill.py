@@ -215,3 +215,65 @@ def test_self_strings_mismatch_above_match(engine):
         assert got[k] == (ax, ay)
     assert got[0] != (raw[0], raw[0])  # the shifted alignment, not the identity
     st.free()
+
+
+def test_ncd_slots_fused_lengths_edges(engine):
+    """taxi2_ncd_slots_dev on crafted slot strings: every orientation's NCD equals alfpy's formula over
+    Python's zlib, where the fused deflate pass (C(x) from the parse of x + y, forked MIN_LOOKAHEAD
+    before x's end) meets its edges -- x shorter than the fork margin (0, 1, 3, 200, 261, 262, 263
+    bytes), matches running through the fork point and across x's end (periodic x, y = x, y a
+    suffix of x), long literal runs, gaps, and orientation pairs that differ (the singles)."""
+    import torch
+
+    from oracle import restatement as R
+
+    rng = random.Random(17)
+
+    def dna(n, alpha="ACGT"):
+        return "".join(rng.choice(alpha) for _ in range(n))
+
+    xs, ys = [], []
+    for L in (0, 1, 3, 200, 261, 262, 263, 264, 300, 520, 777, 1000):
+        xs.append(dna(L))
+        ys.append(dna(rng.randrange(0, 600)))
+    per = "ACGTTGCA" * 120
+    xs += [per[:500], per[:700], per[:1000], "A" * 900, dna(400, "AC-")]
+    ys += [per[:500], per[200:900], per[:30], "A" * 5, dna(380, "AC-")]
+    base = dna(800)
+    xs += [base, base[:600] + dna(200)]
+    ys += [base[300:], base[100:]]
+    n = len(xs)
+    # two orientations per pair: the second one is (x, y) itself (same alignment) for even k, a
+    # different pair of strings for odd k -- the skipped and the computed singles
+    o1 = [(xs[k], ys[k]) if k % 2 == 0 else (dna(len(xs[k]) // 2 + 5), dna(len(ys[k]) // 2 + 3)) for k in range(n)]
+    lens = [max(len(xs[k]), len(ys[k]), len(o1[k][0]), len(o1[k][1])) for k in range(n)]
+    cap = 2 * max(lens) + 8
+    end = np.array([cap - 4] * n, dtype=np.int64)
+    sx = np.zeros((n, 2, cap), dtype=np.uint8)
+    sy = np.zeros((n, 2, cap), dtype=np.uint8)
+    sl = np.zeros((n, 2), dtype=np.int32)
+    for k in range(n):
+        # slot strings are the two aligned strings, equal length: pad the shorter with gaps
+        for o, (a, b) in enumerate(((xs[k], ys[k]), o1[k])):
+            m = max(len(a), len(b))
+            a, b = a.ljust(m, "-"), b.ljust(m, "-")
+            sx[k, o, end[k] - m:end[k]] = np.frombuffer(a.encode(), np.uint8)
+            sy[k, o, end[k] - m:end[k]] = np.frombuffer(b.encode(), np.uint8)
+            sl[k, o] = m
+    dev = torch.device("cuda", 0)
+    t = {k: torch.as_tensor(v, device=dev) for k, v in (("sx", sx), ("sy", sy), ("sl", sl), ("end", end))}
+    out = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    engine.ncd_slots_dev(t["sx"].data_ptr(), t["sy"].data_ptr(), t["sl"].data_ptr(), cap, 2, 2, t["end"].data_ptr(), n,
+                         cap // 2, out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for k in range(n):
+        m0 = int(sl[k, 0])
+        a0 = bytes(sx[k, 0, end[k] - m0:end[k]]).decode()
+        b0 = bytes(sy[k, 0, end[k] - m0:end[k]]).decode()
+        m1 = int(sl[k, 1])
+        a1 = bytes(sx[k, 1, end[k] - m1:end[k]]).decode()
+        b1 = bytes(sy[k, 1, end[k] - m1:end[k]]).decode()
+        e0, e1 = R.ncd(a0, b0), R.ncd(b1, a1)  # orientation 1 is the (b, a) metric
+        assert (np.isnan(got[k, 0]) and e0 is None) or got[k, 0] == e0, (k, len(a0))
+        assert (np.isnan(got[k, 1]) and e1 is None) or got[k, 1] == e1, (k, len(a1))
