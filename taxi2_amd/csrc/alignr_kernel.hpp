@@ -61,6 +61,12 @@ constexpr int AR_TS = TAXI2_AR_TS;
 #define TAXI2_AR_SKIP 0
 #endif
 constexpr bool AR_SKIP = TAXI2_AR_SKIP != 0;
+// prefetch of the next step's table offset (see the fill's step loop): off -- the extra live register
+// takes the kernel to 130 VGPRs, i.e. 3 waves per SIMD instead of 4 (tools/isa_alignr.hip)
+#ifndef TAXI2_AR_PREC
+#define TAXI2_AR_PREC 0
+#endif
+constexpr bool AR_PREC = TAXI2_AR_PREC != 0;
 __host__ __device__ constexpr int ar_pw(int K) { return K % 4 == 0 ? 4 : 2; }
 // byte offset of (step, lane, column k) in a chain's trace buffer (NT lanes)
 // (AR_TS = 0: the plain [step][lane][4K bytes] layout, for comparison)
@@ -564,12 +570,16 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             // one systolic step of fill wave WI (a compile-time index: the ring slots, the lane's
             // column block and its table row are immediate offsets).  Wave 0 takes the column-0
             // boundary; every wave but the last hands its last lane's row on through the ring.
-            auto step = [&](auto WIC, const int s) {
+            auto rec_addr = [&](const int s) -> const char* {  // this lane's row record at step s
+                return (const char*)xinfo + ((((uint32_t)s << 4) - ln16) & ((XR - 1) << 4));
+            };
+            // recx: the record's table offset (.x), read ahead of the step when AR_PREC
+            auto step = [&](auto WIC, const int s, const uint32_t recx) {
                 constexpr int WI = decltype(WIC)::value;
                 constexpr bool FW = WI == 0, HO = WI < W - 1;
                 const int g = s - ln;
                 const int tq = WI * 64 + ln;
-                const uint4 rec = *(const uint4*)((const char*)xinfo + ((((uint32_t)s << 4) - ln16) & ((XR - 1) << 4)));
+                const uint4 rec = *(const uint4*)rec_addr(s);
                 uint2 o_ring = make_uint2(0u, 0u);
                 if constexpr (!FW) o_ring = ring[(WI - 1) * AR_RING + ((s + 1) & (AR_RING - 1))];
                 const bool in_band = (uint8_t)((uint32_t)tq - rec.y) <= (uint8_t)(rec.y >> 8);
@@ -590,7 +600,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     // the row base's table, this lane's EP words of each piece (lane-contiguous reads)
                     // (lane-first base: the other address forms cost the allocator a 129th VGPR, i.e.
                     // one wave per SIMD at the 128-register budget)
-                    const char* tb = (const char*)&eqt[0][0][tq][0] + rec.x;
+                    const char* tb = (const char*)&eqt[0][0][tq][0] + recx;
 #pragma unroll
                     for (int q = 0; q < K / EP; ++q) {
                         const char* pq = tb + (size_t)(q * NT) * (EP * 4);
@@ -728,10 +738,27 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     const unsigned long long t1 = AR_NOW();
                     pf[4] += t1 - t0;
 #endif
+                    // AR_PREC: step s + 1's table offset (record word .x) is read during step s, so its
+                    // eqt reads issue at the top of the step instead of behind a dependent LDS read.  Within
+                    // the block only: wave 0 writes the next 64 rows' records after a block whose end
+                    // is a multiple of 64, so a record past s1 may not be written yet.
+                    auto recx_at = [&](const int s) { return *(const uint32_t*)rec_addr(s); };
+                    auto run = [&](auto WIC) {
+                        if constexpr (AR_PREC) {
+                            uint32_t rx = recx_at(s0);
+                            for (int s = s0; s < s1; ++s) {
+                                const uint32_t nxt = recx_at(s + 1 < s1 ? s + 1 : s);
+                                step(WIC, s, rx);
+                                rx = nxt;
+                            }
+                        } else {
+                            for (int s = s0; s < s1; ++s) step(WIC, s, recx_at(s));
+                        }
+                    };
                     if (w == 0) {
-                        for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 0>{}, s);
+                        run(std::integral_constant<int, 0>{});
                     } else if constexpr (W > 1) {
-                        for (int s = s0; s < s1; ++s) step(std::integral_constant<int, 1>{}, s);
+                        run(std::integral_constant<int, 1>{});
                     }
 #ifdef AR_PROF
                     pf[0] += AR_NOW() - t1;
