@@ -331,6 +331,25 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
                          const int64_t* label_offs, int decimals, const uint8_t* missing, int32_t missing_len,
                          uint8_t* out, int64_t cap, int64_t* out_len);
 
+/* taxi2_format_rows / taxi2_format_summary on values already in device memory (a row block the
+ * engine produced, e.g. versusAll's adjusted rows): value slot g = r * ncols + c starts at
+ * d_vals + g * vstride (vstride >= nm doubles: a metric's column of a wider block is d_vals + m with
+ * vstride = the block's metric count), so the writers' values never cross the host link.  The
+ * fixed-point range check runs on the device (a row with a larger finite value fails the call);
+ * `stream` orders the reads after the values' producer (NULL: the context's stream).  Blocks the
+ * caller until the text is in `out` (pinned host memory is written directly by the kernel). */
+int taxi2_format_rows_dev(taxi2_ctx* ctx, int mode, const double* d_vals, int64_t vstride, int64_t nrows,
+                          int64_t ncols, int nm, const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                          const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                          uint8_t* out, int64_t cap, int64_t* out_len, void* stream);
+int taxi2_format_summary_dev(taxi2_ctx* ctx, const double* d_vals, int64_t vstride, int64_t nrows, int64_t ncols,
+                             int nm, const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                             const int64_t* col_offs, const uint8_t* row_suf, const int64_t* row_suf_offs,
+                             const uint8_t* col_suf, const int64_t* col_suf_offs, const int32_t* row_codes,
+                             const int32_t* col_codes, int has_genera, int has_species, const uint8_t* labels,
+                             const int64_t* label_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                             uint8_t* out, int64_t cap, int64_t* out_len, void* stream);
+
 /* Host-only (no context): the text of the subset statistics files (versus_all.py:642-684, written by
  * tasks/subsets.py write_subset_statistics) for a partition of ns subsets and m metrics, with the
  * handlers' "{:.Nf}" formatter (N = decimals) and missing text "NA".  mean / mn / mx / count are

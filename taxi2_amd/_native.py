@@ -56,6 +56,8 @@ EXPORTS = (
     "taxi2_format_rows",
     "taxi2_format_ragged",
     "taxi2_format_summary",
+    "taxi2_format_rows_dev",
+    "taxi2_format_summary_dev",
     "taxi2_subset_aggregate",
     "taxi2_format_subset_stats",
     "taxi2_subset_aggregate_dev",
@@ -74,6 +76,30 @@ COUNTS_CODE = 16
 # strings (one fill per pair for every metric); other entry points take it through taxi2_ncd_pairs
 NCD_CODE = 4
 MAX_METRICS = 8
+
+
+def _dev_vals(vals, stream):
+    """(data pointer, (nrows, ncols, nm), value stride, stream) of a float64 CUDA tensor whose value
+    slots (r, c) lie at a fixed stride -- (nrows, ncols, nm) with unit metric stride, or (nrows, ncols)
+    -- else None (host values)."""
+    if not (hasattr(vals, "is_cuda") and vals.is_cuda):
+        return None
+    import torch
+
+    if vals.dtype != torch.float64:
+        raise ValueError("device values must be float64")
+    if vals.dim() == 2:
+        nrows, ncols, nm = vals.shape[0], vals.shape[1], 1
+    elif vals.dim() == 3 and (vals.shape[2] == 1 or vals.stride(2) == 1):
+        nrows, ncols, nm = vals.shape
+    else:
+        raise ValueError("device values must be (nrows, ncols) or (nrows, ncols, nm) with unit metric stride")
+    vs = vals.stride(1)
+    if ncols > 1 and nrows > 1 and vals.stride(0) != ncols * vs:
+        raise ValueError("device value rows must be contiguous slot runs")
+    if vs < nm:
+        raise ValueError("device value slots overlap")
+    return vals.data_ptr(), (nrows, ncols, nm), int(vs), stream
 
 
 class NativeError(RuntimeError):
@@ -137,6 +163,10 @@ _SIGNATURES = {
                                    _I64, ctypes.POINTER(_I64)]),
     "taxi2_format_summary": (_INT, [_P, _P, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _INT, _INT,
                                     _P, _P, _INT, _P, _I32, _P, _I64, ctypes.POINTER(_I64)]),
+    "taxi2_format_rows_dev": (_INT, [_P, _INT, _P, _I64, _I64, _I64, _INT, _P, _P, _P, _P, _INT, _P, _I32, _P, _I64,
+                                     ctypes.POINTER(_I64), _P]),
+    "taxi2_format_summary_dev": (_INT, [_P, _P, _I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                        _INT, _INT, _P, _P, _INT, _P, _I32, _P, _I64, ctypes.POINTER(_I64), _P]),
     "taxi2_subset_aggregate": (_INT, [_P, _I64, _INT, _P, _I32, _P, _P, _P, _P, _INT]),
     "taxi2_format_subset_stats": (_INT, [_I64, _INT, _P, _P, _P, _P, _P, _P, _INT, _INT, _P, _I64,
                                          ctypes.POINTER(_I64), _INT]),
@@ -727,13 +757,22 @@ class Engine:
                 )
         return out
 
-    def format_rows(self, vals: np.ndarray, row_pre, col_pre=None, *, decimals: int = 4,
-                    missing: str = "NA", view: bool = False):
+    def format_rows(self, vals, row_pre, col_pre=None, *, decimals: int = 4,
+                    missing: str = "NA", view: bool = False, stream: int | None = None):
         """Writer text (taxi2_format_rows): ``vals`` (nrows, ncols, nm) -> linear rows
         ``row_pre TAB col_pre (TAB value){nm} LF`` per cell; (nrows, ncols) with ``col_pre=None``
-        -> matrix rows ``row_pre (TAB value){ncols} LF``.  Values as Python "%.{decimals}f"."""
-        v = np.ascontiguousarray(vals, dtype=np.float64)
+        -> matrix rows ``row_pre (TAB value){ncols} LF``.  Values as Python "%.{decimals}f".
+        ``vals`` may be a float64 CUDA tensor (slots at a fixed stride, e.g. one metric of a
+        (rows, n, M) block): taxi2_format_rows_dev, ordered on ``stream``."""
         mode = 0 if col_pre is not None else 1
+        dev = _dev_vals(vals, stream)
+        if dev is not None:  # a float64 CUDA tensor: taxi2_format_rows_dev reads it where it is
+            v, nrows, ncols, nm = dev[0], *dev[1]
+            if mode == 1 and nm != 1:
+                raise ValueError("matrix text takes (nrows, ncols) values")
+            return self._format(mode, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing, view=view,
+                                dev=dev)
+        v = np.ascontiguousarray(vals, dtype=np.float64)
         if mode == 1 and v.ndim == 2:
             v = v[:, :, None]
         if v.ndim != 3:
@@ -761,12 +800,16 @@ class Engine:
 
     def format_summary(self, vals: np.ndarray, row_pre, col_pre, row_suf, col_suf, row_codes, col_codes, *,
                        has_genera: bool, has_species: bool, decimals: int = 4, missing: str = "NA",
-                       view: bool = False):
+                       view: bool = False, stream: int | None = None):
         """summary.tsv lines (taxi2_format_summary) for ``vals`` (nrows, ncols, nm): row_suf / col_suf
         = 2 strings per row / column (extras with leading TABs; TAB genus TAB species),
         row_codes / col_codes (n, 2) = (genus, species) subset codes."""
-        v = np.ascontiguousarray(vals, dtype=np.float64)
-        nrows, ncols, nm = v.shape
+        dev = _dev_vals(vals, stream)
+        if dev is not None:
+            v, (nrows, ncols, nm) = dev[0], dev[1]
+        else:
+            v = np.ascontiguousarray(vals, dtype=np.float64)
+            nrows, ncols, nm = v.shape
         rsb, rso = pack_strings(row_suf)
         csb, cso = pack_strings(col_suf)
         if len(rso) != 2 * nrows + 1 or len(cso) != 2 * ncols + 1:
@@ -777,10 +820,10 @@ class Engine:
         extra = (rsb, rso, csb, cso, rc_, cc_, int(bool(has_genera)), int(bool(has_species)), lb, lo)
         sfx = int(rso[-1]) * ncols + int(cso[-1]) * nrows + nrows * ncols * 16
         return self._format(2, v, nrows, None, None, ncols, nm, row_pre, col_pre, decimals, missing, extra, sfx,
-                            view=view)
+                            view=view, dev=dev)
 
     def _format(self, mode, v, nrows, rs, cs, ncols, nm, row_pre, col_pre, decimals, missing, summary=None,
-                extra_cap: int = 0, view: bool = False):
+                extra_cap: int = 0, view: bool = False, dev=None):
         """The formatter call; the text as bytes, or with ``view`` as a memoryview of the engine's
         pinned formatter buffer (valid until the next ``view`` call: write it out at once) -- the
         D2H then runs at full link rate into page-locked memory and no bytes copy is made."""
@@ -798,6 +841,8 @@ class Engine:
                   + (int(co[-1]) * nrows if mode != 1 and rs is None else 0)
                   + (int(np.diff(co).max(initial=0)) * ntok if mode == 0 and rs is not None else 0) + extra_cap)
         name = "taxi2_format_summary" if summary else "taxi2_format_rows" if rs is None else "taxi2_format_ragged"
+        if dev is not None:
+            name += "_dev"
         for _ in range(2):
             if view:
                 buf = getattr(self, "_fmt_buf", None)
@@ -809,7 +854,24 @@ class Engine:
                 out = np.empty(cap, dtype=np.uint8)
             cpre = (cb.ctypes.data if cb is not None else None, co.ctypes.data if co is not None else None)
             with self._lock:
-                if summary is not None:
+                if dev is not None:
+                    _, _, vstride, dst = dev
+                    vp = ctypes.c_void_p(v)
+                    if summary is not None:
+                        rsb, rso, csb, cso, rc_, cc_, hg, hs, lb, lo = summary
+                        rc = self._lib.taxi2_format_summary_dev(
+                            self._ctx, vp, vstride, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data, *cpre,
+                            rsb.ctypes.data, rso.ctypes.data, csb.ctypes.data, cso.ctypes.data, rc_.ctypes.data,
+                            cc_.ctypes.data, hg, hs, lb.ctypes.data, lo.ctypes.data, int(decimals), miss, len(miss),
+                            out.ctypes.data, cap, ctypes.byref(need), ctypes.c_void_p(dst) if dst else None,
+                        )
+                    else:
+                        rc = self._lib.taxi2_format_rows_dev(
+                            self._ctx, mode, vp, vstride, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data, *cpre,
+                            int(decimals), miss, len(miss), out.ctypes.data, cap, ctypes.byref(need),
+                            ctypes.c_void_p(dst) if dst else None,
+                        )
+                elif summary is not None:
                     rsb, rso, csb, cso, rc_, cc_, hg, hs, lb, lo = summary
                     rc = self._lib.taxi2_format_summary(
                         self._ctx, v.ctypes.data, nrows, ncols, nm, rb.ctypes.data, ro.ctypes.data, *cpre,

@@ -779,7 +779,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // up to 120 GB of the 288 GB HBM, at most 45 % of the device's memory (TAXI2_AT_TRACE_GB overrides)
     double budget_gb = std::min(120.0, 0.45 * (double)ctx->total_mem / 1e9);
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
-    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * std::max(1, Y.max_len)) - 64, 4 * v.K, v.W); };
+    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * std::max(1, Y.max_len)) - 64, (int)AR_WB * v.K, v.W); };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
     chunk = (int)eff;
     const int cap_rows = (int)eff * std::max(1, Y.max_len);
@@ -2197,7 +2197,8 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
                        const int64_t* rstart, const int32_t* cols, const uint8_t* row_pre, const int64_t* row_offs,
                        const uint8_t* col_pre, const int64_t* col_offs, int decimals, const uint8_t* missing,
                        int32_t missing_len, uint8_t* out, int64_t cap, int64_t* out_len,
-                       const SummaryHost* sm = nullptr) {
+                       const SummaryHost* sm = nullptr, bool dev_vals = false, int64_t vstride = 0,
+                       hipStream_t st_in = nullptr) {
     if (!ctx) return -1;
     if (!out_len || (nrows > 0 && (!vals || !row_pre || !row_offs))) return fail(ctx, "null argument");
     if (mode < 0 || mode > 2 || (mode == 2) != (sm != nullptr))
@@ -2223,20 +2224,27 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
             if (cols[g] < 0 || cols[g] >= ncols) return fail(ctx, "column %d out of range [0, %lld)", cols[g], (long long)ncols);
     }
     if (ntok == 0) return 0;
+    // dev_vals: `vals` is device memory, slot g at vals + g * vstride (the range check runs in
+    // k_fmt_row_len); host values are packed (vstride = nm), checked here and copied
+    if (dev_vals && ragged) return fail(ctx, "device values are rectangular blocks");
+    if (dev_vals && vstride < nm) return fail(ctx, "value stride %lld below the metric count", (long long)vstride);
+    const int64_t vs = dev_vals ? vstride : nm;
     const double* v0 = ragged ? vals + rstart[0] * nm : vals;
     const int64_t nv = ntok * nm;
     const double lim = std::ldexp(1.0, 63) / (double)pow10_u64(decimals);
-    for (int64_t k = 0; k < nv; ++k)
-        if (std::isfinite(v0[k]) && !(std::fabs(v0[k]) < lim))
-            return fail(ctx, "value %g too large for fixed-point text with %d decimals", v0[k], decimals);
+    if (!dev_vals)
+        for (int64_t k = 0; k < nv; ++k)
+            if (std::isfinite(v0[k]) && !(std::fabs(v0[k]) < lim))
+                return fail(ctx, "value %g too large for fixed-point text with %d decimals", v0[k], decimals);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t fst = st_in ? st_in : ctx->stream;
     const int64_t rp = row_offs[nrows] - row_offs[0];
     const int64_t cp = mode != 1 ? col_offs[ncols] - col_offs[0] : 0;
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
     const int64_t rs_b = sm ? sm->rsuf_offs[2 * nrows] - sm->rsuf_offs[0] : 0;
     const int64_t cs_b = sm ? sm->csuf_offs[2 * ncols] - sm->csuf_offs[0] : 0;
     const int64_t lab_b = sm ? sm->lab_offs[5] - sm->lab_offs[0] : 0;
-    const size_t b_vals = al(nv * 8), b_roffs = al((nrows + 1) * 8), b_coffs = al((ncols + 1) * 8),
+    const size_t b_vals = dev_vals ? 0 : al(nv * 8), b_roffs = al((nrows + 1) * 8), b_coffs = al((ncols + 1) * 8),
                  b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nrows * 8),
                  b_rst = ragged ? al((nrows + 1) * 8) : 0, b_cols = ragged ? al(ntok * 4) : 0,
                  b_rsuf = sm ? al(rs_b + 1) + al((2 * nrows + 1) * 8) + al(2 * nrows * 4) : 0,
@@ -2246,7 +2254,7 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
                          b_rsuf + b_csuf + b_lab;
     if (ensure(ctx, &ctx->d_fmt, &ctx->d_fmt_bytes, fixed)) return -1;
     char* base = (char*)ctx->d_fmt;
-    double* d_vals = (double*)base;
+    const double* d_vals = dev_vals ? vals : (const double*)base;
     int64_t* d_roffs = (int64_t*)(base + b_vals);
     int64_t* d_coffs = (int64_t*)((char*)d_roffs + b_roffs);
     uint8_t* d_rpre = (uint8_t*)d_coffs + b_coffs;
@@ -2282,38 +2290,41 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
         for (int64_t k = 0; k <= 2 * nrows; ++k) rso[k] = sm->rsuf_offs[k] - sm->rsuf_offs[0];
         for (int64_t k = 0; k <= 2 * ncols; ++k) cso[k] = sm->csuf_offs[k] - sm->csuf_offs[0];
         for (int k = 0; k < 6; ++k) lo[k] = sm->lab_offs[k] - sm->lab_offs[0];
-        if (rs_b) HIP_TRY(ctx, hipMemcpyAsync(d_rsuf, sm->rsuf + sm->rsuf_offs[0], rs_b, hipMemcpyHostToDevice, ctx->stream));
-        if (cs_b) HIP_TRY(ctx, hipMemcpyAsync(d_csuf, sm->csuf + sm->csuf_offs[0], cs_b, hipMemcpyHostToDevice, ctx->stream));
-        if (lab_b) HIP_TRY(ctx, hipMemcpyAsync(d_lab, sm->lab + sm->lab_offs[0], lab_b, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_rsoffs, rso.data(), rso.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_csoffs, cso.data(), cso.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_laboffs, lo.data(), 6 * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_rcode, sm->rcode, 2 * nrows * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_ccode, sm->ccode, 2 * ncols * 4, hipMemcpyHostToDevice, ctx->stream));
+        if (rs_b) HIP_TRY(ctx, hipMemcpyAsync(d_rsuf, sm->rsuf + sm->rsuf_offs[0], rs_b, hipMemcpyHostToDevice, fst));
+        if (cs_b) HIP_TRY(ctx, hipMemcpyAsync(d_csuf, sm->csuf + sm->csuf_offs[0], cs_b, hipMemcpyHostToDevice, fst));
+        if (lab_b) HIP_TRY(ctx, hipMemcpyAsync(d_lab, sm->lab + sm->lab_offs[0], lab_b, hipMemcpyHostToDevice, fst));
+        HIP_TRY(ctx, hipMemcpyAsync(d_rsoffs, rso.data(), rso.size() * 8, hipMemcpyHostToDevice, fst));
+        HIP_TRY(ctx, hipMemcpyAsync(d_csoffs, cso.data(), cso.size() * 8, hipMemcpyHostToDevice, fst));
+        HIP_TRY(ctx, hipMemcpyAsync(d_laboffs, lo.data(), 6 * 8, hipMemcpyHostToDevice, fst));
+        HIP_TRY(ctx, hipMemcpyAsync(d_rcode, sm->rcode, 2 * nrows * 4, hipMemcpyHostToDevice, fst));
+        HIP_TRY(ctx, hipMemcpyAsync(d_ccode, sm->ccode, 2 * ncols * 4, hipMemcpyHostToDevice, fst));
     }
     if (ragged) {
         for (int64_t r = 0; r <= nrows; ++r) rst[r] = rstart[r] - rstart[0];
-        HIP_TRY(ctx, hipMemcpyAsync(d_rst, rst.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_cols, cols + rstart[0], ntok * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_rst, rst.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, fst));
+        HIP_TRY(ctx, hipMemcpyAsync(d_cols, cols + rstart[0], ntok * 4, hipMemcpyHostToDevice, fst));
     }
-    HIP_TRY(ctx, hipMemcpyAsync(d_vals, v0, nv * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(d_roffs, roffs.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-    if (rp) HIP_TRY(ctx, hipMemcpyAsync(d_rpre, row_pre + row_offs[0], rp, hipMemcpyHostToDevice, ctx->stream));
+    if (!dev_vals) HIP_TRY(ctx, hipMemcpyAsync((double*)d_vals, v0, nv * 8, hipMemcpyHostToDevice, fst));
+    HIP_TRY(ctx, hipMemcpyAsync(d_roffs, roffs.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, fst));
+    if (rp) HIP_TRY(ctx, hipMemcpyAsync(d_rpre, row_pre + row_offs[0], rp, hipMemcpyHostToDevice, fst));
     if (mode != 1) {
-        HIP_TRY(ctx, hipMemcpyAsync(d_coffs, coffs.data(), (ncols + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        if (cp) HIP_TRY(ctx, hipMemcpyAsync(d_cpre, col_pre + col_offs[0], cp, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_coffs, coffs.data(), (ncols + 1) * 8, hipMemcpyHostToDevice, fst));
+        if (cp) HIP_TRY(ctx, hipMemcpyAsync(d_cpre, col_pre + col_offs[0], cp, hipMemcpyHostToDevice, fst));
     }
-    if (missing_len) HIP_TRY(ctx, hipMemcpyAsync(d_miss, missing, missing_len, hipMemcpyHostToDevice, ctx->stream));
+    if (missing_len) HIP_TRY(ctx, hipMemcpyAsync(d_miss, missing, missing_len, hipMemcpyHostToDevice, fst));
     FmtArgs a{mode, d_vals, nrows, ncols, nm, decimals, d_rpre, d_roffs, d_cpre, d_coffs, d_miss, missing_len,
               d_rst, d_cols, d_rsuf, d_rsoffs, d_csuf, d_csoffs, d_rcode, d_ccode, sm ? sm->has_g : 0,
-              sm ? sm->has_s : 0, d_lab, d_laboffs};
-    hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, ctx->stream, a, d_rlen);
+              sm ? sm->has_s : 0, d_lab, d_laboffs, vs, lim};
+    hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, fst, a, d_rlen);
     HIP_TRY(ctx, hipGetLastError());
     std::vector<int64_t> rlen(nrows), rbase(nrows);
-    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nrows * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nrows * 8, hipMemcpyDeviceToHost, fst));
+    HIP_TRY(ctx, hipStreamSynchronize(fst));
     int64_t total = 0;
     for (int64_t r = 0; r < nrows; ++r) {
+        if (rlen[r] >= ((int64_t)1 << 60))
+            return fail(ctx, "a value of row %lld is too large for fixed-point text with %d decimals", (long long)r,
+                        decimals);
         rbase[r] = total;
         total += rlen[r];
     }
@@ -2322,12 +2333,12 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
     if (!out) return fail(ctx, "null output buffer");
     char* mapped = host_mapped(out);
     if (!mapped && ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 1)) return -1;
-    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nrows * 8, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_fmt_rows, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, ctx->stream, a, d_rbase,
+    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nrows * 8, hipMemcpyHostToDevice, fst));
+    hipLaunchKernelGGL(k_fmt_rows, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, fst, a, d_rbase,
                        mapped ? mapped : (char*)ctx->d_out);
     HIP_TRY(ctx, hipGetLastError());
-    if (!mapped) HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (!mapped) HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, fst));
+    HIP_TRY(ctx, hipStreamSynchronize(fst));
     return 0;
 }
 
@@ -2501,6 +2512,27 @@ int taxi2_format_summary(taxi2_ctx* ctx, const double* vals, int64_t nrows, int6
                          has_genera ? 1 : 0, has_species ? 1 : 0, labels, label_offs};
     return format_impl(ctx, 2, vals, nrows, ncols, nm, nullptr, nullptr, row_pre, row_offs, col_pre, col_offs,
                        decimals, missing, missing_len, out, cap, out_len, &sm);
+}
+
+int taxi2_format_rows_dev(taxi2_ctx* ctx, int mode, const double* d_vals, int64_t vstride, int64_t nrows,
+                          int64_t ncols, int nm, const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                          const int64_t* col_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                          uint8_t* out, int64_t cap, int64_t* out_len, void* stream) {
+    return format_impl(ctx, mode, d_vals, nrows, ncols, nm, nullptr, nullptr, row_pre, row_offs, col_pre, col_offs,
+                       decimals, missing, missing_len, out, cap, out_len, nullptr, true, vstride, (hipStream_t)stream);
+}
+
+int taxi2_format_summary_dev(taxi2_ctx* ctx, const double* d_vals, int64_t vstride, int64_t nrows, int64_t ncols,
+                             int nm, const uint8_t* row_pre, const int64_t* row_offs, const uint8_t* col_pre,
+                             const int64_t* col_offs, const uint8_t* row_suf, const int64_t* row_suf_offs,
+                             const uint8_t* col_suf, const int64_t* col_suf_offs, const int32_t* row_codes,
+                             const int32_t* col_codes, int has_genera, int has_species, const uint8_t* labels,
+                             const int64_t* label_offs, int decimals, const uint8_t* missing, int32_t missing_len,
+                             uint8_t* out, int64_t cap, int64_t* out_len, void* stream) {
+    const SummaryHost sm{row_suf, row_suf_offs, col_suf, col_suf_offs, row_codes, col_codes,
+                         has_genera ? 1 : 0, has_species ? 1 : 0, labels, label_offs};
+    return format_impl(ctx, 2, d_vals, nrows, ncols, nm, nullptr, nullptr, row_pre, row_offs, col_pre, col_offs,
+                       decimals, missing, missing_len, out, cap, out_len, &sm, true, vstride, (hipStream_t)stream);
 }
 
 int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nrows, int64_t ncols, int m,

@@ -111,6 +111,10 @@ struct FmtArgs {
     int has_g, has_s;
     const uint8_t* lab;
     const int64_t* lab_offs;  // [6]: no info, intra-species, inter-species, intra-genus, inter-genus
+    int64_t vstride;  // doubles between consecutive value slots (nm for a packed block; more when the
+                      // values are a column range of a wider device array)
+    double vlim;      // |value| bound of exact fixed-point text: a row holding a larger finite value
+                      // gets a length of 2^60 or more from k_fmt_row_len (the host then fails)
 };
 
 __device__ __forceinline__ bool fmt_defined(double v) { return __builtin_isfinite(v); }
@@ -146,17 +150,21 @@ __device__ __forceinline__ void fmt_token_at(const FmtArgs& a, int64_t r, int64_
 __device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, int64_t t, int64_t nt) {
     int64_t g, c;
     fmt_token_at(a, r, t, g, c);
-    const double* v = a.vals + g * a.nm;
+    const double* v = a.vals + g * a.vstride;
     int64_t len = 0;
     if (a.mode != 1) {
         len = (a.row_offs[r + 1] - a.row_offs[r]) + 1 + (a.col_offs[c + 1] - a.col_offs[c]) + 1;  // + '\n'
-        for (int m = 0; m < a.nm; ++m) len += 1 + (fmt_defined(v[m]) ? fmt_fixed(v[m], a.decimals, nullptr) : a.missing_len);
+        for (int m = 0; m < a.nm; ++m) {
+            len += 1 + (fmt_defined(v[m]) ? fmt_fixed(v[m], a.decimals, nullptr) : a.missing_len);
+            if (fmt_defined(v[m]) && !(__builtin_fabs(v[m]) < a.vlim)) len += (int64_t)1 << 60;
+        }
         if (a.mode == 2)
             len += fmt_span(a.rsuf_offs, 2 * r) + fmt_span(a.csuf_offs, 2 * c) + fmt_span(a.rsuf_offs, 2 * r + 1) +
                    fmt_span(a.csuf_offs, 2 * c + 1) + 1 + fmt_span(a.lab_offs, fmt_comparison(a, r, c));
     } else {
         if (t == 0) len += a.row_offs[r + 1] - a.row_offs[r];
         len += 1 + (fmt_defined(v[0]) ? fmt_fixed(v[0], a.decimals, nullptr) : a.missing_len);
+        if (fmt_defined(v[0]) && !(__builtin_fabs(v[0]) < a.vlim)) len += (int64_t)1 << 60;
         if (t == nt - 1) len += 1;
     }
     return len;
@@ -165,7 +173,7 @@ __device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, in
 __device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int64_t t, int64_t nt, char* o) {
     int64_t g, c;
     fmt_token_at(a, r, t, g, c);
-    const double* v = a.vals + g * a.nm;
+    const double* v = a.vals + g * a.vstride;
     auto put = [&](const uint8_t* s, int64_t n) {
         for (int64_t k = 0; k < n; ++k) *o++ = (char)s[k];
     };
@@ -357,28 +365,35 @@ k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restri
                 Y = a.sy + k * a.cap + end - L;
             }
             const int h = sep + lx + 3 + ly + 1;  // header with its separator
-            for (int64_t t = lane; t < plen; t += 64) {
-                char ch;
+            const int L1 = L + 1;
+            // byte t of the pair's text: the header, then three lines of L + 1 bytes (no division)
+            auto byte_at = [&](int t) -> uint32_t {
                 if (t < h) {
-                    const int u = (int)t - sep;
-                    ch = u < 0 ? '\n' : u < lx ? (char)idx[u] : u < lx + 3 ? " / "[u - lx] : u < lx + 3 + ly ? (char)idy[u - lx - 3] : '\n';
-                } else {
-                    const int64_t v = t - h;
-                    const int line = (int)(v / (L + 1));
-                    const int col = (int)(v - (int64_t)line * (L + 1));
-                    if (col == L) {
-                        ch = '\n';
-                    } else if (line == 0) {
-                        ch = (char)X[col];
-                    } else if (line == 2) {
-                        ch = (char)Y[col];
-                    } else {
-                        const uint8_t p = X[col], q2 = Y[col];
-                        ch = (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
-                    }
+                    const int u = t - sep;
+                    return u < 0 ? '\n' : u < lx ? idx[u] : u < lx + 3 ? (uint32_t)" / "[u - lx] : u < lx + 3 + ly ? idy[u - lx - 3] : '\n';
                 }
-                o[t] = ch;
+                int v = t - h;
+                const int line = v < L1 ? 0 : v < 2 * L1 ? 1 : 2;
+                v -= line * L1;
+                if (v == L) return '\n';
+                if (line == 0) return X[v];
+                if (line == 2) return Y[v];
+                const uint32_t p = X[v], q2 = Y[v];
+                return (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
+            };
+            // 4-byte stores from the first 4-aligned byte of the pair's text (256 bytes per wave store:
+            // the text goes straight to pinned host memory, where wide writes count), bytes at both ends
+            const int pl = (int)plen;
+            const int a0 = min(pl, (int)((4u - (uint32_t)((uintptr_t)o & 3u)) & 3u));
+            const int nw = (pl - a0) >> 2;
+            if (lane < a0) o[lane] = (char)byte_at(lane);
+            for (int wi = lane; wi < nw; wi += 64) {
+                const int t = a0 + 4 * wi;
+                const uint32_t v = byte_at(t) | byte_at(t + 1) << 8 | byte_at(t + 2) << 16 | byte_at(t + 3) << 24;
+                *(uint32_t*)__builtin_assume_aligned(o + t, 4) = v;
             }
+            const int tb = a0 + 4 * nw;
+            if (tb + lane < pl) o[tb + lane] = (char)byte_at(tb + lane);
         }
         base += scan[FMT_BLOCK - 1];
         __syncthreads();

@@ -44,17 +44,33 @@ __host__ __device__ inline int pow2_at_least(int v) {
     return p;
 }
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) / 16 * 16; }
-// LDS layout for streams of at most nmax bytes: [window nmax + 274][key region: npmax x u32][Trees],
-// npmax = nmax - 2 inserted positions at most.  The key region holds the (hash << 16 | position)
-// sort keys; after the sort it is reused as the sorted positions (u16, first half) and each
-// position's sorted index (u16, second half).  The sort network never moves a key past npos (below),
-// so the region is sized by the positions, not by the next power of two (2 050-byte streams, e.g.
-// two 1 025-column aligned strings, would otherwise need a 4 096-key region).
+// LDS layout for streams of at most nmax bytes: [window nmax + 274][key region][tallies], and the
+// Trees overlaid on the key region.  The key region holds the (hash << 16 | position) sort keys
+// (npmax = nmax - 2 inserted positions at most); after the sort it is reused as the sorted positions
+// (u16, first half) and each position's sorted index (u16, second half).  The sort network never
+// moves a key past npos (below), so the region is sized by the positions, not by the next power of
+// two (2 050-byte streams, e.g. two 1 025-column aligned strings, would otherwise need a 4 096-key
+// region).  The parse only counts symbols (the tallies: lfc[0..286) and dfc[0..30) as 158 u16
+// pairs); the trees are built at a flush, and a stream shorter than LIT_BUFSIZE - 1 symbols
+// flushes only at its end, after its last chain walk -- so the Trees (4.5 kB) live in the key
+// region and a wave needs ~5.4 B per byte instead of ~7.4 (13 waves per CU instead of 10 at 2 kB).
+// Longer streams (nmax >= LIT_BUFSIZE - 1) may flush mid-stream and keep the Trees apart.
+constexpr int TAL_L = zl::L_CODES / 2, TAL_W = zl::L_CODES / 2 + zl::D_CODES / 2;
 __host__ __device__ inline int npos_max(int nmax) { return nmax > 4 ? nmax - 2 : 2; }
+__host__ __device__ inline bool trees_overlaid(int nmax) { return nmax < zl::LIT_BUFSIZE - 1; }
 __host__ __device__ inline size_t off_keys(int nmax) { return al16((size_t)nmax + zl::MAX_MATCH + 16); }
 __host__ __device__ inline size_t off_idx(int nmax) { return off_keys(nmax) + (size_t)npos_max(nmax) * 2; }
-__host__ __device__ inline size_t off_trees(int nmax) { return al16(off_keys(nmax) + (size_t)npos_max(nmax) * 4); }
-__host__ __device__ inline size_t lds_bytes(int nmax) { return al16(off_trees(nmax) + sizeof(zl::Trees)); }
+__host__ __device__ inline size_t key_bytes(int nmax) {
+    const size_t k = (size_t)npos_max(nmax) * 4;
+    return al16(trees_overlaid(nmax) && k < sizeof(zl::Trees) ? sizeof(zl::Trees) : k);
+}
+__host__ __device__ inline size_t off_tal(int nmax) { return off_keys(nmax) + key_bytes(nmax); }
+__host__ __device__ inline size_t off_trees(int nmax) {
+    return trees_overlaid(nmax) ? off_keys(nmax) : off_tal(nmax) + al16(TAL_W * 4);
+}
+__host__ __device__ inline size_t lds_bytes(int nmax) {
+    return off_tal(nmax) + al16(TAL_W * 4) + (trees_overlaid(nmax) ? 0 : al16(sizeof(zl::Trees)));
+}
 
 __device__ __forceinline__ uint32_t hash3(const uint8_t* w, int p) {
     return (((uint32_t)w[p] << 10) ^ ((uint32_t)w[p + 1] << 5) ^ (uint32_t)w[p + 2]) & (uint32_t)zl::HASH_MASK;
@@ -155,6 +171,11 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
     uint16_t* spos = reinterpret_cast<uint16_t*>(lds + off_keys(nmax));  // after the sort
     uint16_t* idx_of = reinterpret_cast<uint16_t*>(lds + off_idx(nmax));
     Trees& t = *reinterpret_cast<Trees*>(lds + off_trees(nmax));
+    uint32_t* tal = reinterpret_cast<uint32_t*>(lds + off_tal(nmax));  // the parse's symbol counts
+    // empty statistics, END_BLOCK counted once (init_block's tallies)
+    auto tal_reset = [&]() {
+        for (int w = lane; w < TAL_W; w += 64) tal[w] = w == END_BLOCK / 2 ? 1u : 0u;
+    };
     ZLW_T(tw0);
     for (int i = lane; i < n + MAX_MATCH + 12; i += 64) {
         uint8_t c = 0;
@@ -212,7 +233,7 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
     }
     // the second half of the region is free now: sorted index of every position
     for (int i = lane; i < npos; i += 64) idx_of[spos[i]] = (uint16_t)i;
-    if (lane == 0) init_block(t);
+    tal_reset();
     __syncthreads();
     ZLW_T(tw2);
     ZLW_ADD(1, tw2 - tw1);
@@ -222,15 +243,24 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
     int strstart = 0, lookahead = n;
     int match_length = MIN_MATCH - 1, prev_length = 0, match_start = 0, prev_match = 0;
     bool match_available = false;
-    auto flush = [&](bool last) {  // FLUSH_BLOCK_ONLY, lane 0; bits broadcast
+    auto flush = [&](bool last) {  // FLUSH_BLOCK_ONLY: the tallies into the trees, lane 0 builds them
+        __syncthreads();
+        uint32_t* lw = reinterpret_cast<uint32_t*>(t.lfc);
+        uint32_t* dw = reinterpret_cast<uint32_t*>(t.dfc);
+        for (int w = lane; w < TAL_W; w += 64) {
+            if (w < TAL_L) lw[w] = tal[w];
+            else dw[w - TAL_L] = tal[w];
+        }
+        if (lane < BL_CODES) t.bfc[lane] = 0;
         __syncthreads();
         if (lane == 0) {
+            t.opt_len = t.static_len = 0;
             flush_block_inl(t, strstart - block_start, last, bits);
-            init_block(t);
         }
         bits = __shfl(bits, 0);
         block_start = strstart;
         last_lit = 0;
+        tal_reset();
         __syncthreads();
     };
     // The parse's per-position LDS reads, 64 positions at a time into lane registers: lane l holds
@@ -258,8 +288,8 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
         pbyte = (p >= 1 && p <= nn) ? win[p - 1] : 0u;
     };
     // tallies: no-return LDS atomics on the u16 frequency pairs (lane 0), nothing waits on them
-    auto tally = [&](uint16_t* f, int c) {
-        if (lane == 0) atomicAdd(reinterpret_cast<uint32_t*>(f + (c & ~1)), 1u << (16 * (c & 1)));
+    auto tally = [&](int word0, int c) {
+        if (lane == 0) atomicAdd(tal + word0 + (c >> 1), 1u << (16 * (c & 1)));
     };
     // the fork (c_a): the state at the first step with strstart + MIN_LOOKAHEAD > na
     const bool fork = c_a != nullptr && nb > 0;
@@ -268,11 +298,7 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
     int64_t f_bits = 0;
     int f_block_start = 0, f_last_lit = 0, f_strstart = 0, f_match_length = MIN_MATCH - 1, f_match_start = 0;
     bool f_match_available = false;
-    uint32_t f_tal[3] = {0u, 0u, 0u};  // lfc[0..286) + dfc[0..30) as 158 u16 pairs, three per lane
-    constexpr int TAL_L = L_CODES / 2, TAL_W = L_CODES / 2 + D_CODES / 2;
-    auto tal_word = [&](int w) -> uint32_t* {
-        return w < TAL_L ? reinterpret_cast<uint32_t*>(t.lfc) + w : reinterpret_cast<uint32_t*>(t.dfc) + (w - TAL_L);
-    };
+    uint32_t f_tal[3] = {0u, 0u, 0u};  // the tallies (158 u16 pairs), three words per lane
     auto parse = [&]() {
         while (lookahead != 0) {
             if (!snapped && strstart > fork_at) {  // a alone parses the same up to here: keep the state
@@ -281,7 +307,7 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
                     const int w = lane + 64 * q;
-                    f_tal[q] = w < TAL_W ? *tal_word(w) : 0u;
+                    f_tal[q] = w < TAL_W ? tal[w] : 0u;
                 }
                 f_bits = bits;
                 f_block_start = block_start;
@@ -310,8 +336,8 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
                     match_length = MIN_MATCH - 1;
             }
             if (prev_length >= MIN_MATCH && match_length <= prev_length) {
-                tally(t.lfc, length_code(prev_length - MIN_MATCH) + LITERALS + 1);  // _tr_tally_dist
-                tally(t.dfc, dist_code(strstart - 1 - prev_match - 1));
+                tally(0, length_code(prev_length - MIN_MATCH) + LITERALS + 1);  // _tr_tally_dist
+                tally(TAL_L, dist_code(strstart - 1 - prev_match - 1));
                 const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
                 lookahead -= prev_length - 1;
                 strstart += prev_length - 2;  // the match's other positions (inserted by the sort)
@@ -320,7 +346,7 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
                 strstart++;
                 if (bflush) flush(false);
             } else if (match_available) {
-                tally(t.lfc, (int)__builtin_amdgcn_readlane(pbyte, sl));
+                tally(0, (int)__builtin_amdgcn_readlane(pbyte, sl));
                 const bool bflush = ++last_lit == LIT_BUFSIZE - 1;
                 if (bflush) flush(false);
                 strstart++;
@@ -331,44 +357,67 @@ __device__ inline int compressed_len_wave2(const uint8_t* a, int na, const uint8
                 lookahead--;
             }
         }
-        if (match_available) tally(t.lfc, win[strstart - 1]);
+        if (match_available) tally(0, win[strstart - 1]);  // the stream's end: the caller flushes
+    };
+    ZLW_T(tw3);
+    parse();  // a + b, up to its final flush
+    ZLW_T(tw4);
+    ZLW_ADD(2, tw4 - tw3);
+    auto finish = [&]() {  // the final flush: the stream's length in bytes (header, blocks, adler32)
         flush(true);
         return 2 + (int)(bits >> 3) + 4;
     };
-    ZLW_T(tw3);
-    const int c_ab = parse();
-    ZLW_T(tw4);
-    ZLW_ADD(2, tw4 - tw3);
-    if (fork) {  // a alone from the snapshot: the window past na as the one-stream form has it (zeros)
-        if (!snapped) {  // (a + b ended before the fork point: a is too short to share anything)
-            f_strstart = 0;
-            f_match_length = MIN_MATCH - 1;
-        }
-        for (int i = na + lane; i < n + MAX_MATCH + 12; i += 64) win[i] = 0;
-        __syncthreads();
-        if (lane == 0) init_block(t);
-        __syncthreads();
-        if (snapped) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int w = lane + 64 * q;
-                if (w < TAL_W) *tal_word(w) = f_tal[q];
-            }
-        }
-        __syncthreads();
-        bits = snapped ? f_bits : 0;
-        block_start = snapped ? f_block_start : 0;
-        last_lit = snapped ? f_last_lit : 0;
-        strstart = f_strstart;
-        lookahead = na - strstart;
-        match_length = f_match_length;
-        match_start = snapped ? f_match_start : 0;
-        match_available = snapped && f_match_available;
-        nn = na;
-        pb = -64;  // the prefetched literals past na changed
-        *c_a = parse();
+    if (!fork) {
+        const int c_ab = finish();
+        if (c_a) *c_a = c_ab;  // nb == 0: a + b is a
+        return c_ab;
     }
-    return c_ab;
+    // a + b's end state (its last block's tallies, bit count, block start) waits in registers while a
+    // alone resumes from the snapshot: a's final flush builds its trees over the key region, which
+    // a's parse still needs until then
+    uint32_t g_tal[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int w = lane + 64 * q;
+        g_tal[q] = w < TAL_W ? tal[w] : 0u;
+    }
+    const int64_t g_bits = bits;
+    const int g_block_start = block_start, g_strstart = strstart;
+    // a alone from the snapshot: the window past na as the one-stream form has it (zeros)
+    if (!snapped) {  // (a + b ended before the fork point: a is too short to share anything)
+        f_strstart = 0;
+        f_match_length = MIN_MATCH - 1;
+    }
+    for (int i = na + lane; i < n + MAX_MATCH + 12; i += 64) win[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int w = lane + 64 * q;
+        if (w < TAL_W) tal[w] = snapped ? f_tal[q] : (w == END_BLOCK / 2 ? 1u : 0u);
+    }
+    __syncthreads();
+    bits = snapped ? f_bits : 0;
+    block_start = snapped ? f_block_start : 0;
+    last_lit = snapped ? f_last_lit : 0;
+    strstart = f_strstart;
+    lookahead = na - strstart;
+    match_length = f_match_length;
+    match_start = snapped ? f_match_start : 0;
+    match_available = snapped && f_match_available;
+    nn = na;
+    pb = -64;  // the prefetched literals past na changed
+    parse();
+    *c_a = finish();
+    // a + b's final flush
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int w = lane + 64 * q;
+        if (w < TAL_W) tal[w] = g_tal[q];
+    }
+    bits = g_bits;
+    block_start = g_block_start;
+    strstart = g_strstart;
+    return finish();
 }
 
 // len(zlib.compress(upper(a) + upper(b))); n = na + nb <= nmax (the caller's LDS layout).

@@ -302,9 +302,9 @@ class VersusAll:
         in row blocks (taxi2_tri_strings_dev: the walkers walk both orientations, as the metric
         kernel does), the (a, b) strings formatted with row a's block, the (b, a) strings compacted
         and kept in HBM until row b's block is written (the text kernel reads each pair's strings
-        through a pointer).  One stream, the text after each block's alignment: a two-stream
-        pipeline (block b aligning while block b - 1's text and D2H ran) measured slower on one
-        box (10.85 s vs 10.0 s at N = 5 000, profiles/r3/task_pipeline_ab/) and is gone.  False
+        through a pointer).  Two streams: block b aligns while block b - 1's compaction, text (the
+        kernel writes it straight into pinned host memory) and complete rows run on the other; the
+        linear / matricial / summary writers take each block's rows in a worker thread.  False
         (nothing written) when TAXI2_PAIRS_RECT is set or the packed aligner does not cover the
         shape -- then _rows_with_pairs aligns every ordered pair once instead; when the kept strings
         outgrow params.engine.keep_bytes, the remaining rows switch to it."""
@@ -339,13 +339,27 @@ class VersusAll:
         if n * n * Mc * 8 <= DEVICE_D_BYTES:
             with torch.cuda.stream(stream):  # filled on `stream`, ahead of the scatters queued there
                 Dd = torch.full((n, n, Mc), float("nan"), dtype=torch.float64, device=dev)
+        # the row blocks: rows [x0, x1) hold about `target` triangle pairs, at most 2 * target ordered
+        # pairs of text.  Known up front, so that every per-block buffer is allocated once at its
+        # largest size: an allocation inside the loop (a pinned buffer, a device segment of the
+        # caching allocator) can synchronise the device and serialise the two streams
+        blocks = []
+        x0 = 0
+        while x0 < n:
+            x1, cnt = x0, 0
+            while x1 < n and (x1 == x0 or (cnt + (n - 1 - x1) <= target and (x1 + 1 - x0) * n <= 2 * target)):
+                cnt += n - 1 - x1
+                x1 += 1
+            blocks.append((x0, x1, cnt))
+            x0 = x1
+        rows_max = max(b[1] - b[0] for b in blocks)
         stage = [None, None, None]  # pinned buffer, its event, the rows (x0, x1) it holds
+        if Dd is not None:
+            stage[0] = torch.empty((rows_max, n, Mc), dtype=torch.float64, pin_memory=True)
 
         def rows_out(x0: int, x1: int) -> None:  # queue rows [x0, x1) of Dd to the staging buffer
             if Dd is None or x1 <= x0:
                 return
-            if stage[0] is None or stage[0].shape[0] < x1 - x0:
-                stage[0] = torch.empty((x1 - x0, n, Mc), dtype=torch.float64, pin_memory=True)
             with torch.cuda.stream(tstream):  # after the block's event (post() waits on it)
                 stage[0][: x1 - x0].copy_(Dd[x0:x1], non_blocking=True)
                 stage[1] = torch.cuda.Event()
@@ -388,8 +402,24 @@ class VersusAll:
             kpy = torch.zeros(npairs, dtype=torch.int64, device=dev)
             klen = torch.zeros(npairs, dtype=torch.int32, device=dev)
         tstream.wait_stream(stream)  # the tables above
-        kept = []
+        kept = []  # the arena's chunks: every block's kept strings are carved from the newest one
         kept_b = [0]
+        arena = [None, 0]  # current chunk, its next free byte
+
+        def carve(nbytes: int, cnt: int, k_end: int):
+            """nbytes of kept-string storage (stream-ordered on tstream).  A new chunk holds what the
+            rest of the triangle will keep at this block's bytes per pair (one or two allocations per
+            task instead of one per block), bounded by the keep budget."""
+            if arena[0] is None or arena[1] + nbytes > arena[0].numel():
+                left = npairs - k_end
+                est = int(1.05 * nbytes / max(1, cnt) * left) + nbytes
+                size = max(nbytes, min(est, max(nbytes, keep_limit - kept_b[0])), 1)
+                arena[0] = torch.empty(size, dtype=torch.uint8, device=dev)
+                arena[1] = 0
+                kept.append(arena[0])
+            t = arena[0][arena[1]:arena[1] + nbytes]
+            arena[1] += (nbytes + 255) // 256 * 256
+            return t
         # linear.tsv, the matricial files, summary.tsv and the subset statistics per row block, while
         # the next blocks align and their aligned_pairs.txt text is written: the writers' own engine
         # context (formatting on its own stream, its own lock) in a worker thread, fed each block's
@@ -406,6 +436,15 @@ class VersusAll:
             sink.diag = self._diag_info(seqs, eng, st, True, scores, [str(m) for m in self.params.distances.metrics])
             writers = ThreadPoolExecutor(1, thread_name_prefix="taxi2-writers")
             scale = 100.0 if self.params.format.percentage_multiply else 1.0
+            # three block buffers: a writer reads block k's while block k + 1 is being written and
+            # block k + 2's is filled (at most two blocks queued for the thread)
+            with torch.cuda.stream(tstream):
+                Abuf = [torch.empty((rows_max, n, Mc), dtype=torch.float64, device=dev) for _ in range(3)]
+            nblk = [0]
+
+        # CUs' worth of workgroup slots the fill leaves free, so that the previous block's text kernel
+        # (bound by the host link it writes through) runs beside it instead of after it
+        reserve = int(os.environ.get("TAXI2_TEXT_RESERVE_CUS", "0"))
 
         def launch(x0: int, x1: int, cnt: int):
             """Block rows [x0, x1) (cnt triangle pairs) on `stream`: the fill (metrics + both
@@ -417,7 +456,7 @@ class VersusAll:
                 sy = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
                 sl = torch.empty((cnt, 2), dtype=torch.int32, device=dev)
                 eng.tri_strings_dev(st, k0, cnt, clabels, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
-                                    sl.data_ptr(), scores, stream.cuda_stream)
+                                    sl.data_ptr(), scores, stream.cuda_stream, reserve_cus=reserve)
                 # pair (a, b) of the block: a in [x0, x1), b > a
                 rows = torch.arange(x0, x1, device=dev)
                 per = n - 1 - rows
@@ -453,14 +492,13 @@ class VersusAll:
                     L1 = sl[:, 1].to(torch.int64)
                     off = torch.cumsum(L1, 0) - L1
                     tot = int(L1.sum().item())  # waits for tstream only (this block's fill is done)
-                    kx = torch.empty(max(1, tot), dtype=torch.uint8, device=dev)
-                    ky = torch.empty(max(1, tot), dtype=torch.uint8, device=dev)
+                    kxy = carve(2 * max(1, tot), cnt, k0 + cnt)
+                    kx, ky = kxy[:max(1, tot)], kxy[max(1, tot):]
                     eng.pack_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 1, end.data_ptr(),
                                        off.data_ptr(), cnt, kx.data_ptr(), ky.data_ptr(), tstream.cuda_stream)
                     kpx[k0:k0 + cnt] = kx.data_ptr() + off
                     kpy[k0:k0 + cnt] = ky.data_ptr() + off
                     klen[k0:k0 + cnt] = sl[:, 1]
-                    kept.append((kx, ky))
                     kept_b[0] += 2 * tot
                 # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
                 # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
@@ -488,28 +526,28 @@ class VersusAll:
                 rows_in()  # the previous block's staged rows into D
                 rows_out(x0, x1)
                 if sink is not None:  # rows [x0, x1) are complete: adjusted on the GPU, text in the thread
-                    A = Dd[x0:x1].clone()
-                    if scale != 1.0:
-                        A *= scale
-                    sink.diagonal(x0, x1, A, scale)
-                    sink.aggregate(x0, x1, A)
-                    Ah = A.cpu().numpy()
                     while len(futs) >= 2:  # at most two blocks queued for the thread
                         futs.pop(0).result()
-                    futs.append(writers.submit(sink.write_text_host, x0, x1, Ah))
+                    A = Abuf[nblk[0] % 3][: x1 - x0]
+                    nblk[0] += 1
+                    if scale != 1.0:
+                        torch.mul(Dd[x0:x1], scale, out=A)
+                    else:
+                        A.copy_(Dd[x0:x1])
+                    sink.diagonal(x0, x1, A, scale)
+                    sink.aggregate(x0, x1, A)
+                    ready = torch.cuda.Event()
+                    ready.record(tstream)
+                    # the writers format the block where it is (taxi2_format_rows_dev): no D2H of the
+                    # values and no H2D of them again per file
+                    futs.append(writers.submit(sink.write_text_dev, x0, x1, A, ready))
             if isinstance(self.timings, dict):
                 self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
             report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
                    total)
 
         pending = None
-        x0 = 0
-        while x0 < n:
-            # rows [x0, x1): about `target` triangle pairs, at most 2 * target ordered pairs of text
-            x1, cnt = x0, 0
-            while x1 < n and (x1 == x0 or (cnt + (n - 1 - x1) <= target and (x1 + 1 - x0) * n <= 2 * target)):
-                cnt += n - 1 - x1
-                x1 += 1
+        for x0, x1, cnt in blocks:
             try:
                 blk = launch(x0, x1, cnt) if cnt else dict(x0=x0, x1=x1, k0=0, cnt=0)
             except NativeError as e:
@@ -1388,6 +1426,43 @@ class _BlockWriters:
         if not self.has_text:  # reductions only: the block never leaves HBM
             return
         self.write_text_host(x0, x1, D.cpu().numpy(), pairs_text)
+
+    def write_text_dev(self, x0: int, x1: int, A, ready) -> None:
+        """write_text from the block's adjusted values in HBM (a writer thread's entry): once `ready`
+        (an event after their producer) has fired, the device formatters read them in place --
+        linear rows, one matricial file per metric (a strided column of the block), summary lines.
+        Blocks the formatters cannot take (duplicate ids, aligned pairs here, values too large for
+        exact fixed-point text) go through write_text_host."""
+        torch = self.torch
+        ready.synchronize()
+        dec = self.dec
+        ok = dec is not None and not self.dupids and self.pairs_fh is None
+        if ok and A.numel():
+            if getattr(self, "_wstream", None) is None:  # (not the legacy default stream)
+                self._wstream = torch.cuda.Stream(A.device)
+            with torch.cuda.stream(self._wstream):
+                big = float(torch.where(torch.isfinite(A), A.abs(), torch.zeros_like(A)).max())
+            ok = big * 10.0 ** dec < 2.0 ** 62
+        if not ok:
+            self.write_text_host(x0, x1, A.cpu().numpy())
+            return
+        ids = self.ids
+        if self.lin is not None:
+            write_rows_gpu(self.lin, self.eng, A, self.pre[x0:x1], self.pre, dec, self.missing)
+        if self.mats is not None:
+            for m, fh in enumerate(self.mats):
+                write_rows_gpu(fh, self.eng, A[:, :, m], ids[x0:x1], None, dec, self.missing)
+        if self.summ is None:
+            return
+        from .subsets import SUMMARY_CHUNK_VALUES
+
+        step = max(1, SUMMARY_CHUNK_VALUES // max(1, A.shape[1] * A.shape[2]))
+        for r0 in range(0, x1 - x0, step):
+            r1 = min(x1 - x0, r0 + step)
+            self.summ.write(self.eng.format_summary(
+                A[r0:r1], ids[x0 + r0 : x0 + r1], ids, self.suf[2 * (x0 + r0) : 2 * (x0 + r1)], self.suf,
+                self.codes[x0 + r0 : x0 + r1], self.codes, has_genera=bool(self.genera),
+                has_species=bool(self.species), decimals=dec, missing=self.missing, view=True))
 
     def write_text_host(self, x0: int, x1: int, A: np.ndarray, pairs_text: bytes | None = None) -> None:
         """write_text on the block's values already on the host (a writer thread's entry)."""

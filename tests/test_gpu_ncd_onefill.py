@@ -242,6 +242,8 @@ def test_ncd_slots_fused_lengths_edges(engine):
     base = dna(800)
     xs += [base, base[:600] + dna(200)]
     ys += [base[300:], base[100:]]
+    xs += ["", ""]  # both strings empty (an empty sequence against itself): C(x) = C(x + y)
+    ys += ["", ""]
     n = len(xs)
     # two orientations per pair: the second one is (x, y) itself (same alignment) for even k, a
     # different pair of strings for odd k -- the skipped and the computed singles

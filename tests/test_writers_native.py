@@ -95,3 +95,39 @@ def test_format_rows_gpu(engine, decimals):
     ids = [f"id{i}" for i in range(nrows)]
     expm = "".join(ids[i] + "".join("\t" + txt(M[i, j]) for j in range(ncols)) + "\n" for i in range(nrows))
     assert engine.format_rows(M, ids, None, decimals=decimals, missing="NA").decode() == expm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decimals", [0, 4])
+def test_format_rows_dev_values(engine, decimals):
+    """taxi2_format_rows_dev / taxi2_format_summary_dev (values read in HBM: a block, one metric's
+    strided column of it, a row slice) == the host-value formatters byte for byte; a value too large
+    for exact fixed-point text fails the call instead of printing a wrong number."""
+    import torch
+
+    from taxi2_amd._native import NativeError
+
+    rng = np.random.default_rng(11 + decimals)
+    vals = np.array([v for v in _values(decimals, 3000) if v == v and abs(v) * 10.0 ** decimals < 2.0 ** 62])
+    nrows, ncols, nm = 9, 37, 4
+    V = rng.choice(vals, size=(nrows, ncols, nm))
+    V[0, 0, 0], V[1, 2, 1], V[3, 4, 3], V[2, 2, 2] = np.nan, np.inf, -np.inf, -0.0
+    rows = [f"q{i}\tv{i}" for i in range(nrows)]
+    cols = [f"r{j}\tw{j}" for j in range(ncols)]
+    Vd = torch.as_tensor(V, device="cuda")
+    assert engine.format_rows(Vd, rows, cols, decimals=decimals) == engine.format_rows(V, rows, cols, decimals=decimals)
+    for m in range(nm):  # the matricial files: one metric of the block, stride nm
+        assert (engine.format_rows(Vd[:, :, m], rows, None, decimals=decimals)
+                == engine.format_rows(np.ascontiguousarray(V[:, :, m]), rows, None, decimals=decimals))
+    sub = engine.format_rows(Vd[3:7], rows[3:7], cols, decimals=decimals, view=True)
+    assert bytes(sub) == engine.format_rows(V[3:7], rows[3:7], cols, decimals=decimals)
+    suf_r = [s for i in range(nrows) for s in (f"\tx{i}", f"\tg{i % 2}\ts{i % 3}")]
+    suf_c = [s for j in range(ncols) for s in ("", f"\tg{j % 2}\ts{j % 3}")]
+    rc = np.array([[i % 2, i % 3] for i in range(nrows)], dtype=np.int32)
+    cc = np.array([[j % 2, j % 3] for j in range(ncols)], dtype=np.int32)
+    kw = dict(has_genera=True, has_species=True, decimals=decimals)
+    assert (engine.format_summary(Vd, rows, cols, suf_r, suf_c, rc, cc, **kw)
+            == engine.format_summary(V, rows, cols, suf_r, suf_c, rc, cc, **kw))
+    Vd[5, 6, 1] = 2.0 ** 63
+    with pytest.raises(NativeError, match="too large"):
+        engine.format_rows(Vd, rows, cols, decimals=decimals)

@@ -21,6 +21,8 @@
 #   d2h              tools/d2h_probe (device -> host text bandwidth: memcpy, 4 streams, kernel stores)
 #   tool:SCRIPT      python tools/SCRIPT.py (bench tools), e.g. tool:bench_long
 #   sec:LEG          one bench_secondary.py leg alone (task, config5, config4, allmetrics)
+#   with:V=X,...:STEP  any step with those environment settings (outputs under the step's own names)
+#   secenv:NAME:LEG:V=X,...  that leg with those environment settings -> secenv_NAME.json
 #   sectrace:LEG     rocprofv3 --kernel-trace --stats of that leg
 #   pmcsec:LEG:SET   one rocprofv3 --pmc pass (valu | lds | fetch | write) over that leg's kernels
 #                    matching PMC_SEC_RE (default k_prealigned|k_subset|k_rowmin)
@@ -116,6 +118,16 @@ run_step() {
         (cd "$R" && timeout -k 10 900 python3 -u "tools/${s#tool:}.py" > "$OUT/${s#tool:}.json" 2> "$OUT/${s#tool:}.err") ;;
     sec:*)
         (cd "$R" && timeout -k 10 600 python3 -u bench_secondary.py "${s#sec:}" > "$OUT/sec_${s#sec:}.json" 2> "$OUT/sec_${s#sec:}.err") ;;
+    with:*)  # with:V=X,...:STEP -- any other step with those environment settings
+        local rest=${s#with:}
+        local envs=${rest%%:*} inner=${rest#*:}
+        (for kv in $(echo "$envs" | tr ',' ' '); do export "$kv"; done; run_step "$inner") ;;
+    secenv:*)  # secenv:NAME:LEG:V=X,... -- one bench_secondary leg with those environment settings
+        local rest=${s#secenv:}
+        local name=${rest%%:*}; rest=${rest#*:}
+        local leg=${rest%%:*} envs=${rest#*:}
+        (cd "$R" && env $(echo "$envs" | tr ',' ' ') timeout -k 10 600 python3 -u bench_secondary.py "$leg" \
+            > "$OUT/secenv_$name.json" 2> "$OUT/secenv_$name.err") ;;
     sectrace:*)
         (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sectrace_${s#sectrace:}" -o run -- \
             python3 $R/bench_secondary.py "${s#sectrace:}" > "$OUT/sectrace_${s#sectrace:}.json" 2> "$OUT/sectrace_${s#sectrace:}.err") ;;
