@@ -251,7 +251,8 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
 /* Asynchronous form of taxi2_format_pairs_ptr_dev for pipelines: every input is a device array
  * (ids as concatenated bytes with offsets relative to those bytes), the text goes to the device
  * buffer d_text, and d_total[0] = its length, d_total[1] = 1 if it fit text_cap (else nothing is
- * written: call again with a larger buffer); d_scratch: 2 nrows int64 of device scratch.  Nothing
+ * written: call again with a larger buffer); d_scratch: 2 nrows ceil(ncols / 256) int64 of device
+ * scratch (per-chunk lengths and offsets, 256 columns a chunk).  Nothing
  * synchronises the host or the device: the caller copies d_text[0, d_total[0]) out when the stream
  * reaches it. */
 int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, const uint64_t* d_px,

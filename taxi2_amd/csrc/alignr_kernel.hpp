@@ -67,31 +67,21 @@ constexpr bool AR_SKIP = TAXI2_AR_SKIP != 0;
 #define TAXI2_AR_PREC 0
 #endif
 constexpr bool AR_PREC = TAXI2_AR_PREC != 0;
-// Two-word trace (AR_TR2): the fill stores each column pair's two raw 32-bit differences D = M - Ix and
-// E = M - Iy (both halves, 16 bits each) as they are, 8 bytes, instead of packing their four low
-// bytes into one word with a v_perm (a 4-cycle VOP3 per column pair, ~16 % of the cells' issue
-// cycles); the trace doubles, the walker loads 8 bytes per step.  Plain layout only (AR_TS = 0).
-#ifndef TAXI2_AR_TR2
-#define TAXI2_AR_TR2 0
-#endif
-constexpr bool AR_TR2 = TAXI2_AR_TR2 != 0;
-static_assert(!AR_TR2 || AR_TS == 0, "the two-word trace uses the plain layout");
-constexpr uint32_t AR_WB = AR_TR2 ? 8 : 4;  // trace bytes per column pair
 __host__ __device__ constexpr int ar_pw(int K) { return K % 4 == 0 ? 4 : 2; }
 // byte offset of (step, lane, column k) in a chain's trace buffer (NT lanes)
-// (AR_TS = 0: the plain [step][lane][AR_WB K bytes] layout, for comparison)
+// (AR_TS = 0: the plain [step][lane][4K bytes] layout, for comparison)
 template <int K, int NT>
 __device__ __forceinline__ uint32_t ar_trace_step_off(uint32_t step) {  // of (step, lane 0, column 0)
     constexpr uint32_t PW = ar_pw(K), PB = 4 * PW, NP = K / PW;
-    if constexpr (AR_TS == 0) return step * (NT * AR_WB * K);
+    if constexpr (AR_TS == 0) return step * (NT * 4 * K);
     else return (step / AR_TS) * (NP * NT * AR_TS * PB) + (step % AR_TS) * PB;
 }
-template <int K> constexpr uint32_t ar_lane_bytes() { return AR_TS == 0 ? AR_WB * K : AR_TS * 4 * ar_pw(K); }
-template <int K, int NT> constexpr uint32_t ar_piece_stride() { return AR_TS == 0 ? AR_WB * ar_pw(K) : NT * AR_TS * 4 * ar_pw(K); }
+template <int K> constexpr uint32_t ar_lane_bytes() { return AR_TS == 0 ? 4 * K : AR_TS * 4 * ar_pw(K); }
+template <int K, int NT> constexpr uint32_t ar_piece_stride() { return AR_TS == 0 ? 4 * ar_pw(K) : NT * AR_TS * 4 * ar_pw(K); }
 template <int K, int NT>
 __device__ __forceinline__ uint32_t ar_trace_off(uint32_t step, uint32_t lane, uint32_t k) {
     constexpr uint32_t PW = ar_pw(K);
-    return ar_trace_step_off<K, NT>(step) + lane * ar_lane_bytes<K>() + (k / PW) * ar_piece_stride<K, NT>() + (k % PW) * AR_WB;
+    return ar_trace_step_off<K, NT>(step) + lane * ar_lane_bytes<K>() + (k / PW) * ar_piece_stride<K, NT>() + (k % PW) * 4;
 }
 // trace buffer rows for a chain of `rows` rows: steps up to rows + 62, rounded up to whole blocks
 __host__ __device__ constexpr int ar_trace_rows(int rows) { return rows + 64 + AR_TS; }
@@ -386,19 +376,11 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     const uint32_t tl = (uint32_t)cj / K, k = (uint32_t)cj - tl * K;
                     const uint32_t toff = ar_trace_off<K, NT>((uint32_t)(r0 + ci) + (tl & 63u), tl, k);
                     const uint32_t xa_ = a2_load_byte(rs + ci), yb_ = a2_load_byte(cs + max(nj, 1) - 1);
-                    int d1v, d2v;
-                    if constexpr (AR_TR2) {  // D, E words: half h in bits 16 h.., the high half after the low one's borrow
-                        const uint64_t de = a2_load_trace64(trb + toff);
-                        const uint32_t nd = (uint32_t)de, ne = (uint32_t)(de >> 32);
-                        d1v = (int)(int8_t)(uint8_t)((nd >> (2 * bsh)) + (h ? ((nd >> 15) & 1u) : 0u));
-                        d2v = (int)(int8_t)(uint8_t)((ne >> (2 * bsh)) + (h ? ((ne >> 15) & 1u) : 0u));
-                    } else {
-                        const uint32_t nb = a2_load_trace32(trb + toff);
-                        d1v = (int)(int8_t)(uint8_t)((nb >> bsh) + (h ? ((nb >> 7) & 1u) : 0u));
-                        d2v = (int)(int8_t)(uint8_t)((nb >> (16 + bsh)) + (h ? ((nb >> 23) & 1u) : 0u));
-                    }
+                    const uint32_t nb = a2_load_trace32(trb + toff);
                     xa = ni >= 1 ? xa_ : 0u;
                     yb = nj >= 1 ? yb_ : 0u;
+                    const int d1v = (int)(int8_t)(uint8_t)((nb >> bsh) + (h ? ((nb >> 7) & 1u) : 0u));
+                    const int d2v = (int)(int8_t)(uint8_t)((nb >> (16 + bsh)) + (h ? ((nb >> 23) & 1u) : 0u));
                     const int co = j == nB_ ? co_e : co_i, oy = i == nA_ ? co_e : co_i;
                     const int vM = d1v + (isX ? co : 0);
                     const int vY = d1v - d2v + (isX ? co : isY ? -oy : 0);
@@ -661,10 +643,6 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 }
                 at_s2 F1 = as_s2(inF), Y = as_s2(inY);
                 uint32_t acc[K];
-                constexpr uint32_t PSTRIDE = ar_piece_stride<K, NT>();  // bytes between pieces
-                // uniform step offset (SGPR) + the lane's constant: one VALU add, saddr stores per piece
-                const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane(ar_trace_step_off<K, NT>((uint32_t)s)) +
-                                    (uint32_t)tq * ar_lane_bytes<K>();
                 // Best-open fill on open-shifted cells (alignt2_kernel.hpp cells, RAW): M = G(i-1, j-1) +
                 // (s - co_i), X = max(G_up, X_up), Y = max(G_left, Y_left), B = maximum3(M, X, Y), G = B + o_i.
                 // TR: also the trace words (D1 = M - Ix, D2 = M - Iy of both halves, one v_perm)
@@ -683,17 +661,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         if constexpr (TR) {
                             const uint32_t dD = as_u32(M) - as_u32(Xn);
                             const uint32_t dE = as_u32(M) - as_u32(Yn);
-                            if constexpr (AR_TR2) {  // two columns' (D, E) per 16-byte store, as they are made
-                                if (k & 1) {
-                                    if (in_band)
-                                        *(uint4*)((trb + (k / 2) * 16) + o0) = make_uint4(acc[k - 1], acc[k], dD, dE);
-                                } else {
-                                    acc[k] = dD;
-                                    acc[k + 1] = dE;
-                                }
-                            } else {
-                                acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
-                            }
+                            acc[k] = __builtin_amdgcn_perm(dE, dD, 0x06040200u);
                         }
                         const at_s2 Gn = padd32(as_s2(b3), orow);
                         stG[k] = as_u32(Gn);
@@ -707,7 +675,11 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 // branch is wave-uniform (the band ballot in an SGPR)
                 if (AR_SKIP && bmask == 0) cells(std::false_type{});
                 else cells(std::true_type{});
-                if (!AR_TR2 && in_band) {
+                if (in_band) {
+                    constexpr uint32_t PSTRIDE = ar_piece_stride<K, NT>();  // bytes between pieces
+                    // uniform step offset (SGPR) + the lane's constant: one VALU add, saddr stores per piece
+                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane(ar_trace_step_off<K, NT>((uint32_t)s)) +
+                                        (uint32_t)tq * ar_lane_bytes<K>();
                     if constexpr (K % 4 == 0) {
 #pragma unroll
                         for (int q = 0; q < K / 4; ++q)

@@ -182,8 +182,6 @@ typedef const __attribute__((address_space(1))) uint32_t a2_gword;
 __device__ __forceinline__ uint32_t a2_load_byte(const uint8_t* p) { return *(a2_gbyte*)p; }
 __device__ __forceinline__ uint32_t a2_load_trace(const uint8_t* p) { return *(const volatile a2_gbyte*)p; }
 __device__ __forceinline__ uint32_t a2_load_trace32(const uint8_t* p) { return *(const volatile a2_gword*)p; }
-typedef const __attribute__((address_space(1))) uint64_t a2_gdword;
-__device__ __forceinline__ uint64_t a2_load_trace64(const uint8_t* p) { return *(const volatile a2_gdword*)p; }
 
 // Raw-difference trace (default scores, the band pass).  Instead of forming sign digits per cell
 // (3 subtracts, 3 clamps and 3 multiply-adds per column pair: ~45 % of the fill's issue cycles),

@@ -779,7 +779,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // up to 120 GB of the 288 GB HBM, at most 45 % of the device's memory (TAXI2_AT_TRACE_GB overrides)
     double budget_gb = std::min(120.0, 0.45 * (double)ctx->total_mem / 1e9);
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
-    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * std::max(1, Y.max_len)) - 64, (int)AR_WB * v.K, v.W); };
+    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * std::max(1, Y.max_len)) - 64, 4 * v.K, v.W); };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
     chunk = (int)eff;
     const int cap_rows = (int)eff * std::max(1, Y.max_len);
@@ -2238,6 +2238,14 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
                 return fail(ctx, "value %g too large for fixed-point text with %d decimals", v0[k], decimals);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t fst = st_in ? st_in : ctx->stream;
+    // chunks of FMT_BLOCK tokens per row (format_kernels.hpp): nch per row, nrows * nch workgroups
+    int64_t max_nt = ncols;
+    if (ragged) {
+        max_nt = 0;
+        for (int64_t r = 0; r < nrows; ++r) max_nt = std::max(max_nt, rstart[r + 1] - rstart[r]);
+    }
+    const int64_t nch = std::max<int64_t>(1, (max_nt + FMT_BLOCK - 1) / FMT_BLOCK), nblk = nrows * nch;
+    if (nblk >= ((int64_t)1 << 31)) return fail(ctx, "text block too large (%lld chunks)", (long long)nblk);
     const int64_t rp = row_offs[nrows] - row_offs[0];
     const int64_t cp = mode != 1 ? col_offs[ncols] - col_offs[0] : 0;
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -2245,7 +2253,7 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
     const int64_t cs_b = sm ? sm->csuf_offs[2 * ncols] - sm->csuf_offs[0] : 0;
     const int64_t lab_b = sm ? sm->lab_offs[5] - sm->lab_offs[0] : 0;
     const size_t b_vals = dev_vals ? 0 : al(nv * 8), b_roffs = al((nrows + 1) * 8), b_coffs = al((ncols + 1) * 8),
-                 b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nrows * 8),
+                 b_rpre = al(rp + 1), b_cpre = al(cp + 1), b_miss = al(missing_len + 1), b_len = al(nblk * 8),
                  b_rst = ragged ? al((nrows + 1) * 8) : 0, b_cols = ragged ? al(ntok * 4) : 0,
                  b_rsuf = sm ? al(rs_b + 1) + al((2 * nrows + 1) * 8) + al(2 * nrows * 4) : 0,
                  b_csuf = sm ? al(cs_b + 1) + al((2 * ncols + 1) * 8) + al(2 * ncols * 4) : 0,
@@ -2315,26 +2323,26 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
     FmtArgs a{mode, d_vals, nrows, ncols, nm, decimals, d_rpre, d_roffs, d_cpre, d_coffs, d_miss, missing_len,
               d_rst, d_cols, d_rsuf, d_rsoffs, d_csuf, d_csoffs, d_rcode, d_ccode, sm ? sm->has_g : 0,
               sm ? sm->has_s : 0, d_lab, d_laboffs, vs, lim};
-    hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, fst, a, d_rlen);
+    hipLaunchKernelGGL(k_fmt_row_len, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, fst, a, (int)nch, d_rlen);
     HIP_TRY(ctx, hipGetLastError());
-    std::vector<int64_t> rlen(nrows), rbase(nrows);
-    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nrows * 8, hipMemcpyDeviceToHost, fst));
+    std::vector<int64_t> rlen(nblk), rbase(nblk);
+    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nblk * 8, hipMemcpyDeviceToHost, fst));
     HIP_TRY(ctx, hipStreamSynchronize(fst));
     int64_t total = 0;
-    for (int64_t r = 0; r < nrows; ++r) {
-        if (rlen[r] >= ((int64_t)1 << 60))
-            return fail(ctx, "a value of row %lld is too large for fixed-point text with %d decimals", (long long)r,
-                        decimals);
-        rbase[r] = total;
-        total += rlen[r];
+    for (int64_t b = 0; b < nblk; ++b) {
+        if (rlen[b] >= ((int64_t)1 << 60))
+            return fail(ctx, "a value of row %lld is too large for fixed-point text with %d decimals",
+                        (long long)(b / nch), decimals);
+        rbase[b] = total;
+        total += rlen[b];
     }
     *out_len = total;
     if (total > cap) return 1;  // caller retries with a buffer of *out_len bytes
     if (!out) return fail(ctx, "null output buffer");
     char* mapped = host_mapped(out);
     if (!mapped && ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 1)) return -1;
-    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nrows * 8, hipMemcpyHostToDevice, fst));
-    hipLaunchKernelGGL(k_fmt_rows, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, fst, a, d_rbase,
+    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nblk * 8, hipMemcpyHostToDevice, fst));
+    hipLaunchKernelGGL(k_fmt_rows, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, fst, a, (int)nch, d_rbase,
                        mapped ? mapped : (char*)ctx->d_out);
     HIP_TRY(ctx, hipGetLastError());
     if (!mapped) HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, fst));
@@ -2350,10 +2358,12 @@ int format_pairs_impl(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, PairFmtArgs 
                       const int64_t* row_offs, const uint8_t* col_ids, const int64_t* col_offs, uint8_t* out,
                       int64_t out_cap, int64_t* out_len, hipStream_t st) {
     const int64_t rb = row_offs[nrows] - row_offs[0], cb = col_offs[ncols] - col_offs[0];
+    const int64_t nch = (ncols + FMT_BLOCK - 1) / FMT_BLOCK, nblk = nrows * nch;  // FMT_BLOCK-column chunks
+    if (nblk >= ((int64_t)1 << 31)) return fail(ctx, "pair text block too large (%lld chunks)", (long long)nblk);
     auto al = [](size_t v) { return (v + 255) / 256 * 256; };
     const size_t o_ro = 0, o_co = o_ro + al((size_t)(nrows + 1) * 8), o_rid = o_co + al((size_t)(ncols + 1) * 8);
     const size_t o_cid = o_rid + al((size_t)rb + 1), o_len = o_cid + al((size_t)cb + 1);
-    const size_t o_base = o_len + al((size_t)nrows * 8), fixed = o_base + al((size_t)nrows * 8);
+    const size_t o_base = o_len + al((size_t)nblk * 8), fixed = o_base + al((size_t)nblk * 8);
     if (ensure(ctx, &ctx->d_fmt, &ctx->d_fmt_bytes, fixed)) return -1;
     char* b = (char*)ctx->d_fmt;
     std::vector<int64_t> ro(nrows + 1), co(ncols + 1);
@@ -2370,23 +2380,23 @@ int format_pairs_impl(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, PairFmtArgs 
     a.coffs = (const int64_t*)(b + o_co);
     int64_t* d_rlen = (int64_t*)(b + o_len);
     int64_t* d_rbase = (int64_t*)(b + o_base);
-    hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rlen);
+    hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, st, a, (int)nch, d_rlen);
     HIP_TRY(ctx, hipGetLastError());
-    std::vector<int64_t> rlen(nrows), rbase(nrows);
-    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nrows * 8, hipMemcpyDeviceToHost, st));
+    std::vector<int64_t> rlen(nblk), rbase(nblk);
+    HIP_TRY(ctx, hipMemcpyAsync(rlen.data(), d_rlen, nblk * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(ctx, hipStreamSynchronize(st));
     int64_t total = 0;
-    for (int64_t r = 0; r < nrows; ++r) {
-        rbase[r] = total;
-        total += rlen[r];
+    for (int64_t b = 0; b < nblk; ++b) {
+        rbase[b] = total;
+        total += rlen[b];
     }
     *out_len = total;
     if (total > out_cap) return 1;  // caller retries with a buffer of *out_len bytes
     if (!out) return fail(ctx, "null output buffer");
     char* mapped = host_mapped(out);
     if (!mapped && ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 1)) return -1;
-    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nrows * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rbase,
+    HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nblk * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, st, a, (int)nch, d_rbase,
                        mapped ? mapped : (char*)ctx->d_out);
     HIP_TRY(ctx, hipGetLastError());
     if (!mapped) HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, st));
@@ -2469,16 +2479,18 @@ int taxi2_format_pairs_ptr_async(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, c
     // regrown -- hipFree synchronises the whole device -- while another stream runs); ids and
     // offsets are device arrays the caller keeps: row offsets relative to d_row_ids, column
     // offsets to d_col_ids
+    const int64_t nch = (ncols + FMT_BLOCK - 1) / FMT_BLOCK, nblk = nrows * nch;  // FMT_BLOCK-column chunks
+    if (nblk >= ((int64_t)1 << 31)) return fail(ctx, "pair text block too large (%lld chunks)", (long long)nblk);
     int64_t* d_rlen = d_scratch;
-    int64_t* d_rbase = d_rlen + nrows;
+    int64_t* d_rbase = d_rlen + nblk;
     PairFmtArgs a{nullptr, nullptr, d_slen, 0, nullptr, nullptr, ncols, d_row_ids, d_row_offs, d_col_ids, d_col_offs,
                   first ? 1 : 0, d_px, d_py};
-    hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, d_rlen);
+    hipLaunchKernelGGL(k_pairs_row_len, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, st, a, (int)nch, d_rlen);
     HIP_TRY(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_pairs_row_base, dim3(1), dim3(FMT_BLOCK), 0, st, (const int64_t*)d_rlen, nrows, text_cap,
+    hipLaunchKernelGGL(k_pairs_row_base, dim3(1), dim3(FMT_BLOCK), 0, st, (const int64_t*)d_rlen, nblk, text_cap,
                        d_rbase, d_total);
     HIP_TRY(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nrows), dim3(FMT_BLOCK), 0, st, a, (const int64_t*)d_rbase,
+    hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, st, a, (int)nch, (const int64_t*)d_rbase,
                        (char*)d_text, (const int64_t*)d_total);
     HIP_TRY(ctx, hipGetLastError());
     return 0;

@@ -206,44 +206,66 @@ __device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int
 
 constexpr int FMT_BLOCK = 256;
 
-// Pass 1: total text length of each row.
-__global__ void __launch_bounds__(FMT_BLOCK) k_fmt_row_len(FmtArgs a, int64_t* __restrict__ row_len) {
+// The work unit of both passes is a chunk: FMT_BLOCK consecutive tokens of one row (block b = row
+// b / nch, chunk b % nch), so that a launch has rows x nch workgroups -- one workgroup per row left
+// most of the chip idle on the few-hundred-row blocks of the dense task.
+// Pass 1: text length of each chunk.
+__global__ void __launch_bounds__(FMT_BLOCK) k_fmt_row_len(FmtArgs a, int nch, int64_t* __restrict__ chunk_len) {
     __shared__ int64_t red[FMT_BLOCK];
-    const int64_t r = blockIdx.x;
+    const int64_t r = blockIdx.x / nch;
+    const int64_t t = (int64_t)(blockIdx.x - r * nch) * FMT_BLOCK + threadIdx.x;
     const int64_t nt = fmt_ntok(a, r);
-    int64_t s = 0;
-    for (int64_t t = threadIdx.x; t < nt; t += FMT_BLOCK) s += fmt_token_len(a, r, t, nt);
-    red[threadIdx.x] = s;
+    red[threadIdx.x] = t < nt ? fmt_token_len(a, r, t, nt) : 0;
     __syncthreads();
     for (int w = FMT_BLOCK / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) row_len[r] = red[0];
+    if (threadIdx.x == 0) chunk_len[blockIdx.x] = red[0];
 }
 
-// Pass 2: write; row_base[r] = byte offset of row r in `out`.
+constexpr int FMT_STAGE = 16384;  // LDS bytes a chunk's text is assembled in before it goes out
+
+// Pass 2: write; chunk_base[b] = byte offset of chunk b in `out`.  Each thread renders its token
+// (a few to a few dozen bytes) into LDS; the workgroup then stores the chunk with 16-byte stores
+// from its first 16-aligned byte on -- the text goes to pinned host memory over the link, where a
+// byte store per thread per character wasted most of the bandwidth.  A chunk longer than the
+// stage (very long ids or suffixes) is written token by token.
 __global__ void __launch_bounds__(FMT_BLOCK)
-k_fmt_rows(FmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out) {
+k_fmt_rows(FmtArgs a, int nch, const int64_t* __restrict__ chunk_base, char* __restrict__ out) {
     __shared__ int64_t scan[FMT_BLOCK];
-    const int64_t r = blockIdx.x;
+    __shared__ __attribute__((aligned(16))) char stage[FMT_STAGE + 16];
+    const int64_t r = blockIdx.x / nch;
+    const int64_t t = (int64_t)(blockIdx.x - r * nch) * FMT_BLOCK + threadIdx.x;
     const int64_t nt = fmt_ntok(a, r);
-    int64_t base = row_base[r];
-    for (int64_t t0 = 0; t0 < nt; t0 += FMT_BLOCK) {
-        const int64_t t = t0 + threadIdx.x;
-        const int64_t len = t < nt ? fmt_token_len(a, r, t, nt) : 0;
-        scan[threadIdx.x] = len;
+    const int64_t len = t < nt ? fmt_token_len(a, r, t, nt) : 0;
+    scan[threadIdx.x] = len;
+    __syncthreads();
+    for (int w = 1; w < FMT_BLOCK; w <<= 1) {  // inclusive Hillis-Steele scan
+        const int64_t add = threadIdx.x >= w ? scan[threadIdx.x - w] : 0;
         __syncthreads();
-        for (int w = 1; w < FMT_BLOCK; w <<= 1) {  // inclusive Hillis-Steele scan
-            const int64_t add = threadIdx.x >= w ? scan[threadIdx.x - w] : 0;
-            __syncthreads();
-            scan[threadIdx.x] += add;
-            __syncthreads();
-        }
-        if (t < nt) fmt_token_write(a, r, t, nt, out + base + scan[threadIdx.x] - len);
-        base += scan[FMT_BLOCK - 1];
+        scan[threadIdx.x] += add;
         __syncthreads();
     }
+    const int64_t b0 = chunk_base[blockIdx.x];
+    const int64_t total = scan[FMT_BLOCK - 1];
+    if (total > FMT_STAGE) {
+        if (t < nt) fmt_token_write(a, r, t, nt, out + b0 + scan[threadIdx.x] - len);
+        return;
+    }
+    // stage byte k + sh holds output byte b0 + k: 16-byte output words are 16-byte stage words
+    const int sh = (int)(b0 & 15);
+    if (t < nt) fmt_token_write(a, r, t, nt, stage + sh + scan[threadIdx.x] - len);
+    __syncthreads();
+    const int tot = (int)total;
+    const int h = min(tot, (16 - sh) & 15);  // bytes before the first 16-aligned output byte
+    const int nw = (tot - h) >> 4;
+    if ((int)threadIdx.x < h) out[b0 + threadIdx.x] = stage[sh + threadIdx.x];
+    const uint4* sw = reinterpret_cast<const uint4*>(stage + sh + h);
+    uint4* ow = reinterpret_cast<uint4*>(out + b0 + h);
+    for (int w = threadIdx.x; w < nw; w += FMT_BLOCK) ow[w] = sw[w];
+    const int tb = h + 16 * nw;
+    if (tb + (int)threadIdx.x < tot) out[b0 + tb + threadIdx.x] = stage[sh + tb + threadIdx.x];
 }
 
 // ---- aligned_pairs.txt (pairs.py:51-97 SequencePairHandler.Formatted, fed x-major by
@@ -278,19 +300,18 @@ __device__ __forceinline__ int64_t pair_fmt_len(const PairFmtArgs& a, int64_t r,
     return ((r | c) || !a.first ? 1 : 0) + lx + 3 + ly + 1 + 3 * (L + 1);
 }
 
-// Pass 1: text length of each row of pairs.
-__global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_len(PairFmtArgs a, int64_t* __restrict__ row_len) {
+// Pass 1: text length of each chunk of pairs (FMT_BLOCK columns of one row, as k_fmt_row_len).
+__global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_len(PairFmtArgs a, int nch, int64_t* __restrict__ chunk_len) {
     __shared__ int64_t red[FMT_BLOCK];
-    const int64_t r = blockIdx.x;
-    int64_t s = 0;
-    for (int64_t c = threadIdx.x; c < a.ncols; c += FMT_BLOCK) s += pair_fmt_len(a, r, c);
-    red[threadIdx.x] = s;
+    const int64_t r = blockIdx.x / nch;
+    const int64_t c = (int64_t)(blockIdx.x - r * nch) * FMT_BLOCK + threadIdx.x;
+    red[threadIdx.x] = c < a.ncols ? pair_fmt_len(a, r, c) : 0;
     __syncthreads();
     for (int w = FMT_BLOCK / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) row_len[r] = red[0];
+    if (threadIdx.x == 0) chunk_len[blockIdx.x] = red[0];
 }
 
 // Asynchronous form: exclusive prefix of the row lengths on the device (one workgroup; rows in
@@ -321,20 +342,21 @@ __global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_base(const int64_t* __r
     }
 }
 
-// Pass 2: one workgroup per row; the pair offsets of 256 columns at a time by an LDS scan, then
+// Pass 2: one workgroup per chunk (FMT_BLOCK columns of a row); the pair offsets by an LDS scan, then
 // each wave writes whole pairs, its lanes striding over the pair's bytes (coalesced stores).
 __global__ void __launch_bounds__(FMT_BLOCK)
-k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restrict__ out,
+k_pairs_text(PairFmtArgs a, int nch, const int64_t* __restrict__ chunk_base, char* __restrict__ out,
              const int64_t* __restrict__ cap_ok = nullptr) {
     __shared__ int64_t scan[FMT_BLOCK];
     if (cap_ok && cap_ok[1] == 0) return;  // asynchronous form: the text would not fit the buffer
-    const int64_t r = blockIdx.x;
+    const int64_t r = blockIdx.x / nch;
+    const int64_t c0 = (int64_t)(blockIdx.x - r * nch) * FMT_BLOCK;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int64_t base = row_base[r];
+    const int64_t base = chunk_base[blockIdx.x];
     const int lx = (int)(a.roffs[r + 1] - a.roffs[r]);
     const uint8_t* idx = a.rid + a.roffs[r];
     const int nx = a.px ? 0 : a.qmeta[r].x;
-    for (int64_t c0 = 0; c0 < a.ncols; c0 += FMT_BLOCK) {
+    {
         const int64_t c = c0 + threadIdx.x;
         const int64_t len = c < a.ncols ? pair_fmt_len(a, r, c) : 0;
         scan[threadIdx.x] = len;
@@ -381,22 +403,24 @@ k_pairs_text(PairFmtArgs a, const int64_t* __restrict__ row_base, char* __restri
                 const uint32_t p = X[v], q2 = Y[v];
                 return (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
             };
-            // 4-byte stores from the first 4-aligned byte of the pair's text (256 bytes per wave store:
-            // the text goes straight to pinned host memory, where wide writes count), bytes at both ends
+            // 16-byte stores from the first 16-aligned byte of the pair's text (1 KB per wave store: the
+            // text goes straight to pinned host memory, where the write size sets the link rate --
+            // tools/d2h_probe's 54.7 GB/s is 16-byte stores), bytes at both ends
             const int pl = (int)plen;
-            const int a0 = min(pl, (int)((4u - (uint32_t)((uintptr_t)o & 3u)) & 3u));
-            const int nw = (pl - a0) >> 2;
+            const int a0 = min(pl, (int)((16u - (uint32_t)((uintptr_t)o & 15u)) & 15u));
+            const int nw = (pl - a0) >> 4;
             if (lane < a0) o[lane] = (char)byte_at(lane);
+            auto word_at = [&](int t) {
+                return byte_at(t) | byte_at(t + 1) << 8 | byte_at(t + 2) << 16 | byte_at(t + 3) << 24;
+            };
             for (int wi = lane; wi < nw; wi += 64) {
-                const int t = a0 + 4 * wi;
-                const uint32_t v = byte_at(t) | byte_at(t + 1) << 8 | byte_at(t + 2) << 16 | byte_at(t + 3) << 24;
-                *(uint32_t*)__builtin_assume_aligned(o + t, 4) = v;
+                const int t = a0 + 16 * wi;
+                *(uint4*)__builtin_assume_aligned(o + t, 16) =
+                    make_uint4(word_at(t), word_at(t + 4), word_at(t + 8), word_at(t + 12));
             }
-            const int tb = a0 + 4 * nw;
+            const int tb = a0 + 16 * nw;
             if (tb + lane < pl) o[tb + lane] = (char)byte_at(tb + lane);
         }
-        base += scan[FMT_BLOCK - 1];
-        __syncthreads();
     }
 }
 // Compaction of one orientation's aligned strings out of the walkers' slots (StrOut): pair k's
