@@ -145,6 +145,9 @@ class VersusAll:
         self.params.engine.launch_pairs = WALK_LAUNCH_PAIRS
         # HBM for the (b, a) aligned strings the one-fill aligned_pairs path keeps until row b
         self.params.engine.keep_bytes = 160 << 30
+        # CUs' worth of workgroup slots the one-fill aligned_pairs path leaves free beside each
+        # block's fill, for the previous block's text kernel (host-link bound: it needs few CUs)
+        self.params.engine.text_reserve_cus = 32
         self.params.engine.stream = None
         self.params.engine.dense_limit = 4 << 30
         self.params.engine.block_bytes = 256 << 20
@@ -444,7 +447,9 @@ class VersusAll:
 
         # CUs' worth of workgroup slots the fill leaves free, so that the previous block's text kernel
         # (bound by the host link it writes through) runs beside it instead of after it
-        reserve = int(os.environ.get("TAXI2_TEXT_RESERVE_CUS", "0"))
+        # (measured at N = 5 000: 0 -> 4.9 s, 16 -> 4.2 s, 32 -> 3.6 s, 48 -> 3.6 s, profiles/r5/task_reserve/)
+        reserve = int(os.environ.get("TAXI2_TEXT_RESERVE_CUS", self.params.engine.text_reserve_cus))
+        fill_ev = []  # (start, end) events of every block's fill: the fills' GPU time for task.timings
 
         def launch(x0: int, x1: int, cnt: int):
             """Block rows [x0, x1) (cnt triangle pairs) on `stream`: the fill (metrics + both
@@ -455,14 +460,20 @@ class VersusAll:
                 sx = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
                 sy = torch.empty((cnt, 2, cap), dtype=torch.uint8, device=dev)
                 sl = torch.empty((cnt, 2), dtype=torch.int32, device=dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
                 eng.tri_strings_dev(st, k0, cnt, clabels, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(),
                                     sl.data_ptr(), scores, stream.cuda_stream, reserve_cus=reserve)
+                e1.record(stream)
+                fill_ev.append((e0, e1))
                 # pair (a, b) of the block: a in [x0, x1), b > a
                 rows = torch.arange(x0, x1, device=dev)
                 per = n - 1 - rows
-                ra = torch.repeat_interleave(rows, per)
+                # (output_size: repeat_interleave would otherwise read the total back -- a host sync
+                # behind this block's fill, which kept block k's text from running beside it)
+                ra = torch.repeat_interleave(rows, per, output_size=cnt)
                 first = torch.cumsum(per, 0) - per
-                rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(first, per)
+                rb = ra + 1 + torch.arange(cnt, device=dev) - torch.repeat_interleave(first, per, output_size=cnt)
                 if Dd is not None:
                     Dd[ra, rb] = d[:, 0, :]
                     Dd[rb, ra] = d[:, 1, :]
@@ -579,6 +590,8 @@ class VersusAll:
         tstream.synchronize()
         stream.synchronize()
         del kept
+        if isinstance(self.timings, dict):  # the fills' own GPU time (they overlap the text)
+            self.timings["fill_gpu_s"] = sum(a.elapsed_time(b) for a, b in fill_ev) / 1e3
         if sink is not None:
             t0 = perf_counter()
             for f in futs:
