@@ -63,15 +63,18 @@ def gpu_text_ok(vals: np.ndarray, decimals: int | None) -> bool:
     return fin.size == 0 or float(np.max(np.abs(fin))) * 10.0 ** decimals < 2.0 ** 62
 
 
-def write_rows_gpu(fh, eng, vals: np.ndarray, row_pre: list, col_pre, decimals: int, missing: str,
-                   max_values: int = 1 << 23) -> None:
+def write_rows_gpu(fh, eng, vals, row_pre: list, col_pre, decimals: int, missing: str,
+                   max_values: int = 1 << 23, stream: int | None = None) -> None:
     """Stream writer text (linear when col_pre is given, matrix otherwise) to the binary file
-    ``fh`` in row chunks of about ``max_values`` values."""
-    per_row = max(1, int(np.prod(vals.shape[1:])))
+    ``fh`` in row chunks of about ``max_values`` values (``vals`` on the host, or a CUDA tensor
+    formatted where it is, ordered on ``stream``)."""
+    per_row = max(1, int(np.prod(tuple(vals.shape[1:]))))
     step = max(1, max_values // per_row)
     for r0 in range(0, vals.shape[0], step):
         r1 = min(vals.shape[0], r0 + step)
-        fh.write(eng.format_rows(vals[r0:r1], row_pre[r0:r1], col_pre, decimals=decimals, missing=missing, view=True))
+        kw = {"stream": stream} if stream is not None else {}
+        fh.write(eng.format_rows(vals[r0:r1], row_pre[r0:r1], col_pre, decimals=decimals, missing=missing, view=True,
+                                 **kw))
 
 
 def _brace_to_percent(fmt: str) -> str | None:

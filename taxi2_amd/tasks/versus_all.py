@@ -382,7 +382,10 @@ class VersusAll:
         # complete rows -- runs on `tstream` after block k's event.  Tensors of a block are
         # record_stream()'d on tstream before they are dropped, so the caching allocator never hands
         # their memory to the next block while the text still reads it.
-        tstream = torch.cuda.Stream(dev)
+        # high priority: a queue of its own beside the fill's (HIP multiplexes streams onto
+        # GPU_MAX_HW_QUEUES hardware queues, and two streams sharing one run their kernels in
+        # order), and the dispatcher hands freed slots to the text first
+        tstream = torch.cuda.Stream(dev, priority=0 if os.environ.get("TAXI2_TEXT_PRIO") == "0" else -1)
         with torch.cuda.stream(stream):
             lens = torch.as_tensor(lens_h, device=dev)
             # self alignments (x, x) for the diagonal pairs' text
@@ -1450,9 +1453,13 @@ class _BlockWriters:
         ready.synchronize()
         dec = self.dec
         ok = dec is not None and not self.dupids and self.pairs_fh is None
+        if getattr(self, "_wstream", None) is None:
+            # the writers' own high-priority stream for the check and the formatters (not the
+            # legacy default stream; not a hardware queue shared with the persistent fill, whose
+            # kernels would otherwise hold the writers' behind it)
+            self._wstream = torch.cuda.Stream(A.device, priority=-1)
+        ws = self._wstream.cuda_stream
         if ok and A.numel():
-            if getattr(self, "_wstream", None) is None:  # (not the legacy default stream)
-                self._wstream = torch.cuda.Stream(A.device)
             with torch.cuda.stream(self._wstream):
                 big = float(torch.where(torch.isfinite(A), A.abs(), torch.zeros_like(A)).max())
             ok = big * 10.0 ** dec < 2.0 ** 62
@@ -1461,10 +1468,10 @@ class _BlockWriters:
             return
         ids = self.ids
         if self.lin is not None:
-            write_rows_gpu(self.lin, self.eng, A, self.pre[x0:x1], self.pre, dec, self.missing)
+            write_rows_gpu(self.lin, self.eng, A, self.pre[x0:x1], self.pre, dec, self.missing, stream=ws)
         if self.mats is not None:
             for m, fh in enumerate(self.mats):
-                write_rows_gpu(fh, self.eng, A[:, :, m], ids[x0:x1], None, dec, self.missing)
+                write_rows_gpu(fh, self.eng, A[:, :, m], ids[x0:x1], None, dec, self.missing, stream=ws)
         if self.summ is None:
             return
         from .subsets import SUMMARY_CHUNK_VALUES
@@ -1475,7 +1482,7 @@ class _BlockWriters:
             self.summ.write(self.eng.format_summary(
                 A[r0:r1], ids[x0 + r0 : x0 + r1], ids, self.suf[2 * (x0 + r0) : 2 * (x0 + r1)], self.suf,
                 self.codes[x0 + r0 : x0 + r1], self.codes, has_genera=bool(self.genera),
-                has_species=bool(self.species), decimals=dec, missing=self.missing, view=True))
+                has_species=bool(self.species), decimals=dec, missing=self.missing, view=True, stream=ws))
 
     def write_text_host(self, x0: int, x1: int, A: np.ndarray, pairs_text: bytes | None = None) -> None:
         """write_text on the block's values already on the host (a writer thread's entry)."""

@@ -117,7 +117,8 @@ run_step() {
     tool:*)
         (cd "$R" && timeout -k 10 900 python3 -u "tools/${s#tool:}.py" > "$OUT/${s#tool:}.json" 2> "$OUT/${s#tool:}.err") ;;
     sec:*)
-        (cd "$R" && timeout -k 10 600 python3 -u bench_secondary.py "${s#sec:}" > "$OUT/sec_${s#sec:}.json" 2> "$OUT/sec_${s#sec:}.err") ;;
+        # (sec:A+B+C: those legs one after another in one process, as bench.py runs them)
+        (cd "$R" && timeout -k 10 600 python3 -u bench_secondary.py $(echo "${s#sec:}" | tr '+' ' ') > "$OUT/sec_${s#sec:}.json" 2> "$OUT/sec_${s#sec:}.err") ;;
     with:*)  # with:V=X,...:STEP -- any other step with those environment settings
         local rest=${s#with:}
         local envs=${rest%%:*} inner=${rest#*:}
@@ -126,7 +127,7 @@ run_step() {
         local rest=${s#secenv:}
         local name=${rest%%:*}; rest=${rest#*:}
         local leg=${rest%%:*} envs=${rest#*:}
-        (cd "$R" && env $(echo "$envs" | tr ',' ' ') timeout -k 10 600 python3 -u bench_secondary.py "$leg" \
+        (cd "$R" && env $(echo "$envs" | tr ',' ' ') timeout -k 10 600 python3 -u bench_secondary.py $(echo "$leg" | tr '+' ' ') \
             > "$OUT/secenv_$name.json" 2> "$OUT/secenv_$name.err") ;;
     sectrace:*)
         (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sectrace_${s#sectrace:}" -o run -- \
