@@ -344,10 +344,24 @@ __global__ void __launch_bounds__(FMT_BLOCK) k_pairs_row_base(const int64_t* __r
 
 // Pass 2: one workgroup per chunk (FMT_BLOCK columns of a row); the pair offsets by an LDS scan, then
 // each wave writes whole pairs, its lanes striding over the pair's bytes (coalesced stores).
+//
+// A pair's two aligned strings are first staged in the wave's LDS (PT_STAGE bytes each): every lane
+// issues its share of 4-byte loads of the strings' aligned windows at once and waits once.  Read
+// byte by byte from global memory, as the text needs them, every byte was a load, a wait and a use
+// in sequence (~80 waits per 16 output bytes of a lane): latency-bound, and with the chip shared
+// with the next block's fill the text kernel ran at a fifth of the host link's rate.  Longer pairs
+// (more than PT_STAGE aligned columns) read global memory directly.
+constexpr int PT_STAGE = 2304;  // staged bytes per string and wave (aligned pairs of up to 2 300 columns)
+constexpr int PT_WORDS = (PT_STAGE + 8) / 4;
+constexpr int PT_LOADS = (PT_WORDS + 63) / 64;  // 4-byte loads per lane and string
+constexpr int PT_HDR = 192;  // staged header bytes (separator, "idx / idy", LF) per wave
+
 __global__ void __launch_bounds__(FMT_BLOCK)
 k_pairs_text(PairFmtArgs a, int nch, const int64_t* __restrict__ chunk_base, char* __restrict__ out,
              const int64_t* __restrict__ cap_ok = nullptr) {
     __shared__ int64_t scan[FMT_BLOCK];
+    __shared__ __attribute__((aligned(16))) uint32_t stg[FMT_BLOCK / 64][2][PT_WORDS];
+    __shared__ uint8_t hdr[FMT_BLOCK / 64][PT_HDR];
     if (cap_ok && cap_ok[1] == 0) return;  // asynchronous form: the text would not fit the buffer
     const int64_t r = blockIdx.x / nch;
     const int64_t c0 = (int64_t)(blockIdx.x - r * nch) * FMT_BLOCK;
@@ -356,6 +370,8 @@ k_pairs_text(PairFmtArgs a, int nch, const int64_t* __restrict__ chunk_base, cha
     const int lx = (int)(a.roffs[r + 1] - a.roffs[r]);
     const uint8_t* idx = a.rid + a.roffs[r];
     const int nx = a.px ? 0 : a.qmeta[r].x;
+    const uint8_t* sxb = reinterpret_cast<const uint8_t*>(stg[wv][0]);
+    const uint8_t* syb = reinterpret_cast<const uint8_t*>(stg[wv][1]);
     {
         const int64_t c = c0 + threadIdx.x;
         const int64_t len = c < a.ncols ? pair_fmt_len(a, r, c) : 0;
@@ -386,43 +402,96 @@ k_pairs_text(PairFmtArgs a, int nch, const int64_t* __restrict__ chunk_base, cha
                 X = a.sx + k * a.cap + end - L;
                 Y = a.sy + k * a.cap + end - L;
             }
+            // the strings' aligned 4-byte windows into the wave's stage (wave-uniform branch)
+            const int xo = (int)((uintptr_t)X & 3u), yo = (int)((uintptr_t)Y & 3u);
             const int h = sep + lx + 3 + ly + 1;  // header with its separator
-            const int L1 = L + 1;
-            // byte t of the pair's text: the header, then three lines of L + 1 bytes (no division)
-            auto byte_at = [&](int t) -> uint32_t {
-                if (t < h) {
-                    const int u = t - sep;
-                    return u < 0 ? '\n' : u < lx ? idx[u] : u < lx + 3 ? (uint32_t)" / "[u - lx] : u < lx + 3 + ly ? idy[u - lx - 3] : '\n';
-                }
-                int v = t - h;
-                const int line = v < L1 ? 0 : v < 2 * L1 ? 1 : 2;
-                v -= line * L1;
-                if (v == L) return '\n';
-                if (line == 0) return X[v];
-                if (line == 2) return Y[v];
-                const uint32_t p = X[v], q2 = Y[v];
-                return (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
+            auto hdr_at = [&](int t) -> uint32_t {
+                const int u = t - sep;
+                return u < 0 ? '\n' : u < lx ? idx[u] : u < lx + 3 ? (uint32_t)" / "[u - lx] : u < lx + 3 + ly ? idy[u - lx - 3] : '\n';
             };
+            const bool staged = L <= PT_STAGE && h <= PT_HDR;
+            if (staged) {
+                const uint32_t* xw = reinterpret_cast<const uint32_t*>(X - xo);
+                const uint32_t* yw = reinterpret_cast<const uint32_t*>(Y - yo);
+                const int nwx = (xo + L + 3) >> 2, nwy = (yo + L + 3) >> 2;
+                uint32_t rx[PT_LOADS], ry[PT_LOADS];
+#pragma unroll
+                for (int i = 0; i < PT_LOADS; ++i) {
+                    const int w = lane + 64 * i;
+                    rx[i] = w < nwx ? xw[w] : 0u;
+                    ry[i] = w < nwy ? yw[w] : 0u;
+                }
+                uint32_t hb[PT_HDR / 64];
+#pragma unroll
+                for (int i = 0; i < PT_HDR / 64; ++i) hb[i] = lane + 64 * i < h ? hdr_at(lane + 64 * i) : 0u;
+                __builtin_amdgcn_wave_barrier();  // the previous pair's reads of the stage are done
+#pragma unroll
+                for (int i = 0; i < PT_LOADS; ++i) {
+                    const int w = lane + 64 * i;
+                    if (w < nwx) stg[wv][0][w] = rx[i];
+                    if (w < nwy) stg[wv][1][w] = ry[i];
+                }
+#pragma unroll
+                for (int i = 0; i < PT_HDR / 64; ++i) hdr[wv][lane + 64 * i] = (uint8_t)hb[i];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            const int L1 = L + 1;
+            const int pl = (int)plen;
             // 16-byte stores from the first 16-aligned byte of the pair's text (1 KB per wave store: the
             // text goes straight to pinned host memory, where the write size sets the link rate --
             // tools/d2h_probe's 54.7 GB/s is 16-byte stores), bytes at both ends
-            const int pl = (int)plen;
             const int a0 = min(pl, (int)((16u - (uint32_t)((uintptr_t)o & 15u)) & 15u));
             const int nw = (pl - a0) >> 4;
-            if (lane < a0) o[lane] = (char)byte_at(lane);
-            auto word_at = [&](int t) {
-                return byte_at(t) | byte_at(t + 1) << 8 | byte_at(t + 2) << 16 | byte_at(t + 3) << 24;
-            };
-            for (int wi = lane; wi < nw; wi += 64) {
-                const int t = a0 + 16 * wi;
-                *(uint4*)__builtin_assume_aligned(o + t, 16) =
-                    make_uint4(word_at(t), word_at(t + 4), word_at(t + 8), word_at(t + 12));
-            }
             const int tb = a0 + 16 * nw;
-            if (tb + lane < pl) o[tb + lane] = (char)byte_at(tb + lane);
+            // the text from the stage (LDS reads) or, for a long pair, from global memory: two
+            // instantiations, so that the staged form's reads are ds_read and not flat loads
+            auto emit = [&](auto STG) {
+                constexpr bool S = decltype(STG)::value;
+                // byte t of the pair's text: the header, then three lines of L + 1 bytes (no division).
+                // Staged: branch-free -- both string bytes and the header byte are read from LDS at
+                // clamped positions and selected, so a lane's 16 bytes issue their reads together
+                auto byte_at = [&](int t) -> uint32_t {
+                    if constexpr (S) {
+                        const uint32_t hbyte = hdr[wv][min(t, PT_HDR - 1)];
+                        int v = t - h;
+                        const int line = (v >= L1) + (v >= 2 * L1);
+                        v -= line * L1;
+                        const int vc = max(0, min(v, L - 1));
+                        const uint32_t p = sxb[xo + vc], q2 = syb[yo + vc];
+                        const uint32_t pat = (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
+                        const uint32_t body = v == L ? '\n' : line == 0 ? p : line == 2 ? q2 : pat;
+                        return t < h ? hbyte : body;
+                    } else {
+                        if (t < h) return hdr_at(t);
+                        int v = t - h;
+                        const int line = v < L1 ? 0 : v < 2 * L1 ? 1 : 2;
+                        v -= line * L1;
+                        if (v == L) return '\n';
+                        if (line == 0) return X[v];
+                        if (line == 2) return Y[v];
+                        const uint32_t p = X[v], q2 = Y[v];
+                        return (p == q2 && p != '-') ? '|' : (p == '-' || q2 == '-') ? '-' : '.';
+                    }
+                };
+                auto word_at = [&](int t) {
+                    return byte_at(t) | byte_at(t + 1) << 8 | byte_at(t + 2) << 16 | byte_at(t + 3) << 24;
+                };
+                if (lane < a0) o[lane] = (char)byte_at(lane);
+                for (int wi = lane; wi < nw; wi += 64) {
+                    const int t = a0 + 16 * wi;
+                    *(uint4*)__builtin_assume_aligned(o + t, 16) =
+                        make_uint4(word_at(t), word_at(t + 4), word_at(t + 8), word_at(t + 12));
+                }
+                if (tb + lane < pl) o[tb + lane] = (char)byte_at(tb + lane);
+            };
+            if (staged) emit(std::true_type{});
+            else emit(std::false_type{});
         }
     }
 }
+
 // Compaction of one orientation's aligned strings out of the walkers' slots (StrOut): pair k's
 // string is the last slen[k * nslot + slot] bytes before byte end[k] of its slot, copied to
 // dst + off[k].  One wave per pair, lanes striding over the bytes (coalesced loads and stores).

@@ -24,6 +24,7 @@ NotImplementedError.
 from __future__ import annotations
 
 import os
+import sys
 from pathlib import Path
 from time import perf_counter
 from typing import Callable
@@ -83,6 +84,8 @@ def walk_strings_ok(scores: tuple, seqs: list) -> bool:
 WALK_LAUNCH_PAIRS = 1 << 19  # ordered pairs per string-emitting aligner launch (the bench's batch)
 WALK_BLOCK_BYTES = 8 << 30   # HBM for one block's string slots + metrics
 DEVICE_D_BYTES = 16 << 30    # the walked path's device copy of the counter metrics, at most
+TEXT_CALL_BYTES = 1 << 30    # aligned_pairs.txt text per formatter call (bound), i.e. its pinned buffer
+PIPE_DEPTH = 2               # one-fill aligned_pairs path: blocks aligned ahead of the block being written
 
 
 def walk_block_rows(n: int, per_pair: int, block_bytes: int, launch_pairs: int = WALK_LAUNCH_PAIRS) -> int:
@@ -326,6 +329,10 @@ class VersusAll:
         Mc = len(cidx)
         npairs = n * (n - 1) // 2
         ids = pack_strings([s.id for s in seqs])
+        # text bytes of row x, bounded above: per pair "idx / idy" + 4 LF + 3 lines of at most
+        # len(x) + len(y) columns
+        idl = np.diff(ids[1]).astype(np.int64)
+        row_text_bound = n * (idl + 8 + 3 * lens_h + 3) + int(idl.sum()) + 3 * int(lens_h.sum())
         total = len(self.params.distances.metrics) * n * n
         launch = int(self.params.engine.launch_pairs or 0)
         slot_budget = max(int(self.params.engine.block_bytes), WALK_BLOCK_BYTES if launch else 0)
@@ -484,10 +491,43 @@ class VersusAll:
                 ev.record(stream)
             return dict(x0=x0, x1=x1, k0=k0, cnt=cnt, d=d, sx=sx, sy=sy, sl=sl, ra=ra, rb=rb, ev=ev)
 
+        prof = {} if os.environ.get("TAXI2_TASK_PROFILE") else None
+
+        def pointers(x0, x1, k0, cnt, sx=None, sy=None, sl=None, end=None):
+            """Per-pair string pointers and lengths of the text of rows [x0, x1) x every y: (x, y > x)
+            from this block's slot 0, (x, y < x) from the kept (y, x) strings -- x's aligned string
+            is the pair's b side (sy) -- and (x, x) from the self alignments (on tstream)."""
+            xs_ = torch.arange(x0, x1, device=dev)[:, None]
+            ys_ = torch.arange(n, device=dev)[None, :]
+            up = ys_ > xs_
+            lo = ys_ < xs_
+            pu = xs_ * (2 * n - xs_ - 1) // 2 + (ys_ - xs_ - 1)   # pair (x, y) for y > x
+            pl = ys_ * (2 * n - ys_ - 1) // 2 + (xs_ - ys_ - 1)   # pair (y, x) for y < x
+            px = torch.where(lo, kpy[pl.clamp(0, npairs - 1)], px_self[xs_.expand(-1, n)])
+            py = torch.where(lo, kpx[pl.clamp(0, npairs - 1)], py_self[xs_.expand(-1, n)])
+            ln = torch.where(lo, klen[pl.clamp(0, npairs - 1)], slen_self[xs_.expand(-1, n)])
+            if cnt:
+                q = (pu - k0).clamp(0, max(0, cnt - 1))
+                L0 = sl[:, 0].to(torch.int64)
+                start0 = q * 2 * cap + end[q] - L0[q]
+                px = torch.where(up, sx.data_ptr() + start0, px)
+                py = torch.where(up, sy.data_ptr() + start0, py)
+                ln = torch.where(up, sl[:, 0][q], ln)
+            return px.contiguous(), py.contiguous(), ln.to(torch.int32).contiguous()
+
         def post(b) -> None:
             """Block b's compaction, text and rows on tstream (after its fill)."""
             x0, x1, k0, cnt = b["x0"], b["x1"], b["k0"], b["cnt"]
             t0 = perf_counter()
+            pt = {}  # TAXI2_TASK_PROFILE: host time per step of post()
+            tl = [t0]
+
+            def mark(name):
+                if prof is not None:
+                    t = perf_counter()
+                    pt[name] = t - tl[0]
+                    tl[0] = t
+
             with torch.cuda.stream(tstream):
                 if cnt:
                     tstream.wait_event(b["ev"])
@@ -506,6 +546,7 @@ class VersusAll:
                     L1 = sl[:, 1].to(torch.int64)
                     off = torch.cumsum(L1, 0) - L1
                     tot = int(L1.sum().item())  # waits for tstream only (this block's fill is done)
+                    mark("wait")
                     kxy = carve(2 * max(1, tot), cnt, k0 + cnt)
                     kx, ky = kxy[:max(1, tot)], kxy[max(1, tot):]
                     eng.pack_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 1, end.data_ptr(),
@@ -514,31 +555,28 @@ class VersusAll:
                     kpy[k0:k0 + cnt] = ky.data_ptr() + off
                     klen[k0:k0 + cnt] = sl[:, 1]
                     kept_b[0] += 2 * tot
-                # text of rows [x0, x1) x every y: (x, y > x) from this block's slot 0, (x, y < x)
-                # from the kept (y, x) strings -- x's aligned string is the pair's b side (sy) --
-                # and (x, x) from the self alignments
-                xs_ = torch.arange(x0, x1, device=dev)[:, None]
-                ys_ = torch.arange(n, device=dev)[None, :]
-                up = ys_ > xs_
-                lo = ys_ < xs_
-                pu = xs_ * (2 * n - xs_ - 1) // 2 + (ys_ - xs_ - 1)   # pair (x, y) for y > x
-                pl = ys_ * (2 * n - ys_ - 1) // 2 + (xs_ - ys_ - 1)   # pair (y, x) for y < x
-                px = torch.where(lo, kpy[pl.clamp(0, npairs - 1)], px_self[xs_.expand(-1, n)])
-                py = torch.where(lo, kpx[pl.clamp(0, npairs - 1)], py_self[xs_.expand(-1, n)])
-                ln = torch.where(lo, klen[pl.clamp(0, npairs - 1)], slen_self[xs_.expand(-1, n)])
-                if cnt:
-                    q = (pu - k0).clamp(0, max(0, cnt - 1))
-                    L0 = sl[:, 0].to(torch.int64)
-                    start0 = q * 2 * cap + end[q] - L0[q]
-                    px = torch.where(up, sx.data_ptr() + start0, px)
-                    py = torch.where(up, sy.data_ptr() + start0, py)
-                    ln = torch.where(up, sl[:, 0][q], ln)
-                px, py, ln = px.contiguous(), py.contiguous(), ln.to(torch.int32).contiguous()
-                fh.write(eng.format_pairs_ptr_dev(x1 - x0, n, px.data_ptr(), py.data_ptr(), ln.data_ptr(),
-                                                  (ids[0], ids[1][x0:x1 + 1]), ids, first=x0 == 0,
-                                                  stream=tstream.cuda_stream))
+                mark("pack")
+                px, py, ln = pointers(x0, x1, k0, cnt, sx, sy, sl, end) if cnt else pointers(x0, x1, k0, 0)
+                mark("pointers")
+                # the text in row runs of at most TEXT_CALL_BYTES (an upper bound from the lengths):
+                # the pinned buffer the kernel writes into stays ~1 GB, allocated once -- a block's
+                # whole text (~4 GB at N = 5 000) took ~1 s to pin, twice as the buffer grew
+                r0 = x0
+                while r0 < x1:
+                    r1 = r0 + 1
+                    tot_b = row_text_bound[r0]
+                    while r1 < x1 and tot_b + row_text_bound[r1] <= TEXT_CALL_BYTES:
+                        tot_b += row_text_bound[r1]
+                        r1 += 1
+                    o = (r0 - x0) * n
+                    fh.write(eng.format_pairs_ptr_dev(r1 - r0, n, px.data_ptr() + 8 * o, py.data_ptr() + 8 * o,
+                                                      ln.data_ptr() + 4 * o, (ids[0], ids[1][r0:r1 + 1]), ids,
+                                                      first=r0 == 0, stream=tstream.cuda_stream))
+                    r0 = r1
+                mark("text")
                 rows_in()  # the previous block's staged rows into D
                 rows_out(x0, x1)
+                mark("rows")
                 if sink is not None:  # rows [x0, x1) are complete: adjusted on the GPU, text in the thread
                     while len(futs) >= 2:  # at most two blocks queued for the thread
                         futs.pop(0).result()
@@ -555,12 +593,21 @@ class VersusAll:
                     # the writers format the block where it is (taxi2_format_rows_dev): no D2H of the
                     # values and no H2D of them again per file
                     futs.append(writers.submit(sink.write_text_dev, x0, x1, A, ready))
+                    mark("writers")
+            if prof is not None:
+                print(f"taxi2 task block {x0}-{x1}: " + " ".join(f"{k} {v * 1e3:.1f}" for k, v in pt.items()),
+                      file=sys.stderr)
             if isinstance(self.timings, dict):
                 self.timings["pairs_text_s"] = self.timings.get("pairs_text_s", 0.0) + perf_counter() - t0
             report(self.progress_handler, "distance.x.id", min(total, len(self.params.distances.metrics) * n * x1),
                    total)
 
-        pending = None
+        # blocks launched and not yet posted: the fills run PIPE_DEPTH blocks ahead of the text, so
+        # the fill stream never waits for the host to finish a block's text before its next launch
+        from collections import deque
+
+        pending = deque()
+        first = True
         for x0, x1, cnt in blocks:
             try:
                 blk = launch(x0, x1, cnt) if cnt else dict(x0=x0, x1=x1, k0=0, cnt=0)
@@ -568,15 +615,39 @@ class VersusAll:
                 if x0 == 0 and "walker strings need" in str(e):
                     return False
                 raise
-            if pending is not None:
-                post(pending)  # block k - 1's text while block k aligns
-            pending = blk
-            x0 = x1
-            if x0 < n and kept_b[0] > keep_limit:
+            pending.append(blk)
+            if first and (len(pending) == 2 or x1 >= n):
+                # while the first two blocks align: the text calls' pinned buffer, and the kept-string
+                # arena at its estimated size (both orientations' strings of every pair below the
+                # diagonal: 2 x 1.04 x the longer sequence of each pair; a short estimate only means
+                # a second chunk later)
+                first = False
+                tp = [perf_counter()]
+                eng._pinned_view(min(TEXT_CALL_BYTES, int(row_text_bound.sum())))
+                tp.append(perf_counter())
+                ls = np.sort(lens_h)
+                est = int(2.08 * float(np.dot(ls, np.arange(n, dtype=np.float64)))) + (1 << 20)
+                with torch.cuda.stream(tstream):
+                    arena[0] = torch.empty(max(1, min(est, keep_limit)), dtype=torch.uint8, device=dev)
+                    tp.append(perf_counter())
+                    # the first use of each torch kernel of post() loads its code object (~0.2 s in
+                    # all): a one-row dummy block here, while the GPU aligns
+                    z8, z32 = torch.zeros((1, 2, cap), dtype=torch.uint8, device=dev), torch.zeros(
+                        (1, 2), dtype=torch.int32, device=dev)
+                    pointers(0, 1, 0, 1, z8, z8, z32, torch.zeros(1, dtype=torch.int64, device=dev))
+                tp.append(perf_counter())
+                arena[1] = 0
+                kept.append(arena[0])
+                if prof is not None:
+                    print("taxi2 task setup: pinned %.1f arena %.1f warm %.1f ms" % tuple(
+                        1e3 * (tp[i + 1] - tp[i]) for i in range(3)), file=sys.stderr)
+            if len(pending) > PIPE_DEPTH:
+                post(pending.popleft())  # block k's text while blocks k + 1 .. k + PIPE_DEPTH align
+            if x1 < n and kept_b[0] > keep_limit:
                 # the kept strings outgrew their budget: the remaining rows align every ordered pair
                 # once (row blocks of the rect path), nothing kept
-                post(pending)
-                pending = None
+                while pending:
+                    post(pending.popleft())
                 rows_in()
                 tstream.synchronize()
                 stream.synchronize()
@@ -586,9 +657,9 @@ class VersusAll:
                         f.result()
                     writers.shutdown()
                     sink.abandon()
-                return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x0)
-        if pending is not None:
-            post(pending)
+                return self._rows_with_pairs(seqs, eng, st, D, cidx, clabels, scores, fh, x_start=x1)
+        while pending:
+            post(pending.popleft())
         rows_in()
         tstream.synchronize()
         stream.synchronize()
