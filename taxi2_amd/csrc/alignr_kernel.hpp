@@ -97,8 +97,13 @@ __device__ unsigned long long ar_prof[8];
 
 // Host-built segment: units u0 .. u0 + nb - 1 are (x0, x1, y = b0 + (u - u0)); pair (x_h, y) has
 // launch index p_h + (u - u0) (x1 = -1, p1 = -1: one pair per unit).
+// Swapped segment (sw = number of pairs > 0): the pairs (x0, y) of ONE row, y = b0 .. b0 + sw - 1 at
+// launch indices p0 .. p0 + sw - 1, which no second row shares (a launch with an odd number of rows
+// over these columns).  Unit du is the row sequence x0 against the two column sequences y = b0 +
+// 2 du and b0 + 2 du + 1 -- both halves busy, where a (x0, -1, y) unit idles one -- and is a chain of
+// its own (a chain keeps its column sequences).
 struct ArSeg {
-    int64_t x0, x1, b0, nb, p0, p1, u0, pad;
+    int64_t x0, x1, b0, nb, p0, p1, u0, sw;
 };
 
 struct ArRow {  // one unit of a chain: its row sequence and pairs
@@ -110,6 +115,7 @@ struct ArChain {
     const uint8_t* cseq[2];
     int nB[2], fy[2], ly[2], off[2];
     int n;
+    int swp;  // 1: the rows are the pairs' FIRST sequence (a swapped segment's unit)
 };
 struct ArWalk {
     int i, j, st, first, t, h, prio;
@@ -283,8 +289,9 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             if (r.p[h] >= 0) {
                 W_.t = t;
                 W_.h = h;
-                // rows = y, the pair's second sequence: orientation A (prio 0) is (y, x) = slot 1
-                W_.prio = out_mode == OUT_BOTH ? o : 1;
+                // rows = y, the pair's second sequence: orientation A (prio 0) is (y, x) = slot 1; in a
+                // swapped chain the rows are x and the pair's own orientation (x, y) is prio 0
+                W_.prio = out_mode == OUT_BOTH ? o : (chs[pb].swp ? 0 : 1);
                 W_.i = r.nA + 1;
                 W_.j = chs[pb].nB[h] + 1;
                 W_.st = AT_M;
@@ -315,11 +322,16 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
         int i = W_.i, j = W_.j, first = W_.first;
         uint32_t xa = W_.xa, yb = W_.yb;
         int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap, sc2 = W_.sc2, ncol = W_.ncol;
-        uint64_t wx = 0, wy = 0;  // string windows: bits 0-7 = the last column produced
+        uint64_t wx = 0, wy = 0;  // string windows (column, row sequence): bits 0-7 = the last column produced
         const int co_i = sc.io - sc.ie, co_e = sc.eo - sc.ee;
         const int bsh = h ? 8 : 0;
-        const int oslot = prio ^ 1;  // swp = 1: rows are the pair's second sequence
+        // rows are the pair's second sequence (orientation A = (y, x), prio 0, is slot 1), or its
+        // first in a swapped chain (prio 0 is then slot 0)
+        const int oslot = ch.swp ? prio : prio ^ 1;
         const size_t sbase = so.sx ? ((size_t)p * so.nslot + (oslot & (so.nslot - 1))) * (size_t)so.cap : 0;
+        // the string of the column sequence and of the row sequence: x = the pair's first
+        uint8_t* const dcol = ch.swp ? so.sy : so.sx;
+        uint8_t* const drow = ch.swp ? so.sx : so.sy;
         for (;;) {
             if (!__any(st < AT_DONE)) break;
             if (st < AT_DONE) {
@@ -333,15 +345,15 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 gap += (isX && bx < 4 && j - 1 >= fy && j <= ly) || (isY && by < 4 && i - 1 >= fx && i <= lx);
                 sc2 += (isM && !first) ? (xa == yb ? sc.ma : sc.mi) : 0;
                 const int ni = isY ? i : i - 1, nj = isX ? j : j - 1;
-                if (so.sx && !first) {  // this column of the alignment, right to left, (x, y) order
+                if (so.sx && !first) {  // this column of the alignment, right to left
                     const uint32_t rc = isY ? (uint32_t)'-' : xa, cc = isX ? (uint32_t)'-' : yb;
                     wx = (wx << 8) | cc;
                     wy = (wy << 8) | rc;
                     ++ncol;
                     if ((ncol & 7) == 0) {  // columns [E - ncol, E - ncol + 8) of the slot (E = nA + nB)
                         const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
-                        ar_store8(so.sx + o, wx);
-                        ar_store8(so.sy + o, wy);
+                        ar_store8(dcol + o, wx);
+                        ar_store8(drow + o, wy);
                     }
                 }
                 first = 0;
@@ -358,12 +370,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         if (so.sx && (ncol & 7)) {  // the columns since the last window store
                             const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
                             if (ncol >= 8) {  // the window's older bytes are already in place
-                                ar_store8(so.sx + o, wx);
-                                ar_store8(so.sy + o, wy);
+                                ar_store8(dcol + o, wx);
+                                ar_store8(drow + o, wy);
                             } else {
                                 for (int q = 0; q < ncol; ++q) {
-                                    so.sx[o + q] = (uint8_t)(wx >> (8 * q));
-                                    so.sy[o + q] = (uint8_t)(wy >> (8 * q));
+                                    dcol[o + q] = (uint8_t)(wx >> (8 * q));
+                                    drow[o + q] = (uint8_t)(wy >> (8 * q));
                                 }
                             }
                         }
@@ -455,6 +467,45 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         if (n > 0 && sg != s_seg) break;  // a chain keeps one segment's columns
                         s_seg = sg;
                         const ArSeg S = segs[sg];
+                        if (S.sw > 0) {  // swapped: row x0 against columns b0 + 2 du (+ 1), a chain of its own
+                            if (n > 0) break;
+                            const int64_t du = q - S.u0;
+                            const int4 mr = XS.meta[S.x0];
+                            const uint8_t* xr_ = XS.bytes + XS.offs[S.x0];
+                            int64_t ph[2];
+                            int4 mc[2];
+                            const uint8_t* cs_[2];
+                            bool live[2];
+#pragma unroll
+                            for (int hh = 0; hh < 2; ++hh) {
+                                const int64_t k = 2 * du + hh;
+                                ph[hh] = k < S.sw ? S.p0 + k : -1;
+                                live[hh] = ph[hh] >= 0;
+                                mc[hh] = live[hh] ? YS.meta[S.b0 + k] : make_int4(0, 0, 0, 0);
+                                cs_[hh] = live[hh] ? YS.bytes + YS.offs[S.b0 + k] : YS.bytes;
+                                if (live[hh] && (mc[hh].x == 0 || mr.x == 0)) {  // an empty side: no fill
+                                    empty_pair(ph[hh], xr_, mr.x, cs_[hh], mc[hh].x);
+                                    live[hh] = false;
+                                }
+                            }
+                            if (!live[0] && !live[1]) continue;
+                            ArChain& c = chs[cur];
+#pragma unroll
+                            for (int hh = 0; hh < 2; ++hh) {
+                                const int nb_ = live[hh] ? mc[hh].x : 0;
+                                c.cseq[hh] = cs_[hh];
+                                c.nB[hh] = nb_;
+                                c.fy[hh] = live[hh] ? mc[hh].y : 0;
+                                c.ly[hh] = live[hh] ? mc[hh].z : 0;
+                                c.off[hh] = nb_ > 0 ? (K - nb_ % K) % K : 0;
+                            }
+                            c.swp = 1;
+                            tab[cur][0] = ArRow{xr_, {live[0] ? ph[0] : -1, live[1] ? ph[1] : -1}, mr.x, mr.y, mr.z, 0};
+                            rows = mr.x;
+                            n = 1;
+                            ++q;
+                            break;
+                        }
                         const int64_t du = q - S.u0;
                         const int64_t b = S.b0 + du;
                         const int4 mb = YS.meta[b];
@@ -490,6 +541,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                                 c.ly[hh] = m.z;
                                 c.off[hh] = m.x > 0 ? (K - m.x % K) % K : 0;
                             }
+                            c.swp = 0;
                         }
                         tab[cur][n] = ArRow{yb_, {live[0] ? ph[0] : -1, live[1] ? ph[1] : -1}, mb.x, mb.y, mb.z, rows};
                         rows += mb.x;

@@ -647,7 +647,10 @@ struct RowIv {
 // stays one segment for as long as the pairing keeps it.  Rows enter and leave the active set only
 // at their interval ends, and in the triangle they enter in x order at the end of the order, so the
 // pairing of earlier rows persists: few segments, few single units.
-void build_segments(std::vector<RowIv>& rows, std::vector<ArSeg>& segs, int64_t& units) {
+// swap_ok: a row whose pairs no second row shares (an odd number of rows over those columns) becomes a
+// swapped segment -- units of two of its pairs sharing the row's sequence -- instead of units that
+// idle one half (needs the aligner shape to hold the column set's sequences as columns too)
+void build_segments(std::vector<RowIv>& rows, std::vector<ArSeg>& segs, int64_t& units, bool swap_ok) {
     segs.clear();
     units = 0;
     std::sort(rows.begin(), rows.end(), [](const RowIv& a, const RowIv& b) { return a.x < b.x; });
@@ -682,8 +685,12 @@ void build_segments(std::vector<RowIv>& rows, std::vector<ArSeg>& segs, int64_t&
         }
         sg.b0 = o.b0;
         sg.nb = nb;
+        if (o.r1 < 0 && swap_ok && nb > 1) {  // one row alone: pairs of its own columns per unit
+            sg.sw = nb;
+            sg.nb = (nb + 1) / 2;
+        }
         sg.u0 = units;
-        units += nb;
+        units += sg.nb;
         segs.push_back(sg);
     };
     for (size_t e = 0; e + 1 < pts.size(); ++e) {
@@ -748,7 +755,11 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     }
     std::vector<ArSeg> segs;
     int64_t units = 0;
-    build_segments(rows, segs, units);
+    // swapped units (TAXI2_AR_SWAP=1) put the column set's sequences on the columns: the shape must
+    // hold them.  Off by default: each swapped unit is a chain of its own, whose walks (latency-bound,
+    // four per chain instead of up to 32) outlast its fill, so the fill waves wait at the chain's end
+    // barrier -- 94.6 vs 93.6 ms per config-3 launch although the units drop by 4.4 %
+    build_segments(rows, segs, units, 64 * v.K * v.W >= Y.max_len && getenv("TAXI2_AR_SWAP"));
     if (segs.empty()) return 0;
     const int f = ctx->seg_flip;
     ctx->seg_flip ^= 1;
@@ -779,10 +790,12 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // up to 120 GB of the 288 GB HBM, at most 45 % of the device's memory (TAXI2_AT_TRACE_GB overrides)
     double budget_gb = std::min(120.0, 0.45 * (double)ctx->total_mem / 1e9);
     if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
-    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * std::max(1, Y.max_len)) - 64, 4 * v.K, v.W); };
+    // chain rows: row sequences of the row set, or (swapped units) one of the column set's
+    const int rmax = std::max(1, std::max(X.max_len, Y.max_len));
+    auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * rmax) - 64, 4 * v.K, v.W); };
     while (eff > 1 && (double)grid * 2.0 * (double)buf_bytes(eff) > budget_gb * 1e9) eff = eff / 2;
     chunk = (int)eff;
-    const int cap_rows = (int)eff * std::max(1, Y.max_len);
+    const int cap_rows = (int)eff * rmax;
     const size_t bb = buf_bytes(eff);
     // trace band: 2.5 sqrt(L) (80 at 1 000 bp: the widest measured excursion is 67; escapes requeue
     // exactly).  Narrower bands cut the trace writes (337 KB per pair at 80, 275 at 64) but the
@@ -828,7 +841,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
         HIP_TRY(ctx, hipStreamSynchronize(st));
         int64_t single = 0;  // units of one pair (x1 = -1): the other half of every lane idles
         for (const auto& sg : segs)
-            if (sg.x1 < 0) single += sg.nb;
+            if (sg.x1 < 0) single += sg.sw ? (sg.sw & 1) : sg.nb;
         fprintf(stderr, "taxi2 band: k_alignr<%d,%d> band %d: %llu of %lld pairs took the full-trace pass (%zu segments, "
                 "%lld units, %lld single-pair units = %.2f %%, grid %lld, chunk %d)\n", v.K, v.W, band, q,
                 (long long)ps.count, segs.size(), (long long)units, (long long)single,

@@ -176,3 +176,44 @@ def test_alignr_off_matches_default(engine, oracle_c):
     r_off = _with_env({"TAXI2_NO_ALIGNR": "1"}, lambda: engine.rect_pairs(st, st, 3, 9, METRICS, sc))
     assert np.array_equal(r_on.view(np.int64), r_off.view(np.int64))
     st.free()
+
+
+def test_alignr_swapped_units_match_default(engine):
+    """TAXI2_AR_SWAP=1 (k_alignr pairs a launch's unshared row with itself: units of two of its pairs
+    on the row's sequence, walked in the other orientation) gives the default's scores, metrics and
+    aligned strings bit for bit: whole triangles (every odd column count leaves a row alone), a
+    mid-row launch, a rectangle (one orientation), and both orientations' strings."""
+    from taxi2_amd._native import tri_pairs
+
+    seqs = _tie_heavy(24, 1000, 0x6B) + ["ACGT" * 200, "A", "", "N" * 40]
+    st = engine.upload(seqs, align=True)
+    a, b = tri_pairs(len(seqs))
+    sc = SCORE_SETS["default"]
+    swap = {"TAXI2_AR_SWAP": "1"}
+    for k0, cnt in ((0, len(a)), (7, len(a) - 19)):
+        got, gsc = engine.all_pairs(st, k0, cnt, METRICS, sc, with_scores=True)
+        sw, ssc = _with_env(swap, lambda: engine.all_pairs(st, k0, cnt, METRICS, sc, with_scores=True))
+        assert np.array_equal(got.view(np.int64), sw.view(np.int64)) and np.array_equal(gsc, ssc)
+    r_on = engine.rect_pairs(st, st, 3, 11, METRICS, sc)
+    r_sw = _with_env(swap, lambda: engine.rect_pairs(st, st, 3, 11, METRICS, sc))
+    assert np.array_equal(r_on.view(np.int64), r_sw.view(np.int64))
+    import torch
+
+    cnt = len(a)
+    cap = 2 * max(len(s) for s in seqs) + 1
+
+    def strings():
+        d = torch.empty((cnt, 2, len(METRICS)), dtype=torch.float64, device="cuda")
+        sx = torch.zeros((cnt, 2, cap), dtype=torch.uint8, device="cuda")
+        sy = torch.zeros((cnt, 2, cap), dtype=torch.uint8, device="cuda")
+        sl = torch.zeros((cnt, 2), dtype=torch.int32, device="cuda")
+        engine.tri_strings_dev(st, 0, cnt, METRICS, d.data_ptr(), cap, sx.data_ptr(), sy.data_ptr(), sl.data_ptr(),
+                               sc)
+        torch.cuda.synchronize()
+        return [t.cpu().numpy() for t in (d, sx, sy, sl)]
+
+    s_def = strings()
+    s_sw = _with_env(swap, strings)
+    for u, v in zip(s_def, s_sw):
+        assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
+    st.free()
