@@ -86,6 +86,19 @@ __device__ __forceinline__ uint32_t load4(const uint8_t* w, int p) {
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(p & 3));
 }
 
+// Maximum of a non-negative int over the wave, uniform result: DPP butterflies within each row of 16
+// lanes, then the row broadcasts (lane 63 ends with the wave's maximum) -- register-to-register
+// steps only, where a bisection on ballots took nine dependent compare / ballot rounds.
+__device__ __forceinline__ int wave_max_nonneg(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1, 0, 3, 2]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2, 3, 0, 1]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));   // row_bcast15 (rows 1, 3)
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));   // row_bcast31 (rows 2, 3)
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // zlib's longest_match for the query at `strstart` (see the header comment); uniform in, uniform out
 __device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint16_t* spos, int i0, uint32_t h,
                                                   int strstart, int lookahead, int prev_length, int& match_start,
@@ -129,16 +142,11 @@ __device__ __forceinline__ int coop_longest_match(const uint8_t* win, const uint
             if (len < zl::MIN_MATCH) len = 0;
         }
         const uint64_t stop = __ballot(len >= nice && len > prev_length);
-        // lanes up to the stop, then the longest (earliest on ties) by bisection on ballots: no
-        // cross-lane data movement but one readlane
+        // lanes up to the stop, then the longest (earliest on ties): the wave maximum by DPP, the
+        // earliest lane holding it by one ballot
         const uint64_t upto = stop ? (stop ^ (stop - 1)) : ~0ull;
         const int lv = (upto >> lane) & 1ull ? len : 0;
-        int rlen = 0;
-#pragma unroll
-        for (int bit = 8; bit >= 0; --bit) {
-            const int t = rlen | (1 << bit);
-            if (__ballot(lv >= t)) rlen = t;
-        }
+        const int rlen = wave_max_nonneg(lv);
         if (rlen > best) {
             best = rlen;
             best_pos = __builtin_amdgcn_readlane(cand, __builtin_ctzll(__ballot(lv == rlen)));
