@@ -1210,6 +1210,15 @@ struct Tracer {
 };
 
 // first_only: the one-thread path compresses each descriptor's first part alone (launch_zlen2)
+// Workgroups of `lds` bytes the 160 KiB of a gfx950 CU's LDS hold: the LDS is allocated in 256-byte
+// granules, which hipOccupancyMaxActiveBlocksPerMultiprocessor does not round to (it answered 14
+// for 11 568-byte workgroups that fit 13 at a time).  A persistent grid sized for one workgroup too
+// many per CU runs its extra workgroups as a second round behind the whole first one.
+static int lds_fit_per_cu(size_t lds) {
+    const size_t g = (lds + 255) / 256 * 256;
+    return g ? (int)((size_t)160 * 1024 / g) : 1 << 20;
+}
+
 int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, int max_n, bool latin1,
                 hipStream_t st = nullptr, int likely_n = 0, int first_only = 0);
 
@@ -1279,6 +1288,7 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
             HIP_TRY(ctx, hipFuncSetAttribute((const void*)k_zlen_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int per_cu = 0;
         HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave, 64, lds));
+        per_cu = std::min(per_cu, lds_fit_per_cu(lds));
         const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
         hipLaunchKernelGGL(k_zlen_wave, dim3((unsigned)grid), dim3(64), lds, st, d_st, n, nmax, d_out, redo);
         HIP_TRY(ctx, hipGetLastError());
@@ -1334,6 +1344,7 @@ int launch_zlen2(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out,
             HIP_TRY(ctx, hipFuncSetAttribute((const void*)k_zlen_wave2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int per_cu = 0;
         HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave2, 64, lds));
+        per_cu = std::min(per_cu, lds_fit_per_cu(lds));
         const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
         hipLaunchKernelGGL(k_zlen_wave2, dim3((unsigned)grid), dim3(64), lds, st, d_st, n, nmax, d_out, d_out_a, redo);
         HIP_TRY(ctx, hipGetLastError());
@@ -1383,8 +1394,25 @@ int ncd_from_slots(taxi2_ctx* ctx, const SlotSrc& ss, const DevSet& X, const Dev
     HIP_TRY(ctx, hipGetLastError());
     // each launch first sized for the likely length (an aligned string is rarely much longer than
     // the longer sequence: +1/16 + 32 bytes), a second pass over the streams that did not fit
+    // The fused pass's occupancy is set by its LDS (~5 B per stream byte): among first-pass sizes
+    // from the longer sequence + 1/32 + 16 to + 1/16 + 32 bytes per string, the largest that keeps
+    // the most waves per CU (at 1 000 bp: 14 instead of 13 waves, all metrics 5.1e5 -> 6.8e5 pairs/s;
+    // the few longer alignments take the redo pass).  TAXI2_NCD_MARGIN fixes the margin instead.
     const int lmax = std::max(X.max_len, Y.max_len);
-    const int likely = std::min(max_str / 2, lmax + lmax / 16 + 32);
+    int likely = lmax + lmax / 16 + 32;
+    if (const char* e = getenv("TAXI2_NCD_MARGIN")) {
+        likely = lmax + std::max(0, atoi(e));
+    } else {
+        int best_w = -1;
+        for (int L = lmax + lmax / 32 + 16; L <= lmax + lmax / 16 + 32; L += 2) {
+            const int w = lds_fit_per_cu(zlw::lds_bytes(std::max(2 * L, 4)));
+            if (w >= best_w) {  // ties: the larger size (fewer redos)
+                best_w = w;
+                likely = L;
+            }
+        }
+    }
+    likely = std::min(max_str / 2, likely);
     if (launch_zlen2(ctx, d_fused, nf, d_cab, d_ca, max_str, latin1, st, 2 * likely)) return -1;
     if (launch_zlen(ctx, d_single, ns, d_cs, max_str / 2, latin1, st, likely)) return -1;
     hipLaunchKernelGGL(k_ncd_slot_finish, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, d_cab, d_ca, d_cs, n,
