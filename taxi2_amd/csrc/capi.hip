@@ -778,6 +778,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // ---- resident grid, chunk (units per cursor step) and trace buffers, as launch_alignt_pairs
     int per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 64 * (v.W + 1), 0));
+    if (const char* e = getenv("TAXI2_AR_PERCU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));  // scaling probe
     const int64_t resident =
         (int64_t)std::max(1, ctx->num_cus - std::max(0, std::min(ctx->reserve_cus, ctx->num_cus - 1))) *
         std::max(1, per_cu);
