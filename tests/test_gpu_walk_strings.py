@@ -122,14 +122,19 @@ def test_task_pairs_from_walks_equal_round2_path(tmp_path, engine, variant, stre
         assert (tmp_path / "walk" / f).read_bytes() == (tmp_path / "r2" / f).read_bytes(), f
 
 
-@pytest.mark.parametrize("mode", ["one_block", "small_blocks", "switch"])
+@pytest.mark.parametrize("mode", ["one_block", "small_blocks", "switch", "split_text"])
 @pytest.mark.parametrize("variant", ["default", "generic"])
-def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant):
+def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant, monkeypatch):
     """Dense aligned_pairs.txt from ONE fill per unordered pair (taxi2_tri_strings_dev: both
     orientations walked, the (b, a) strings kept in HBM until row b, text through per-pair pointers)
     == the rect path that aligns every ordered pair once (TAXI2_PAIRS_RECT=1), every output file
-    byte for byte: one block, many small blocks, and a keep budget that runs out mid-way (the
-    remaining rows switch to the rect path)."""
+    byte for byte: one block, many small blocks (the pipeline two blocks deep, the writers formatting
+    each block from HBM), a keep budget that runs out mid-way (the remaining rows switch to the rect
+    path), and a block's text split over many formatter calls (a one-row bound per call)."""
+    from taxi2_amd.tasks import versus_all as VA
+
+    if mode == "split_text":
+        monkeypatch.setattr(VA, "TEXT_CALL_BYTES", 1)
     from taxi2_amd.align import Scores
     from taxi2_amd.sequences import Sequence, Sequences
     from taxi2_amd.tasks import VersusAll
