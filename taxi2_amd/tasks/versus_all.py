@@ -384,9 +384,10 @@ class VersusAll:
             D[x0:x1, :, cidx] = stage[0][: x1 - x0].numpy()
             stage[2] = None
 
-        # Two streams: block k + 1 aligns on `stream` while block k's post-processing -- compaction of
-        # its kept (b, a) strings, the text kernel, the text's D2H and file write, the staging of its
-        # complete rows -- runs on `tstream` after block k's event.  Tensors of a block are
+        # Two streams: blocks k + 1 .. k + PIPE_DEPTH align on `stream` while block k's post-processing
+        # -- compaction of its kept (b, a) strings, the text kernel (straight into pinned host
+        # memory) and the file write, the staging of its complete rows -- runs on `tstream` after
+        # block k's event.  Tensors of a block are
         # record_stream()'d on tstream before they are dropped, so the caching allocator never hands
         # their memory to the next block while the text still reads it.
         # high priority: a queue of its own beside the fill's (HIP multiplexes streams onto
