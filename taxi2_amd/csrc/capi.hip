@@ -1346,6 +1346,7 @@ int launch_zlen2(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out,
         int per_cu = 0;
         HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave2, 64, lds));
         per_cu = std::min(per_cu, lds_fit_per_cu(lds));
+        if (const char* e = getenv("TAXI2_ZLEN_PERCU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));  // scaling probe
         const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
         hipLaunchKernelGGL(k_zlen_wave2, dim3((unsigned)grid), dim3(64), lds, st, d_st, n, nmax, d_out, d_out_a, redo);
         HIP_TRY(ctx, hipGetLastError());
