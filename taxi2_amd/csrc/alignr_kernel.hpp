@@ -32,7 +32,13 @@
 
 namespace taxi2 {
 
-constexpr int AR_BLK = 16;  // steps between the fill waves' progress checks / publications
+// steps between the fill waves' progress checks / publications (a divisor of INTERVAL). Config-3
+// launch time, one box: 8 -> 96.7 ms, 16 -> 93.8, 32 -> 92.5; another box: 16 -> 95.3, 32 -> 94.5,
+// 64 -> 95.2 (profiles/r5/ar_blk/)
+#ifndef TAXI2_AR_BLK
+#define TAXI2_AR_BLK 32
+#endif
+constexpr int AR_BLK = TAXI2_AR_BLK;
 // Rows buffered between the fill waves (the ring) and how far wave 0 may run ahead of wave 1: wave 0
 // rewrites a ring slot AR_RING - 63 steps after wave 1 read it, and the row record of row r
 // (XR = 512 slots, written up to 64 rows ahead) AR_XR - 64 - 63 rows after wave 1's oldest use.
