@@ -47,6 +47,11 @@ constexpr int AR_BLK = TAXI2_AR_BLK;
 #endif
 constexpr int AR_RING = TAXI2_AR_RING;
 constexpr int AR_AHEAD = (AR_RING - 63) < (512 - 64 - 63 - AR_BLK) ? (AR_RING - 63) : (512 - 64 - 63 - AR_BLK);
+// Liveness of the two fill waves' pacing (the step loop's waits): wave 1 finishing block k needs
+// wave 0 through step (k + 1) AR_BLK + 63, published at the block end after it; wave 0 may start that
+// block only while it is at most AR_AHEAD steps ahead of wave 1's published k AR_BLK.  A ring of 128
+// (AR_AHEAD 65 < 96 at AR_BLK 32) deadlocks on the GPU.
+static_assert(AR_AHEAD >= AR_BLK * (1 + (63 + AR_BLK - 1) / AR_BLK), "fill waves would deadlock");
 #ifndef TAXI2_AR_UNITS
 #define TAXI2_AR_UNITS 8
 #endif
