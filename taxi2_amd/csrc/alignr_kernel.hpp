@@ -42,8 +42,10 @@ constexpr int AR_BLK = TAXI2_AR_BLK;
 // Rows buffered between the fill waves (the ring) and how far wave 0 may run ahead of wave 1: wave 0
 // rewrites a ring slot AR_RING - 63 steps after wave 1 read it, and the row record of row r
 // (XR = 512 slots, written up to 64 rows ahead) AR_XR - 64 - 63 rows after wave 1's oldest use.
+// Ring 256 -> 512 (4 KB of LDS per workgroup, AR_AHEAD 193 -> 353): 92.9 -> 92.3 ms per config-3
+// launch, same-box A/B x3 (profiles/r5/ar_ring/).
 #ifndef TAXI2_AR_RING
-#define TAXI2_AR_RING 256
+#define TAXI2_AR_RING 512
 #endif
 constexpr int AR_RING = TAXI2_AR_RING;
 constexpr int AR_AHEAD = (AR_RING - 63) < (512 - 64 - 63 - AR_BLK) ? (AR_RING - 63) : (512 - 64 - 63 - AR_BLK);
