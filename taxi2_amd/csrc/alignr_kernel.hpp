@@ -34,9 +34,10 @@ namespace taxi2 {
 
 // steps between the fill waves' progress checks / publications (a divisor of INTERVAL). Config-3
 // launch time, one box: 8 -> 96.7 ms, 16 -> 93.8, 32 -> 92.5; another box: 16 -> 95.3, 32 -> 94.5,
-// 64 -> 95.2 (profiles/r5/ar_blk/)
+// 64 -> 95.2 (ring 256, profiles/r5/ar_blk/); with the 512-row ring, 32 -> 91.7 and 64 -> 91.2 ms, same-box
+// A/B x3 (profiles/r5/ar_blk/ring512_*)
 #ifndef TAXI2_AR_BLK
-#define TAXI2_AR_BLK 32
+#define TAXI2_AR_BLK 64
 #endif
 constexpr int AR_BLK = TAXI2_AR_BLK;
 // Rows buffered between the fill waves (the ring) and how far wave 0 may run ahead of wave 1: wave 0
