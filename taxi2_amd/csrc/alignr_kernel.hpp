@@ -58,7 +58,15 @@ static_assert(AR_AHEAD >= AR_BLK * (1 + (63 + AR_BLK - 1) / AR_BLK), "fill waves
 #ifndef TAXI2_AR_UNITS
 #define TAXI2_AR_UNITS 8
 #endif
-constexpr int AR_UNITS = TAXI2_AR_UNITS;  // units (row sequences, up to two pairs each) per chain
+constexpr int AR_UNITS = TAXI2_AR_UNITS;
+// Bound of one pacing wait (polls of s_sleep 1, ~64 clocks each: ~0.5 s at 2.4 GHz, against ~1e3
+// polls for the longest wait measured).  Pacing is deadlock-free by the static_assert above; the
+// bound turns a pacing or launch-shape error into a failed launch (pace_err -> taxi2_last_error)
+// instead of a hung device.
+#ifndef TAXI2_AR_SPIN_CAP
+#define TAXI2_AR_SPIN_CAP (1 << 24)
+#endif
+constexpr int AR_SPIN_CAP = TAXI2_AR_SPIN_CAP;  // units (row sequences, up to two pairs each) per chain
 // Trace layout.  AR_TS = 0 (default): [step][lane][4K bytes], a lane's K columns contiguous.
 // AR_TS >= 1: the columns are cut into pieces of ar_pw(K) columns (16 bytes for K % 4 == 0), and
 // piece q of all lanes over AR_TS consecutive steps is one run, [step / AR_TS][piece][lane][step %
@@ -75,12 +83,6 @@ constexpr int AR_TS = TAXI2_AR_TS;
 #define TAXI2_AR_SKIP 0
 #endif
 constexpr bool AR_SKIP = TAXI2_AR_SKIP != 0;
-// prefetch of the next step's table offset (see the fill's step loop): off -- the extra live register
-// takes the kernel to 130 VGPRs, i.e. 3 waves per SIMD instead of 4 (tools/isa_alignr.hip)
-#ifndef TAXI2_AR_PREC
-#define TAXI2_AR_PREC 0
-#endif
-constexpr bool AR_PREC = TAXI2_AR_PREC != 0;
 __host__ __device__ constexpr int ar_pw(int K) { return K % 4 == 0 ? 4 : 2; }
 // byte offset of (step, lane, column k) in a chain's trace buffer (NT lanes)
 // (AR_TS = 0: the plain [step][lane][4K bytes] layout, for comparison)
@@ -105,7 +107,7 @@ __host__ __device__ constexpr int ar_trace_rows(int rows) { return rows + 64 + A
 // tables, first barrier), [3] walker walking, [4] fill waits for the other fill wave, [5] walker
 // chain-end barrier, [6] chains
 #ifdef AR_PROF
-__device__ unsigned long long ar_prof[8];
+__device__ unsigned long long ar_prof[12];  // + [7] fill-wave polls, [8] walker loop iterations, [9] fill steps
 #define AR_NOW() __builtin_amdgcn_s_memtime()
 #endif
 
@@ -224,7 +226,8 @@ __global__ void __launch_bounds__(64 * (W + 1), OCC) __attribute__((amdgpu_num_v
 k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64_t total, int64_t npairs,
          MetricSpec ms, int chunk_req, int out_mode, double* __restrict__ out, int32_t* __restrict__ sout,
          uint8_t* __restrict__ trace, int64_t buf_bytes, int cap_rows, unsigned long long* __restrict__ next,
-         int band, int64_t* __restrict__ esc_list, unsigned long long* __restrict__ esc_n, StrOut so) {
+         int band, int64_t* __restrict__ esc_list, unsigned long long* __restrict__ esc_n, StrOut so,
+         unsigned int* __restrict__ pace_err) {
     static_assert(K % 2 == 0 && K <= 8 && W <= 2, "row-shared shapes: K <= 8 columns per lane, one or two fill waves");
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
@@ -247,6 +250,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     __shared__ int s_prog[2];  // steps completed by each fill wave in the current chain
     __shared__ ArWalk wks[NW];
     __shared__ int escf[2][AR_UNITS][2];
+    __shared__ uint8_t wct[256];  // the walker's base codes: a2_wcode of every byte
 
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -262,6 +266,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
         s_seg = 0;
     }
     int cur = 0, prev_n = 0;
+    for (int c = tid; c < 256; c += 64 * (W + 1)) wct[c] = (uint8_t)a2_wcode((uint32_t)c);  // (first barrier below)
+    // set when a fill wave's wait for its partner exceeds AR_SPIN_CAP polls: the wave stops waiting
+    // for the rest of the launch and the host reports the launch as failed (pace_err)
+    bool stalled = false;
 
     // outputs of a pair with an empty side (no fill): metrics of no columns, the end-gap score,
     // the other sequence against gaps as its alignment (both orientation slots alike)
@@ -314,137 +322,181 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
         }
     };
 
-    // branch-free best-open walker (alignt2_kernel.hpp walk_run_raw), per-half column sequence and
-    // shift; walks the chain in buffer pb to the end.  Aligned strings (so.sx): each walk keeps the
-    // last 8 columns it produced in a 64-bit window per string and stores the window (8 bytes,
-    // unaligned) every 8 columns and at the walk's end -- not a byte store per column and string
+    // The walker (one lane per walk, up to NW = 4 AR_UNITS walks of the previous chain): the best-open
+    // traceback of alignt2_kernel.hpp walk_run_raw, specialised to the default scores and written for
+    // few VALU per step -- its instructions take issue slots from the fill waves on the same SIMD
+    // (round 6: the walker was 11.6 % of the kernel's VALU, 137 per step; with no walker at all the
+    // launch ran 9.7 % faster, profiles/r6/).  Per step of every walk:
+    //  * the cell (i, j) in state st is accounted from its bytes' codes (an LDS table of a2_wcode);
+    //  * the path score is checked through its decomposition under the default scores: a path with
+    //    nm M columns of which nmatch match and nio internal gap opens scores 2 nmatch + nm - 7 nio
+    //    - (nA + nB) (M: +1 / -1; every gap column -1; an internal open -7 more, an end open nothing),
+    //    which must equal the fill's optimum (fin - nA - nB in drift coordinates);
+    //  * the predecessor's sequence bytes and trace word are loaded through 32-bit offsets from the
+    //    uniform sequence-set and trace bases (the row bytes are never masked: a walk on row 0 or
+    //    column 0 moves in Iy / Ix, whose accounting reads only the other byte);
+    //  * a walk reaching (0, 0) parks in AT_FIN with its counters; every parked walk is checked and
+    //    written after the loop in one pass (the f64 metric epilogue once per wave, not once per
+    //    finishing lane).
+    // Aligned strings (so.sx): each walk keeps the last 8 columns it produced in a 64-bit window per
+    // string and stores the window (8 bytes, unaligned) every 8 columns and at the walk's end.
+    static_assert(AR_TS == 0, "the walker addresses the plain [step][lane][4K] trace layout");
+    constexpr int AT_FIN = AT_ESC + 1;
+#ifdef AR_PROF
+    unsigned long long wit = 0;  // walker loop iterations
+#endif
     auto walk = [&](int pb) {
+#ifdef AR_NOWALK
+        return;
+#endif
         ArWalk& W_ = wks[lane < NW ? lane : 0];
         int st = lane < NW ? W_.st : AT_DONE;
         if (!__any(st != AT_DONE)) return;
         const int t = W_.t, h = W_.h, prio = W_.prio;
         const ArRow& r = tab[pb][t];
         const ArChain& ch = chs[pb];
-        const int nA_ = r.nA, nB_ = ch.nB[h], off = ch.off[h];
-        const int fx = r.fx, lx = r.lx, fy = ch.fy[h], ly = ch.ly[h], r0 = r.r0;
+        // rows are the pair's second sequence (orientation A = (y, x), prio 0, is slot 1), or its
+        // first in a swapped chain (prio 0 is then slot 0)
+        const bool swp = __builtin_amdgcn_readfirstlane(ch.swp) != 0;
+        const uint8_t* const rbase = swp ? XS.bytes : YS.bytes;  // the row / column sequence sets
+        const uint8_t* const cbase = swp ? YS.bytes : XS.bytes;
+        const int nA_ = r.nA, nB_ = ch.nB[h], off = ch.off[h], r0 = r.r0;
+        const uint32_t roff = (uint32_t)(r.rseq - rbase), coff = (uint32_t)(ch.cseq[h] - cbase);
+        // internal-gap column ranges of the p-gaps count: fx + 1 <= i <= lx, fy + 1 <= j <= ly
+        const int fx1 = r.fx + 1, fy1 = ch.fy[h] + 1;
+        const uint32_t giw = (uint32_t)max(r.lx - r.fx, 0), gjw = (uint32_t)max(ch.ly[h] - ch.fy[h], 0);
         const int64_t p = r.p[h];
         const int bdl = min(0, nB_ - nA_) - band;
         const uint32_t bwd = (uint32_t)(abs(nB_ - nA_) + 2 * band);
-        const uint8_t* rs = r.rseq;
-        const uint8_t* cs = ch.cseq[h];
-        const uint8_t* trb = bufs + (size_t)pb * (size_t)buf_bytes;
-        int i = W_.i, j = W_.j, first = W_.first;
-        uint32_t xa = W_.xa, yb = W_.yb;
-        int valid = W_.valid, ts = W_.ts, tv = W_.tv, gap = W_.gap, sc2 = W_.sc2, ncol = W_.ncol;
-        uint64_t wx = 0, wy = 0;  // string windows (column, row sequence): bits 0-7 = the last column produced
-        const int co_i = sc.io - sc.ie, co_e = sc.eo - sc.ee;
-        const int bsh = h ? 8 : 0;
-        // rows are the pair's second sequence (orientation A = (y, x), prio 0, is slot 1), or its
-        // first in a swapped chain (prio 0 is then slot 0)
-        const int oslot = ch.swp ? prio : prio ^ 1;
+        const uint8_t* const trb = bufs + (size_t)pb * (size_t)buf_bytes;
+        // the high half's trace bytes carry the low half's borrow (a2_raw_de): added back per 16 bits
+        const uint32_t hmask = h ? 0x00800080u : 0u;
+        const uint32_t bsh = h ? 8u : 0u;
+        const int oslot = swp ? prio : prio ^ 1;
         const size_t sbase = so.sx ? ((size_t)p * so.nslot + (oslot & (so.nslot - 1))) * (size_t)so.cap : 0;
-        // the string of the column sequence and of the row sequence: x = the pair's first
-        uint8_t* const dcol = ch.swp ? so.sy : so.sx;
-        uint8_t* const drow = ch.swp ? so.sx : so.sy;
+        uint8_t* const dcol = swp ? so.sy : so.sx;  // the string of the column sequence and of the row one
+        uint8_t* const drow = swp ? so.sx : so.sy;
+        int i = nA_ + 1, j = nB_ + 1;  // the virtual end cell, in M: its first move picks the end state
+        uint32_t xa = 0u, yb = 0u;
+        int valid = 0, ts = 0, tv = 0, gap = 0, nmc = 0, nmatch = 0, nio = 0, ncol = 0;
+        uint64_t wx = 0, wy = 0;  // string windows (column, row sequence): bits 0-7 = the last column produced
+        bool first = true;        // the virtual end cell (uniform: every walk starts together)
+        // Every lane runs the body every step (no per-lane region: its merge copies cost ~20 VALU a
+        // step); a walk that ends parks its outcome in its LDS record and keeps stepping harmlessly
+        // (clamped loads, no stores) until the wave's last walk ends.
+        bool alive = lane < NW && st < AT_DONE;
         for (;;) {
-            if (!__any(st < AT_DONE)) break;
-            if (st < AT_DONE) {
-                const bool isM = st == AT_M, isX = st == AT_IX, isY = st == AT_IY;
-                const uint32_t bx = a2_wcode(xa), by = a2_wcode(yb);
-                const uint32_t dd = bx ^ by;
-                const bool cnt = isM && !first && (bx | by) < 4u;
-                valid += cnt;
-                ts += cnt && dd == 3u;
-                tv += cnt && (dd == 1u || dd == 2u);
-                gap += (isX && bx < 4 && j - 1 >= fy && j <= ly) || (isY && by < 4 && i - 1 >= fx && i <= lx);
-                sc2 += (isM && !first) ? (xa == yb ? sc.ma : sc.mi) : 0;
-                const int ni = isY ? i : i - 1, nj = isX ? j : j - 1;
-                if (so.sx && !first) {  // this column of the alignment, right to left
-                    const uint32_t rc = isY ? (uint32_t)'-' : xa, cc = isX ? (uint32_t)'-' : yb;
-                    wx = (wx << 8) | cc;
-                    wy = (wy << 8) | rc;
-                    ++ncol;
-                    if ((ncol & 7) == 0) {  // columns [E - ncol, E - ncol + 8) of the slot (E = nA + nB)
-                        const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
-                        ar_store8(dcol + o, wx);
-                        ar_store8(drow + o, wy);
-                    }
-                }
-                first = 0;
-                if (ni == 0 && nj == 0) {
-                    if (!isM) sc2 += sc.eo;
-                    if (sc2 != fin[pb][t][h] + (nA_ + nB_) * dz) {
-                        st = AT_ESC;
-                    } else {
-                        double* o = out_mode == OUT_BOTH ? out + (p * 2 + oslot) * nm : out + p * nm;
-                        for (int m = 0; m < nm; ++m)
-                            o[m] = metric_value(ms.code[m], (uint32_t)valid, (uint32_t)ts, (uint32_t)tv, (uint32_t)gap);
-                        if (sout && (out_mode != OUT_BOTH || oslot == 0)) sout[p] = fin[pb][t][h] + (nA_ + nB_) * dz;
-                        if (so.slen) so.slen[p * so.nslot + (oslot & (so.nslot - 1))] = ncol;
-                        if (so.sx && (ncol & 7)) {  // the columns since the last window store
-                            const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
-                            if (ncol >= 8) {  // the window's older bytes are already in place
-                                ar_store8(dcol + o, wx);
-                                ar_store8(drow + o, wy);
-                            } else {
-                                for (int q = 0; q < ncol; ++q) {
-                                    dcol[o + q] = (uint8_t)(wx >> (8 * q));
-                                    drow[o + q] = (uint8_t)(wy >> (8 * q));
-                                }
-                            }
-                        }
-                        st = AT_DONE;
-                    }
-                } else {
-                    const bool in = ni >= 1 && nj >= 1;
-                    const bool esc = in && band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
-                    const int cj = max(nj, 1) - 1 + off, ci = max(ni, 1) - 1;  // virtual column of (ni, nj) - 1
-                    const uint32_t tl = (uint32_t)cj / K, k = (uint32_t)cj - tl * K;
-                    const uint32_t toff = ar_trace_off<K, NT>((uint32_t)(r0 + ci) + (tl & 63u), tl, k);
-                    const uint32_t xa_ = a2_load_byte(rs + ci), yb_ = a2_load_byte(cs + max(nj, 1) - 1);
-                    const uint32_t nb = a2_load_trace32(trb + toff);
-                    xa = ni >= 1 ? xa_ : 0u;
-                    yb = nj >= 1 ? yb_ : 0u;
-                    const int d1v = (int)(int8_t)(uint8_t)((nb >> bsh) + (h ? ((nb >> 7) & 1u) : 0u));
-                    const int d2v = (int)(int8_t)(uint8_t)((nb >> (16 + bsh)) + (h ? ((nb >> 23) & 1u) : 0u));
-                    const int co = j == nB_ ? co_e : co_i, oy = i == nA_ ? co_e : co_i;
-                    const int vM = d1v + (isX ? co : 0);
-                    const int vY = d1v - d2v + (isX ? co : isY ? -oy : 0);
-                    const int vm = max(max(vM, vY), 0);
-                    int nst = vM == vm ? AT_M : prio ? (vY == vm ? AT_IY : AT_IX) : (vm == 0 ? AT_IX : AT_IY);
-                    nst = ni == 0 ? AT_IY : nj == 0 ? AT_IX : nst;
-                    const bool ext = isX ? nst == AT_IX : nst == AT_IY;
-                    const bool en = isX ? (j == nB_ || j == 0) : (i == nA_ || i == 0);
-                    sc2 += isM ? 0 : ext ? (en ? sc.ee : sc.ie) : (en ? sc.eo : sc.io);
-                    i = ni;
-                    j = nj;
-                    st = esc ? AT_ESC : nst;
+            if (!__any(alive)) break;
+#ifdef AR_PROF
+            ++wit;
+#endif
+            const bool isM = st == AT_M, isX = st == AT_IX, isY = st == AT_IY;
+            // ---- account the cell (i, j) in state st
+            const uint32_t bx = wct[xa], by = wct[yb];
+            const bool mcol = isM && !first;
+            const bool cnt = mcol && (bx | by) < 4u;
+            const uint32_t dd = bx ^ by;
+            valid += cnt;
+            ts += cnt && dd == 3u;
+            tv += cnt && dd - 1u < 2u;
+            gap += (isX && bx < 4u && (uint32_t)(j - fy1) < gjw) || (isY && by < 4u && (uint32_t)(i - fx1) < giw);
+            nmc += mcol;
+            nmatch += mcol && xa == yb;
+            const int ni = i - (isY ? 0 : 1), nj = j - (isX ? 0 : 1);
+            if (so.sx && !first) {  // this column of the alignment, right to left
+                const uint32_t rc = isY ? (uint32_t)'-' : xa, cc = isX ? (uint32_t)'-' : yb;
+                wx = (wx << 8) | cc;
+                wy = (wy << 8) | rc;
+                ++ncol;
+                if ((ncol & 7) == 0 && alive) {  // columns [E - ncol, E - ncol + 8) of the slot (E = nA + nB)
+                    const size_t o = sbase + (size_t)(nA_ + nB_ - ncol);
+                    ar_store8(dcol + o, wx);
+                    ar_store8(drow + o, wy);
                 }
             }
+            // ---- the predecessor (ni, nj): its bytes and trace word (clamped into the matrix on row /
+            // column 0, where the move is forced and the word unused)
+            const int ci = max(ni, 1) - 1, cjr = max(nj, 1) - 1;
+            const uint32_t cj = (uint32_t)(cjr + off);  // virtual column
+            const uint32_t tstep = (uint32_t)(r0 + ci) + ((cj / K) & 63u);
+            const uint32_t toff = tstep * (uint32_t)(NT * 4 * K) + cj * 4u;
+            const uint32_t xn = a2_load_byte(rbase + (roff + (uint32_t)ci));
+            const uint32_t yn = a2_load_byte(cbase + (coff + (uint32_t)cjr));
+            uint32_t nb = a2_load_trace32(trb + toff);
+            nb = as_u32(as_s2(nb) + as_s2((nb & hmask) << 1));  // v_pk_add_u16: no carry between halves
+            const int d1v = (int)(int8_t)(uint8_t)(nb >> bsh);          // M - Ix of (ni, nj)
+            const int d2v = (int)(int8_t)(uint8_t)(nb >> (bsh + 16u));  // M - Iy
+            // ---- the predecessor's state (first-path tie order), relative to its Ix
+            const int co = j == nB_ ? 0 : -7;  // Ix open of column j (end gap: eo - ee = 0)
+            const int oy = i == nA_ ? 0 : -7;  // Iy open of row i
+            const int aX = isX ? co : 0;
+            const int aY = isX ? co : isY ? -oy : 0;
+            const int vM = d1v + aX, vY = d1v - d2v + aY;
+            const int vm = max(max(vM, vY), 0);
+            const int alt = prio ? AT_IX + (vY == vm) : AT_IY - (vm == 0);  // Ix = 1, Iy = 2
+            int nst = vM == vm ? AT_M : alt;
+            nst = ni == 0 ? AT_IY : nj == 0 ? AT_IX : nst;
+            // a gap run's open (its last move, walked backward): internal unless on an edge
+            const bool en = isX ? (j == nB_ || j == 0) : (i == nA_ || i == 0);
+            nio += !isM && nst != st && !en;
+            const bool fin_now = alive && (ni | nj) == 0;
+            const bool esc_now = alive && !fin_now && ni >= 1 && nj >= 1 && band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
+            if (fin_now || esc_now) {  // park the walk's outcome (no values leave this region)
+                ArWalk& R = wks[lane];
+                R.st = fin_now ? AT_FIN : AT_ESC;
+                R.valid = valid;
+                R.ts = ts;
+                R.tv = tv;
+                R.gap = gap;
+                R.sc2 = 2 * nmatch + nmc - 7 * nio;
+                R.ncol = ncol;
+                if (fin_now && so.sx && (ncol & 7)) {  // the columns since the last window store
+                    const size_t o8 = sbase + (size_t)(nA_ + nB_ - ncol);
+                    if (ncol >= 8) {  // the window's older bytes are already in place
+                        ar_store8(dcol + o8, wx);
+                        ar_store8(drow + o8, wy);
+                    } else {
+                        for (int q = 0; q < ncol; ++q) {
+                            dcol[o8 + q] = (uint8_t)(wx >> (8 * q));
+                            drow[o8 + q] = (uint8_t)(wy >> (8 * q));
+                        }
+                    }
+                }
+            }
+            alive = alive && !fin_now && !esc_now;
+            st = nst;
+            i = ni;
+            j = nj;
+            xa = xn;
+            yb = yn;
+            first = false;
         }
-        if (st == AT_ESC) {  // queue the pair (once) for the full-trace pass (k_alignt2_queued)
-            if (atomicOr(&escf[pb][t][h], 1) == 0 && esc_list) esc_list[atomicAdd(esc_n, 1ull)] = p;
-            st = AT_DONE;
+        // ---- every parked walk: its score check (the path's score against the fill's optimum) and
+        // outputs, in one pass of the wave
+        if (lane < NW) {
+            const ArWalk& R = wks[lane];
+            int fst = R.st;
+            if (fst == AT_FIN) {
+                if (R.sc2 != fin[pb][t][h]) {
+                    fst = AT_ESC;
+                } else {
+                    double* o = out_mode == OUT_BOTH ? out + (p * 2 + oslot) * nm : out + p * nm;
+                    for (int m = 0; m < nm; ++m)
+                        o[m] = metric_value(ms.code[m], (uint32_t)R.valid, (uint32_t)R.ts, (uint32_t)R.tv, (uint32_t)R.gap);
+                    if (sout && (out_mode != OUT_BOTH || oslot == 0)) sout[p] = fin[pb][t][h] + (nA_ + nB_) * dz;
+                    if (so.slen) so.slen[p * so.nslot + (oslot & (so.nslot - 1))] = R.ncol;
+                }
+            }
+            if (fst == AT_ESC)  // queue the pair (once) for the full-trace pass (k_alignt2_queued)
+                if (atomicOr(&escf[pb][t][h], 1) == 0 && esc_list) esc_list[atomicAdd(esc_n, 1ull)] = p;
         }
-        if (lane >= NW) return;
-        W_.i = i;
-        W_.j = j;
-        W_.st = st;
-        W_.first = first;
-        W_.xa = xa;
-        W_.yb = yb;
-        W_.valid = valid;
-        W_.ts = ts;
-        W_.tv = tv;
-        W_.gap = gap;
-        W_.sc2 = sc2;
-        W_.ncol = ncol;
+        if (lane < NW) W_.st = AT_DONE;
     };
 
     auto chain_loop = [&](auto WK) {
         constexpr bool IS_W = decltype(WK)::value;
 #ifdef AR_PROF
-        unsigned long long pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long pf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         unsigned long long tA = AR_NOW();
 #endif
         for (;;) {
@@ -626,7 +678,30 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             uint32_t payF = NEG16X2, payY = NEG16X2, carry = GZ;
             uint8_t* trb = bufs + (size_t)cur * (size_t)buf_bytes;
             const int ln = __lane_id();
-            const uint32_t ln16 = (uint32_t)ln << 4;
+            // (opaque: the compiler would otherwise fold (s << 4) - (ln << 4) into (s - ln) << 4, one
+            // more VALU in every step's record address)
+            uint32_t ln16 = (uint32_t)ln << 4;
+            asm volatile("" : "+v"(ln16));
+            uint32_t eq_lane = (uint32_t)ln * (EP * 4);  // the lane's byte offset in a table piece
+            asm volatile("" : "+v"(eq_lane));
+            // the lane's column bytes of both halves (bytes k of colb[h]) and its pre-columns (bit
+            // 8 h + k): a row byte other than A/C/G/T compares against these (rare rows; kept in
+            // registers so that this path does not set the step loop's register pressure)
+            constexpr int CW = (K + 3) / 4;
+            uint32_t colb[2][CW];
+            uint32_t premask = 0;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+                for (int q = 0; q < CW; ++q) colb[hh][q] = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int jr = tq0 * K + k + 1 - ch.off[hh];
+                    const uint32_t cb = (jr >= 1 && jr <= ch.nB[hh]) ? (uint32_t)ch.cseq[hh][jr - 1] : 0u;
+                    colb[hh][k / 4] |= cb << (8 * (k % 4));
+                    if (jr < 1) premask |= 1u << (8 * hh + k);
+                }
+            }
             __syncthreads();  // xinfo block 0, tables
 #ifdef AR_PROF
             pf[2] += AR_NOW() - tA;
@@ -639,15 +714,52 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             auto rec_addr = [&](const int s) -> const char* {  // this lane's row record at step s
                 return (const char*)xinfo + ((((uint32_t)s << 4) - ln16) & ((XR - 1) << 4));
             };
-            // recx: the record's table offset (.x), read ahead of the step when AR_PREC
-            auto step = [&](auto WIC, const int s, const uint32_t recx) {
+            // A step's LDS operands -- the lane's row record, its row base's table words and (waves
+            // after the first) the ring entry of its first lane -- are read one step AHEAD, during the
+            // previous step: the record at the step's top, the table words (which need the record)
+            // half way through its cells.  Without it every step began with two dependent LDS round
+            // trips.  Prefetches stay inside the progress block: wave 0 writes the next 64 rows'
+            // records only after a block whose end is a multiple of 64 (the last step prefetches
+            // itself again).
+            struct StepIn {
+                uint4 rec;
+                uint32_t eq[K];
+                uint2 ring;
+            };
+            auto load_rec = [&](auto WIC, const int s, StepIn& o) {
+                constexpr int WI = decltype(WIC)::value;
+                o.rec = *(const uint4*)rec_addr(s);
+                if constexpr (WI > 0) o.ring = ring[(WI - 1) * AR_RING + ((s + 1) & (AR_RING - 1))];
+                else o.ring = make_uint2(0u, 0u);
+            };
+            auto load_eq = [&](auto WIC, StepIn& o) {
+                constexpr int WI = decltype(WIC)::value;
+                constexpr int tq = WI * 64;
+                // the row base's table, this lane's EP words of each piece (lane-contiguous reads)
+                const char* tb = (const char*)&eqt[0][0][tq][0] + eq_lane + o.rec.x;
+#pragma unroll
+                for (int q = 0; q < K / EP; ++q) {
+                    const char* pq = tb + (size_t)(q * NT) * (EP * 4);
+                    if constexpr (EP == 4) {
+                        const uint4 v = *(const uint4*)__builtin_assume_aligned(pq, 16);
+                        o.eq[4 * q] = v.x;
+                        o.eq[4 * q + 1] = v.y;
+                        o.eq[4 * q + 2] = v.z;
+                        o.eq[4 * q + 3] = v.w;
+                    } else {
+                        const uint2 v = *(const uint2*)__builtin_assume_aligned(pq, 8);
+                        o.eq[2 * q] = v.x;
+                        o.eq[2 * q + 1] = v.y;
+                    }
+                }
+            };
+            auto step = [&](auto WIC, const int s, StepIn& I, const int sn, StepIn& N) {
                 constexpr int WI = decltype(WIC)::value;
                 constexpr bool FW = WI == 0, HO = WI < W - 1;
                 const int g = s - ln;
                 const int tq = WI * 64 + ln;
-                const uint4 rec = *(const uint4*)rec_addr(s);
-                uint2 o_ring = make_uint2(0u, 0u);
-                if constexpr (!FW) o_ring = ring[(WI - 1) * AR_RING + ((s + 1) & (AR_RING - 1))];
+                const uint4 rec = I.rec;
+                load_rec(WIC, sn, N);  // the next step's record (and ring entry)
                 const bool in_band = (uint8_t)((uint32_t)tq - rec.y) <= (uint8_t)(rec.y >> 8);
                 const uint64_t bmask = __builtin_amdgcn_ballot_w64(in_band);
                 asm volatile("" ::"s"(bmask));
@@ -658,31 +770,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     inF = shr_old(payF, rec.w);
                     inY = shr_old(payY, NEG16X2);
                 } else {
-                    inF = shr_old(payF, o_ring.x);
-                    inY = shr_old(payY, o_ring.y);
+                    inF = shr_old(payF, I.ring.x);
+                    inY = shr_old(payY, I.ring.y);
                 }
-                uint32_t eq[K];
-                {
-                    // the row base's table, this lane's EP words of each piece (lane-contiguous reads)
-                    // (lane-first base: the other address forms cost the allocator a 129th VGPR, i.e.
-                    // one wave per SIMD at the 128-register budget)
-                    const char* tb = (const char*)&eqt[0][0][tq][0] + recx;
-#pragma unroll
-                    for (int q = 0; q < K / EP; ++q) {
-                        const char* pq = tb + (size_t)(q * NT) * (EP * 4);
-                        if constexpr (EP == 4) {
-                            const uint4 v = *(const uint4*)__builtin_assume_aligned(pq, 16);
-                            eq[4 * q] = v.x;
-                            eq[4 * q + 1] = v.y;
-                            eq[4 * q + 2] = v.z;
-                            eq[4 * q + 3] = v.w;
-                        } else {
-                            const uint2 v = *(const uint2*)__builtin_assume_aligned(pq, 8);
-                            eq[2 * q] = v.x;
-                            eq[2 * q + 1] = v.y;
-                        }
-                    }
-                }
+                uint32_t* const eq = I.eq;
                 if (pre) {  // a unit's first or last row, or a byte other than A/C/G/T
                     if (rec.y & AR_FIRST) {  // row 0 of the new pair: B = 0, Ix = -inf, diagonal B(0, j0 - 1) = 0
 #pragma unroll
@@ -699,16 +790,24 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                             int s2[2];
 #pragma unroll
                             for (int hh = 0; hh < 2; ++hh) {
-                                const int jr = tq * K + k + 1 - ch.off[hh];
-                                const uint32_t cb = (jr >= 1 && jr <= ch.nB[hh]) ? (uint32_t)ch.cseq[hh][jr - 1] : 0u;
-                                s2[hh] = (jr < 1 ? 0 : (cb == rb ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
+                                const uint32_t cb = (colb[hh][k / 4] >> (8 * (k % 4))) & 0xFFu;
+                                s2[hh] = (((premask >> (8 * hh + k)) & 1u) ? 0 : (cb == rb ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
                             }
                             eq[k] = ar_pk_int(s2[0], s2[1]);
+                            __builtin_amdgcn_sched_barrier(0);  // one column at a time: few live values
                         }
                     }
                 }
                 at_s2 F1 = as_s2(inF), Y = as_s2(inY);
                 uint32_t acc[K];
+                constexpr uint32_t PSTRIDE = ar_piece_stride<K, NT>();  // bytes between pieces
+                // uniform step offset (SGPR) + the lane's constant: one VALU add, saddr stores per piece
+                const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane(ar_trace_step_off<K, NT>((uint32_t)s)) +
+                                    (uint32_t)tq * ar_lane_bytes<K>();
+                // the trace words of columns 4 q .. 4 q + 3, as soon as they are computed (K % 4 == 0)
+                auto store_piece = [&](const int q) {
+                    if (in_band) *(uint4*)((trb + q * PSTRIDE) + o0) = make_uint4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                };
                 // Best-open fill on open-shifted cells (alignt2_kernel.hpp cells, RAW): M = G(i-1, j-1) +
                 // (s - co_i), X = max(G_up, X_up), Y = max(G_left, Y_left), B = maximum3(M, X, Y), G = B + o_i.
                 // TR: also the trace words (D1 = M - Ix, D2 = M - Iy of both halves, one v_perm)
@@ -717,6 +816,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     at_s2 Mk = padd32(as_s2(carry), eq[0]);
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
+                        if (k == K / 2) {  // the next step's table words (its record has arrived by now)
+                            __builtin_amdgcn_sched_barrier(0);
+                            load_eq(WIC, N);
+                        }
+                        if constexpr (TR && K % 4 == 0)
+                            if (k % 4 == 0 && k > 0) store_piece(k / 4 - 1);
                         const at_s2 Gu = as_s2(stG[k]), Xu = as_s2(stX[k]);
                         const at_s2 M = Mk;
                         if (k + 1 < K) Mk = padd32(Gu, eq[k + 1]);
@@ -741,19 +846,11 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 // branch is wave-uniform (the band ballot in an SGPR)
                 if (AR_SKIP && bmask == 0) cells(std::false_type{});
                 else cells(std::true_type{});
-                if (in_band) {
-                    constexpr uint32_t PSTRIDE = ar_piece_stride<K, NT>();  // bytes between pieces
-                    // uniform step offset (SGPR) + the lane's constant: one VALU add, saddr stores per piece
-                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane(ar_trace_step_off<K, NT>((uint32_t)s)) +
-                                        (uint32_t)tq * ar_lane_bytes<K>();
-                    if constexpr (K % 4 == 0) {
+                if constexpr (K % 4 == 0) {
+                    store_piece(K / 4 - 1);
+                } else if (in_band) {
 #pragma unroll
-                        for (int q = 0; q < K / 4; ++q)
-                            *(uint4*)((trb + q * PSTRIDE) + o0) = make_uint4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < K / 2; ++q) *(uint2*)((trb + q * PSTRIDE) + o0) = make_uint2(acc[2 * q], acc[2 * q + 1]);
-                    }
+                    for (int q = 0; q < K / 2; ++q) *(uint2*)((trb + q * PSTRIDE) + o0) = make_uint2(acc[2 * q], acc[2 * q + 1]);
                 }
                 payF = as_u32(F1);
                 payY = as_u32(Y);
@@ -795,31 +892,37 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 #ifdef AR_PROF
                     const unsigned long long t0 = AR_NOW();
 #endif
-                    if (W > 1) {  // wait for the other fill wave
+                    if (W > 1 && !stalled) {  // wait for the other fill wave (a bounded wait, see AR_SPIN_CAP)
                         const int need = w == 0 ? s1 - AR_AHEAD : s1 + 63;
-                        while (__hip_atomic_load(&s_prog[other], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+                        int polls = 0;
+                        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_prog[other], __ATOMIC_ACQUIRE,
+                                                                                __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
                             __builtin_amdgcn_s_sleep(1);
+#ifdef AR_PROF
+                            pf[7] += 1;
+#endif
+                            if (++polls >= AR_SPIN_CAP) {
+                                stalled = true;
+                                break;
+                            }
+                        }
+                        if (stalled && lane == 0) __hip_atomic_store(pace_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
 #ifdef AR_PROF
                     const unsigned long long t1 = AR_NOW();
                     pf[4] += t1 - t0;
 #endif
-                    // AR_PREC: step s + 1's table offset (record word .x) is read during step s, so its
-                    // eqt reads issue at the top of the step instead of behind a dependent LDS read.  Within
-                    // the block only: wave 0 writes the next 64 rows' records after a block whose end
-                    // is a multiple of 64, so a record past s1 may not be written yet.
-                    auto recx_at = [&](const int s) { return *(const uint32_t*)rec_addr(s); };
+                    // two step states used alternately (a loop unrolled by two: no copies between steps)
                     auto run = [&](auto WIC) {
-                        if constexpr (AR_PREC) {
-                            uint32_t rx = recx_at(s0);
-                            for (int s = s0; s < s1; ++s) {
-                                const uint32_t nxt = recx_at(s + 1 < s1 ? s + 1 : s);
-                                step(WIC, s, rx);
-                                rx = nxt;
-                            }
-                        } else {
-                            for (int s = s0; s < s1; ++s) step(WIC, s, recx_at(s));
+                        StepIn A, B;
+                        load_rec(WIC, s0, A);
+                        load_eq(WIC, A);
+                        int s = s0;
+                        for (; s + 1 < s1; s += 2) {
+                            step(WIC, s, A, s + 1, B);
+                            step(WIC, s + 1, B, s + 2 < s1 ? s + 2 : s + 1, A);
                         }
+                        if (s < s1) step(WIC, s, A, s, B);
                     };
                     if (w == 0) {
                         run(std::integral_constant<int, 0>{});
@@ -828,14 +931,16 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     }
 #ifdef AR_PROF
                     pf[0] += AR_NOW() - t1;
+                    pf[9] += s1 - s0;
 #endif
                     if (w == 0 && (s1 & (INTERVAL - 1)) == 0) {  // the next 64 rows' records
                         const int gpre = s1 + lane;
                         xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
                     }
                     // publish (the ring / record writes above complete first: release)
+                    // (a stalled wave publishes "done": its partner never waits on it again)
                     if (lane == 0)
-                        __hip_atomic_store(&s_prog[mine], s1 >= nsteps ? 0x3FFFFFFF : s1, __ATOMIC_RELEASE,
+                        __hip_atomic_store(&s_prog[mine], (stalled || s1 >= nsteps) ? 0x3FFFFFFF : s1, __ATOMIC_RELEASE,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 __builtin_amdgcn_s_waitcnt(0);  // this chain's trace stores are done before the walker reads them
@@ -853,7 +958,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
         }
 #ifdef AR_PROF
         if (lane == 0)
-            for (int q = 0; q < 8; ++q) atomicAdd(&ar_prof[q], pf[q]);
+        {
+            pf[8] = wit;
+            for (int q = 0; q < 12; ++q) atomicAdd(&ar_prof[q], pf[q]);
+        }
 #endif
     };
     if (walker) chain_loop(std::true_type{});

@@ -34,6 +34,21 @@ using namespace taxi2;
 
 namespace {
 
+// Environment switches.  test_env: the parity tests' switches, kept in the product library -- each
+// forces another kernel family or launch shape over the same pairs so that two paths can be compared
+// (TAXI2_NO_ALIGNR / NO_PACKED / NO_ALIGNT / NO_ALIGN1 / LONG / LONG_TILE, AT_BAND, AT_CHUNK, AT_HOPS,
+// A1_CHUNK, A1_NOCHAIN, AR_SWAP, PRE_NOTILE, ZLEN_SERIAL, SUB_GATHER, NO_WALK_STRINGS; AT_BAND_STATS prints
+// the queued-pair count the band tests assert on).
+// probe_env: tuning probes and diagnostics (occupancy caps, variant forcing, band statistics, trace
+// budget, ...), read only by the variant builds (make variant VFLAGS=-DTAXI2_PROBES ...): the
+// product library ignores them.
+const char* test_env(const char* name) { return getenv(name); }
+#ifdef TAXI2_PROBES
+const char* probe_env(const char* name) { return getenv(name); }
+#else
+const char* probe_env(const char*) { return nullptr; }
+#endif
+
 struct DevSet {
     bool live = false;
     int mode = 0;
@@ -97,6 +112,9 @@ struct taxi2_ctx {
     size_t h_seg_cap[2] = {0, 0};
     hipEvent_t seg_ev[2] = {nullptr, nullptr};
     int seg_flip = 0;
+    // k_alignr's bounded pacing wait (alignr_kernel.hpp AR_SPIN_CAP): a host-mapped word the kernel
+    // sets (never clears) when a fill wave gave up waiting; read by pace_check
+    unsigned int* h_pace = nullptr;
 };
 
 namespace {
@@ -141,6 +159,18 @@ int shared_release(taxi2_ctx* ctx, hipStream_t st) {
     if (!ctx->shared_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->shared_ev, hipEventDisableTiming));
     HIP_TRY(ctx, hipEventRecord(ctx->shared_ev, st));
     ctx->shared_st = st;
+    return 0;
+}
+
+// A k_alignr launch whose fill waves gave up a pacing wait (alignr_kernel.hpp AR_SPIN_CAP) set
+// ctx->h_pace: its results are invalid.  Checked after the blocking entry points' synchronisation
+// and before the next row-shared launch (the *_dev calls' asynchronous launches report there).
+int pace_check(taxi2_ctx* ctx) {
+    if (ctx->h_pace && __atomic_load_n(ctx->h_pace, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(ctx->h_pace, 0u, __ATOMIC_RELEASE);
+        return fail(ctx, "k_alignr: a fill wave's pacing wait exceeded its bound (AR_SPIN_CAP); the launch was "
+                         "abandoned and its results are invalid");
+    }
     return 0;
 }
 
@@ -236,7 +266,7 @@ const Variant* find_variant(const Variant (&tab)[N], int K, int W, int occ, bool
 
 const Variant* pick_variant(const KScores& k, int max_len) {
     const bool lin = is_linear(k), def = !lin && is_default(k);
-    if (const char* force = getenv("TAXI2_VARIANT")) {  // tuning hook: "K,W,OCC"
+    if (const char* force = probe_env("TAXI2_VARIANT")) {  // tuning hook: "K,W,OCC"
         int K = 0, W = 0, occ = 0;
         if (sscanf(force, "%d,%d,%d", &K, &W, &occ) == 3 && 64 * K * W >= max_len) {
             const Variant* v = find_variant(kSweep, K, W, occ, lin, def);
@@ -329,7 +359,7 @@ const Variant1 kAlign1Sweep[] = {
 
 const Variant1* pick_variant1(const KScores& k, int max_len) {
     const bool def = is_default(k);
-    if (const char* force = getenv("TAXI2_VARIANT1")) {
+    if (const char* force = probe_env("TAXI2_VARIANT1")) {
         int K = 0, W = 0, occ = 0;
         if (sscanf(force, "%d,%d,%d", &K, &W, &occ) == 3 && 64 * K * W >= max_len) {
             for (const auto* tab : {kAlign1Sweep, kAlign1Def, kAlign1}) {
@@ -357,7 +387,7 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
                         hipStream_t st, int xcap) {
     // chained kernel (consecutive pairs sharing their column sequence stream through the lanes);
     // TAXI2_A1_NOCHAIN=1 selects the one-pair-at-a-time kernel
-    const bool chain = !getenv("TAXI2_A1_NOCHAIN");
+    const bool chain = !test_env("TAXI2_A1_NOCHAIN");
     if (chain && ps.count >= ((int64_t)1 << 31))  // worklist entries: pair index | orientation << 31
         return fail(ctx, "single-orientation aligner: %lld pairs in one call (limit 2^31 - 1)", (long long)ps.count);
     const size_t lds = chain ? a1c_lds_bytes(v.K, v.W, v.def) : a1_lds_bytes(xcap, v.K, v.W, v.def);
@@ -382,7 +412,7 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
     // TAXI2_A1_CHUNK forces 1..16 pairs per cursor step, e.g. to test long chains on small inputs)
     int arg = xcap;
     if (chain) {
-        const char* c = getenv("TAXI2_A1_CHUNK");
+        const char* c = test_env("TAXI2_A1_CHUNK");
         arg = c ? std::max(0, std::min(A1C_CHUNK, atoi(c))) : 0;
     }
     launch[0](dim3((unsigned)grid), dim3(64 * v.W), lds, st, view(X), view(Y), ps, k, ms, arg, out_mode, d_out,
@@ -392,7 +422,7 @@ int launch_align1_pairs(taxi2_ctx* ctx, const Variant1& v, const DevSet& X, cons
               nullptr, wlist, wcount, next + 1);
     HIP_TRY(ctx, hipGetLastError());
     if (shared_release(ctx, st)) return -1;
-    if (getenv("TAXI2_A1_STATS")) {  // diagnostics: share of pairs re-run in orientation B
+    if (probe_env("TAXI2_A1_STATS")) {  // diagnostics: share of pairs re-run in orientation B
         uint32_t n2 = 0;
         HIP_TRY(ctx, hipMemcpyAsync(&n2, wcount, 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(ctx, hipStreamSynchronize(st));
@@ -496,7 +526,7 @@ const VariantT kAlignT2R[] = {
 bool bopen_ok(const KScores& k) {
     auto ab = [](int v) { return v < 0 ? -v : v; };
     const int big = std::max({ab(k.ma), ab(k.mi), ab(k.io), ab(k.ie), ab(k.eo), ab(k.ee)});
-    return k.ie == k.ee && k.io <= k.ie && k.eo <= k.ee && big <= 12 && !getenv("TAXI2_NO_BOPEN");
+    return k.ie == k.ee && k.io <= k.ie && k.eo <= k.ee && big <= 12 && !probe_env("TAXI2_NO_BOPEN");
 }
 
 const VariantT* pick_variantt2(const KScores& k, int max_len) {
@@ -525,14 +555,14 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     // rule (at least ~8 chunks per workgroup); it bounds the rows of a chain, hence the buffers
     const int cmax = packed ? AT2_CHUNK : AT_CHUNK;
     int chunk = 0;
-    if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(cmax, atoi(c)));
+    if (const char* c = test_env("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(cmax, atoi(c)));
     int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(cmax, ps.count / (grid * 8)));
     // two trace buffers per resident workgroup: shrink the chunk (hence the chain rows) until they
     // fit the budget (TAXI2_AT_TRACE_GB, default 40 GB of the 288 GB HBM; 80 GB for the packed
     // default-score kernel, whose raw-difference trace takes 4 bytes per lane-column and step)
     const bool raw = packed && v.raw;  // best-open fill + raw-difference trace (alignt2_kernel.hpp)
     double budget_gb = raw ? 80.0 : 40.0;
-    if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
+    if (const char* b = probe_env("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     auto buf_bytes = [&](int64_t e) {
         const int64_t per_stream = packed ? (e + 1) / 2 : e;  // a stream takes every other pair of a chain
         return at_buf_bytes((int)per_stream * std::max(1, max_len), packed ? (raw ? 4 : 2) * v.K : v.K, v.W);
@@ -544,7 +574,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     const size_t bb = buf_bytes(eff);
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, (size_t)grid * 2 * bb)) return -1;
     int hops = 4096;  // per-interval cap; the packed kernel stops at the fill waves' signal
-    if (const char* h = getenv("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
+    if (const char* h = test_env("TAXI2_AT_HOPS")) hops = std::max(1, atoi(h));
     // Packed kernel: the fill stores only a diagonal strip of each pair's trace (band half-width in
     // columns: TAXI2_AT_BAND, 0 = everything; default 3 sqrt(max_len), at least 32: wider than the
     // first paths of synthetic families measured at 200-2 000 bp); walks that leave
@@ -553,7 +583,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
     if (packed) {
         band = std::max(32, (int)std::ceil(3.0 * std::sqrt((double)std::max(1, max_len))));
         if (4 * band >= max_len) band = 0;  // the strip would be most of the row
-        if (const char* e = getenv("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
+        if (const char* e = test_env("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
     }
     // d_work: [u64 pad] [u64 pass-1 cursor] [u64 pass-2 cursor] [u64 queue count] [pad] [i64 queue...]
     // (the queue also takes raw-difference walks whose score check failed, so it exists whenever
@@ -576,7 +606,7 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
         v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), p2, k, ms, chunk, out_mode, d_out,
                  d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, hops, next2, BandArgs{0, nullptr, nullptr}, str);
         HIP_TRY(ctx, hipGetLastError());
-        if (getenv("TAXI2_AT_BAND_STATS")) {  // diagnostics: queued pairs of this call on stderr
+        if (test_env("TAXI2_AT_BAND_STATS")) {  // diagnostics: queued pairs of this call on stderr
             unsigned long long q = 0;
             HIP_TRY(ctx, hipMemcpyAsync(&q, esc_n, sizeof q, hipMemcpyDeviceToHost, st));
             HIP_TRY(ctx, hipStreamSynchronize(st));
@@ -616,15 +646,16 @@ struct VariantR {
     const void* fn;
     void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, const ArSeg*, int, int64_t, int64_t, MetricSpec, int,
                    int, double*, int32_t*, uint8_t*, int64_t, int, unsigned long long*, int, int64_t*,
-                   unsigned long long*, StrOut);
+                   unsigned long long*, StrOut, unsigned int*);
 };
 
 template <int K, int W, int OCC>
 void launch_alignr(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, const ArSeg* segs, int nseg, int64_t units,
                    int64_t npairs, MetricSpec ms, int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb,
-                   int cap, unsigned long long* nx, int band, int64_t* el, unsigned long long* en, StrOut str) {
+                   int cap, unsigned long long* nx, int band, int64_t* el, unsigned long long* en, StrOut str,
+                   unsigned int* perr) {
     hipLaunchKernelGGL((k_alignr<K, W, OCC>), g, b, 0, st, x, y, segs, nseg, units, npairs, ms, chunk, om, out, so, tr, bb,
-                       cap, nx, band, el, en, str);
+                       cap, nx, band, el, en, str, perr);
 }
 
 // waves per SIMD the row-shared shapes are compiled for: LDS (~23.5 KB per workgroup of three waves)
@@ -722,9 +753,11 @@ void build_segments(std::vector<RowIv>& rows, std::vector<ArSeg>& segs, int64_t&
 }
 
 const VariantR* pick_variantr(const KScores& k, const DevSet& X, const DevSet& Y, const PairSrc& ps) {
-    if (!is_default(k) || getenv("TAXI2_NO_ALIGNR") || getenv("TAXI2_NO_PACKED") || ps.sel) return nullptr;
+    if (!is_default(k) || test_env("TAXI2_NO_ALIGNR") || test_env("TAXI2_NO_PACKED") || ps.sel) return nullptr;
     if (ps.mode != PAIRS_TRI && ps.mode != PAIRS_RECT) return nullptr;
     if (X.max_len > 1024 || Y.max_len > 1024) return nullptr;  // the f16-maximum3 value range (BIAS16)
+    // the walker addresses sequence bytes by 32-bit offsets from the sets' bases
+    if (X.nbytes >= ((int64_t)1 << 32) || Y.nbytes >= ((int64_t)1 << 32)) return nullptr;
     for (const auto& v : kAlignR)
         if (64 * v.K * v.W >= X.max_len) return &v;
     return nullptr;
@@ -733,6 +766,7 @@ const VariantR* pick_variantr(const KScores& k, const DevSet& X, const DevSet& Y
 int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
                         hipStream_t st, StrOut str = StrOut{}) {
+    if (pace_check(ctx)) return -1;  // an earlier asynchronous launch failed
     // ---- segments of the launch's pairs (host), staged through a pinned buffer
     std::vector<RowIv> rows;
     if (ps.mode == PAIRS_TRI) {
@@ -759,7 +793,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // hold them.  Off by default: each swapped unit is a chain of its own, whose walks (latency-bound,
     // four per chain instead of up to 32) outlast its fill, so the fill waves wait at the chain's end
     // barrier -- 94.6 vs 93.6 ms per config-3 launch although the units drop by 4.4 %
-    build_segments(rows, segs, units, 64 * v.K * v.W >= Y.max_len && getenv("TAXI2_AR_SWAP"));
+    build_segments(rows, segs, units, 64 * v.K * v.W >= Y.max_len && test_env("TAXI2_AR_SWAP"));
     if (segs.empty()) return 0;
     const int f = ctx->seg_flip;
     ctx->seg_flip ^= 1;
@@ -778,19 +812,19 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // ---- resident grid, chunk (units per cursor step) and trace buffers, as launch_alignt_pairs
     int per_cu = 0;
     HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 64 * (v.W + 1), 0));
-    if (const char* e = getenv("TAXI2_AR_PERCU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));  // scaling probe
+    if (const char* e = probe_env("TAXI2_AR_PERCU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));  // scaling probe
     const int64_t resident =
         (int64_t)std::max(1, ctx->num_cus - std::max(0, std::min(ctx->reserve_cus, ctx->num_cus - 1))) *
         std::max(1, per_cu);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(units, resident));
     const int max_len = std::max(1, std::max(X.max_len, Y.max_len));
     int chunk = 0;
-    if (const char* c = getenv("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(AR_UNITS, (atoi(c) + 1) / 2));
+    if (const char* c = test_env("TAXI2_AT_CHUNK")) chunk = std::max(0, std::min(AR_UNITS, (atoi(c) + 1) / 2));
     int64_t eff = chunk >= 1 ? chunk : std::max<int64_t>(1, std::min<int64_t>(AR_UNITS, units / (grid * 8)));
     // trace buffers: two per resident workgroup, AR_UNITS rows of sequences each (8 x 1 000 bp: 33 MB);
     // up to 120 GB of the 288 GB HBM, at most 45 % of the device's memory (TAXI2_AT_TRACE_GB overrides)
     double budget_gb = std::min(120.0, 0.45 * (double)ctx->total_mem / 1e9);
-    if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
+    if (const char* b = probe_env("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     // chain rows: row sequences of the row set, or (swapped units) one of the column set's
     const int rmax = std::max(1, std::max(X.max_len, Y.max_len));
     auto buf_bytes = [&](int64_t e) { return at_buf_bytes(ar_trace_rows((int)e * rmax) - 64, 4 * v.K, v.W); };
@@ -803,7 +837,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // requeued pairs' full-trace pass costs more than the writes save
     int band = std::max(32, (int)std::ceil(2.5 * std::sqrt((double)max_len)));
     if (4 * band >= max_len) band = 0;
-    if (const char* e = getenv("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
+    if (const char* e = test_env("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
     // the queued pass (k_alignt2_queued over the launch's PairSrc, sign-digit full trace)
     const VariantT* vq = pick_variantt2(k, max_len);
     if (!vq) return fail(ctx, "no packed variant for the queued pass at length %d", max_len);
@@ -828,7 +862,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 64, st));
     v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), (const ArSeg*)ctx->d_seg, (int)segs.size(),
              units, ps.count, ms, chunk, out_mode, d_out, d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, next,
-             band, esc_list, esc_n, str);
+             band, esc_list, esc_n, str, ctx->h_pace);
     HIP_TRY(ctx, hipGetLastError());
     PairSrc p2 = ps;
     p2.sel = esc_list;
@@ -836,7 +870,7 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     vq->launch(dim3((unsigned)grid_q), dim3(64 * (vq->W + 1)), st, view(X), view(Y), p2, k, ms, chunk_q, out_mode, d_out,
                d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb_q, cap_rows_q, 4096, next2, BandArgs{0, nullptr, nullptr}, str);
     HIP_TRY(ctx, hipGetLastError());
-    if (getenv("TAXI2_AT_BAND_STATS")) {
+    if (test_env("TAXI2_AT_BAND_STATS")) {
         unsigned long long q = 0;
         HIP_TRY(ctx, hipMemcpyAsync(&q, esc_n, sizeof q, hipMemcpyDeviceToHost, st));
         HIP_TRY(ctx, hipStreamSynchronize(st));
@@ -850,13 +884,13 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     }
 #ifdef AR_PROF
     {  // profiling build: the launch's per-wave phase totals (alignr_kernel.hpp AR_PROF)
-        unsigned long long pf[8] = {0}, z[8] = {0};
+        unsigned long long pf[12] = {0}, z[12] = {0};
         HIP_TRY(ctx, hipStreamSynchronize(st));
         HIP_TRY(ctx, hipMemcpyFromSymbol(pf, HIP_SYMBOL(ar_prof), sizeof pf));
         HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(ar_prof), z, sizeof z));
         fprintf(stderr, "taxi2 arprof: k_alignr<%d,%d> grid %lld units %lld chains %llu | fill steps %llu waits %llu barrier %llu"
-                " setup %llu | walker walking %llu barrier %llu\n", v.K, v.W, (long long)grid, (long long)units,
-                pf[6], pf[0], pf[4], pf[1], pf[2], pf[3], pf[5]);
+                " setup %llu | walker walking %llu barrier %llu | polls %llu walker iterations %llu fill steps %llu\n", v.K, v.W,
+                (long long)grid, (long long)units, pf[6], pf[0], pf[4], pf[1], pf[2], pf[3], pf[5], pf[7], pf[8], pf[9]);
     }
 #endif
     if (shared_release(ctx, st)) return -1;
@@ -895,7 +929,7 @@ int launch_alignlong_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, con
     if (ps.count <= 0) return 0;
     const bool lin = is_linear(k);
     const VariantL* v = lin ? &kAlignLong[3] : &kAlignLong[0];
-    if (const char* t = getenv("TAXI2_LONG_TILE")) {
+    if (const char* t = test_env("TAXI2_LONG_TILE")) {
         const int tc = atoi(t);
         for (const auto& c : kAlignLong)
             if (64 * c.K * c.W == tc && c.lin == lin) v = &c;
@@ -910,7 +944,7 @@ int launch_alignlong_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, con
     // workgroup busy (pairs past ~6 500 bp need > 80 MB of trace each); TAXI2_AT_TRACE_GB fixes it
     const int64_t resident = (int64_t)ctx->num_cus * std::max(1, per_cu);
     double budget_gb = std::max(40.0, std::min(96.0, (double)std::min<int64_t>(ps.count, resident) * 2.0 * (double)bb / 1e9));
-    if (const char* b = getenv("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
+    if (const char* b = probe_env("TAXI2_AT_TRACE_GB")) budget_gb = std::max(1.0, atof(b));
     const int64_t fit = (int64_t)(budget_gb * 1e9 / (2.0 * (double)bb));
     if (2.0 * (double)bb > 200e9)
         return fail(ctx, "pair trace of %lld x %lld bp needs %.1f GB (limit 200 GB)", (long long)rows,
@@ -943,7 +977,7 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
             return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     }
     // past every register-resident shape (and on request, TAXI2_LONG=1): the column-tiled aligner
-    if (max_len > 4095 || getenv("TAXI2_LONG"))
+    if (max_len > 4095 || test_env("TAXI2_LONG"))
         return launch_alignlong_pairs(ctx, X, Y, ps, k, ms, out_mode, d_out, d_scores, st);
     const Variant* v = pick_variant(k, max_len);
     if (!v) return fail(ctx, "sequence length %d exceeds the aligner's column capacity", max_len);
@@ -953,9 +987,9 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (mag * (2LL * max_len + 2) >= (1LL << 26))
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
-    if (!is_linear(k) && !getenv("TAXI2_NO_ALIGNT")) {
+    if (!is_linear(k) && !test_env("TAXI2_NO_ALIGNT")) {
         // packed 16-bit fill when every difference fits int16 (TAXI2_NO_PACKED=1: 32-bit fill)
-        const bool packed = at_fits16(k, max_len) && !getenv("TAXI2_NO_PACKED");
+        const bool packed = at_fits16(k, max_len) && !test_env("TAXI2_NO_PACKED");
         if (packed)
             if (const VariantR* vr = pick_variantr(k, X, Y, ps)) {
                 if (ps.count <= 0) return 0;
@@ -967,7 +1001,7 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
             return launch_alignt_pairs(ctx, *vt, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, max_len, packed);
         }
     }
-    if (!is_linear(k) && max_len <= A1_MAX_LEN_LONG && !getenv("TAXI2_NO_ALIGN1")) {
+    if (!is_linear(k) && max_len <= A1_MAX_LEN_LONG && !test_env("TAXI2_NO_ALIGN1")) {
         if (ps.count <= 0) return 0;
         const Variant1* v1 = pick_variant1(k, max_len);
         if (v1) return launch_align1_pairs(ctx, *v1, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, xcap);
@@ -993,8 +1027,8 @@ int launch_packed_strings(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, cons
                           StrOut str) {
     const KScores k = kscores(sc);
     const int max_len = std::max(X.max_len, Y.max_len);
-    if (is_linear(k) || !at_fits16(k, max_len) || getenv("TAXI2_NO_ALIGNT") || getenv("TAXI2_NO_PACKED") ||
-        getenv("TAXI2_LONG") || getenv("TAXI2_NO_WALK_STRINGS"))
+    if (is_linear(k) || !at_fits16(k, max_len) || test_env("TAXI2_NO_ALIGNT") || test_env("TAXI2_NO_PACKED") ||
+        test_env("TAXI2_LONG") || test_env("TAXI2_NO_WALK_STRINGS"))
         return 1;
     const VariantT* vt = pick_variantt2(k, max_len);
     if (!vt) return 1;
@@ -1026,7 +1060,7 @@ int launch_prealigned(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const Pa
     // TAXI2_PRE_NOTILE=1 keeps the one-thread-per-pair kernel (A/B and parity tests)
     // (the row-block epilogue of taxi2_rect_block_dev exists only in the tiled kernel)
     const bool epi = tb.rmin_v || tb.diag || tb.scale != 1.0 || tb.ynat;
-    if (ps.mode != PAIRS_LIST && (epi || (ps.count >= 4096 && !getenv("TAXI2_PRE_NOTILE")))) {
+    if (ps.mode != PAIRS_LIST && (epi || (ps.count >= 4096 && !test_env("TAXI2_PRE_NOTILE")))) {
         int64_t x0, nx, y0, ny;
         if (ps.mode == PAIRS_TRI) {
             const int64_t a0 = tri_row_host(ps.k0, ps.N), a1 = tri_row_host(ps.k0 + ps.count - 1, ps.N);
@@ -1097,6 +1131,7 @@ int run_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, PairSrc base, co
             HIP_TRY(ctx, hipMemcpyAsync(scores_out + done, d_sc, (size_t)n * 4, hipMemcpyDeviceToHost,
                                         ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (pace_check(ctx)) return -1;
     }
     return 0;
 }
@@ -1139,7 +1174,7 @@ struct Tracer {
         k = ks;
         lin = is_linear(k);
         cap = cap_;
-        longp = max_len > 4095 || getenv("TAXI2_LONG");
+        longp = max_len > 4095 || test_env("TAXI2_LONG");
         if (longp) {  // strings from k_alignlong's walkers: only the index and output staging
             chunk = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 30) / (4 * (int64_t)std::max(cap, 1))));
             HIP_TRY(ctx, hipMalloc(&d_idx, (size_t)chunk * 2 * sizeof(int64_t)));
@@ -1281,7 +1316,7 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
                 hipStream_t st, int likely_n, int first_only) {
     if (n <= 0) return 0;
     if (!st) st = ctx->stream;
-    bool wave_ok = !latin1 && !getenv("TAXI2_ZLEN_SERIAL");
+    bool wave_ok = !latin1 && !test_env("TAXI2_ZLEN_SERIAL");
     auto wave_pass = [&](int nmax_in, int redo) -> int {
         const int nmax = std::max(nmax_in, 4);
         const size_t lds = zlw::lds_bytes(nmax);
@@ -1307,7 +1342,7 @@ int launch_zlen(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out, 
     // waves per SIMD of the one-thread-per-stream parse (TAXI2_ZLEN_WAVES, 1..4: VGPRs cap it at 4);
     // each thread owns 113 KB of HBM scratch
     int wps = 2;
-    if (const char* e = getenv("TAXI2_ZLEN_WAVES")) wps = std::max(1, std::min(4, atoi(e)));
+    if (const char* e = probe_env("TAXI2_ZLEN_WAVES")) wps = std::max(1, std::min(4, atoi(e)));
     const int64_t want = std::min<int64_t>(n, (int64_t)ctx->num_cus * 4 * 64 * wps);
     const int64_t threads = (want + 63) / 64 * 64;
     if (ctx->z_threads < threads) {
@@ -1334,7 +1369,7 @@ int launch_zlen2(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out,
                  bool latin1, hipStream_t st, int likely_n) {
     if (n <= 0) return 0;
     if (!st) st = ctx->stream;
-    if (latin1 || getenv("TAXI2_ZLEN_SERIAL") || max_n > zlw::NMAX) {
+    if (latin1 || test_env("TAXI2_ZLEN_SERIAL") || max_n > zlw::NMAX) {
         if (launch_zlen(ctx, d_st, n, d_out, max_n, latin1, st)) return -1;
         return launch_zlen(ctx, d_st, n, d_out_a, max_n, latin1, st, 0, 1);
     }
@@ -1346,7 +1381,7 @@ int launch_zlen2(taxi2_ctx* ctx, const ZStream* d_st, int64_t n, int32_t* d_out,
         int per_cu = 0;
         HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_zlen_wave2, 64, lds));
         per_cu = std::min(per_cu, lds_fit_per_cu(lds));
-        if (const char* e = getenv("TAXI2_ZLEN_PERCU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));  // scaling probe
+        if (const char* e = probe_env("TAXI2_ZLEN_PERCU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));  // scaling probe
         const int64_t grid = std::min<int64_t>(n, (int64_t)ctx->num_cus * std::max(1, per_cu));
         hipLaunchKernelGGL(k_zlen_wave2, dim3((unsigned)grid), dim3(64), lds, st, d_st, n, nmax, d_out, d_out_a, redo);
         HIP_TRY(ctx, hipGetLastError());
@@ -1402,7 +1437,7 @@ int ncd_from_slots(taxi2_ctx* ctx, const SlotSrc& ss, const DevSet& X, const Dev
     // the few longer alignments take the redo pass).  TAXI2_NCD_MARGIN fixes the margin instead.
     const int lmax = std::max(X.max_len, Y.max_len);
     int likely = lmax + lmax / 16 + 32;
-    if (const char* e = getenv("TAXI2_NCD_MARGIN")) {
+    if (const char* e = probe_env("TAXI2_NCD_MARGIN")) {
         likely = lmax + std::max(0, atoi(e));
     } else {
         int best_w = -1;
@@ -1509,6 +1544,12 @@ int taxi2_ctx_create(int device, taxi2_ctx** out) {
         delete ctx;
         return -6;
     }
+    if (hipHostMalloc((void**)&ctx->h_pace, sizeof(unsigned int), hipHostMallocMapped) != hipSuccess) {
+        (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return -7;
+    }
+    *ctx->h_pace = 0;
     *out = ctx;
     return 0;
 }
@@ -1535,6 +1576,7 @@ void taxi2_ctx_destroy(taxi2_ctx* ctx) {
     if (ctx->d_ncd) (void)hipFree(ctx->d_ncd);
     if (ctx->d_nslots) (void)hipFree(ctx->d_nslots);
     if (ctx->shared_ev) (void)hipEventDestroy(ctx->shared_ev);
+    if (ctx->h_pace) (void)hipHostFree(ctx->h_pace);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -2226,7 +2268,7 @@ struct SummaryHost {
 // (tools/d2h_probe: 54.7 GB/s from kernel stores against 27-30 GB/s for hipMemcpyAsync into the same
 // pinned buffer), with no staging copy in HBM and no separate D2H.  TAXI2_TEXT_D2H=1: the copy path.
 static char* host_mapped(void* out) {
-    if (!out || getenv("TAXI2_TEXT_D2H")) return nullptr;
+    if (!out || probe_env("TAXI2_TEXT_D2H")) return nullptr;
     hipPointerAttribute_t at{};
     if (hipPointerGetAttributes(&at, out) != hipSuccess) {
         (void)hipGetLastError();  // pageable memory: not an error of the call
@@ -2615,7 +2657,7 @@ int taxi2_subset_aggregate_dev(taxi2_ctx* ctx, const double* d_vals, int64_t nro
     const int64_t per_row = (int64_t)ns * m;
     // few subsets: natural-order rows (k_subset_rows_nat), ns x nch chunk slots per row
     const int64_t nch = std::max<int64_t>(1, (ncols + SUB_CH - 1) / SUB_CH);
-    const bool nat = ns <= 4 && !getenv("TAXI2_SUB_GATHER");
+    const bool nat = ns <= 4 && !test_env("TAXI2_SUB_GATHER");
     const int64_t tmax64 = nat ? (int64_t)ns * nch : (int64_t)ns + (ncols + SUB_CH - 1) / SUB_CH;
     if (tmax64 > INT32_MAX / 2) return fail(ctx, "taxi2_subset_aggregate_dev: too many subsets");
     const int tmax = (int)tmax64;

@@ -84,6 +84,10 @@ run_step() {
         (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM \
             SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE $PMC_OPTS -d "$OUT/pmc_lds" -o run -- \
             $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_lds.err") ;;
+    pmc_mem)  # the vector-memory and texture pipeline: instruction counts and TA/TD busy
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_SMEM \
+            TA_TA_BUSY_sum TA_BUFFER_WAVEFRONTS_sum GRBM_GUI_ACTIVE $PMC_OPTS -d "$OUT/pmc_mem" -o run -- \
+            $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_mem.err") ;;
     pmc_fetch)
         (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE $PMC_OPTS -d "$OUT/pmc_fetch" -o run -- \
             $BENCH --steps 1 --warmup 0 > /dev/null 2> "$OUT/pmc_fetch.err") ;;
