@@ -278,7 +278,8 @@ int taxi2_pack_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_s
  * d_out[k * no + o] = NCD (distances.py:351-358) of that ordered pair.  max_len: the longest
  * sequence of the pairs (sizes the deflate working set; any aligned string is at most twice it);
  * latin1: some byte >= 0x80 (compressed as its UTF-8 upper case).  Asynchronous on `stream`; uses
- * the context's NCD staging (one call at a time per context). */
+ * the context's NCD staging: a call on another stream than the context's previous device work is
+ * ordered behind that work (no two streams use the staging at once). */
 int taxi2_ncd_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
                         int nslot, int no, const int64_t* d_end, int64_t count, int32_t max_len, int latin1,
                         double* d_out, void* stream);

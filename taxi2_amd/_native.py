@@ -94,12 +94,14 @@ def _dev_vals(vals, stream):
         nrows, ncols, nm = vals.shape
     else:
         raise ValueError("device values must be (nrows, ncols) or (nrows, ncols, nm) with unit metric stride")
-    vs = vals.stride(1)
+    # slot g = r * ncols + c lies at g * vs: with one column the slots are the rows (stride(0)), else
+    # the rows must be contiguous runs of slots
+    vs = vals.stride(0) if ncols == 1 else vals.stride(1)
     if ncols > 1 and nrows > 1 and vals.stride(0) != ncols * vs:
         raise ValueError("device value rows must be contiguous slot runs")
-    if vs < nm:
+    if nrows * ncols > 1 and vs < nm:
         raise ValueError("device value slots overlap")
-    return vals.data_ptr(), (nrows, ncols, nm), int(vs), stream
+    return vals.data_ptr(), (nrows, ncols, nm), int(max(vs, nm)), stream
 
 
 class NativeError(RuntimeError):
@@ -757,6 +759,10 @@ class Engine:
                 )
         return out
 
+    def _check_dev_tensor(self, vals, dev) -> None:
+        if dev is not None and vals.device.index is not None and vals.device.index != self.device:
+            raise ValueError(f"device values live on cuda:{vals.device.index}, the engine on device {self.device}")
+
     def format_rows(self, vals, row_pre, col_pre=None, *, decimals: int = 4,
                     missing: str = "NA", view: bool = False, stream: int | None = None):
         """Writer text (taxi2_format_rows): ``vals`` (nrows, ncols, nm) -> linear rows
@@ -766,6 +772,7 @@ class Engine:
         (rows, n, M) block): taxi2_format_rows_dev, ordered on ``stream``."""
         mode = 0 if col_pre is not None else 1
         dev = _dev_vals(vals, stream)
+        self._check_dev_tensor(vals, dev)
         if dev is not None:  # a float64 CUDA tensor: taxi2_format_rows_dev reads it where it is
             v, nrows, ncols, nm = dev[0], *dev[1]
             if mode == 1 and nm != 1:
@@ -805,6 +812,7 @@ class Engine:
         = 2 strings per row / column (extras with leading TABs; TAB genus TAB species),
         row_codes / col_codes (n, 2) = (genus, species) subset codes."""
         dev = _dev_vals(vals, stream)
+        self._check_dev_tensor(vals, dev)
         if dev is not None:
             v, (nrows, ncols, nm) = dev[0], dev[1]
         else:

@@ -55,6 +55,9 @@ constexpr int AR_AHEAD = (AR_RING - 63) < (512 - 64 - 63 - AR_BLK) ? (AR_RING - 
 // block only while it is at most AR_AHEAD steps ahead of wave 1's published k AR_BLK.  A ring of 128
 // (AR_AHEAD 65 < 96 at AR_BLK 32) deadlocks on the GPU.
 static_assert(AR_AHEAD >= AR_BLK * (1 + (63 + AR_BLK - 1) / AR_BLK), "fill waves would deadlock");
+// Wave 0 writes the next INTERVAL rows' records after a block whose end is a multiple of INTERVAL:
+// every block end must be able to be one, and no block may outrun the rows written
+static_assert(AR_BLK <= INTERVAL && INTERVAL % AR_BLK == 0, "AR_BLK must divide INTERVAL (row records)");
 #ifndef TAXI2_AR_UNITS
 #define TAXI2_AR_UNITS 8
 #endif
@@ -66,7 +69,15 @@ constexpr int AR_UNITS = TAXI2_AR_UNITS;
 #ifndef TAXI2_AR_SPIN_CAP
 #define TAXI2_AR_SPIN_CAP (1 << 24)
 #endif
-constexpr int AR_SPIN_CAP = TAXI2_AR_SPIN_CAP;  // units (row sequences, up to two pairs each) per chain
+constexpr int AR_SPIN_CAP = TAXI2_AR_SPIN_CAP;
+// wave priorities (s_setprio 0-3) of the walker and of fill waves 0 / 1.  Config-3 launch, same box,
+// two runs each (profiles/r6/prio/): 0,0,0 87.9 ms; 0,1,1 86.6; 0,2,1 86.4; 0,1,2 90.4 -- the walker
+// fills idle issue slots, and the leading fill wave (which the other waits on) goes first
+#ifndef TAXI2_AR_PRIO
+#define TAXI2_AR_PRIO 0, 2, 1
+#endif
+constexpr int AR_PRIOS[3] = {TAXI2_AR_PRIO};
+constexpr int AR_PRIO_WALK = AR_PRIOS[0], AR_PRIO_W0 = AR_PRIOS[1], AR_PRIO_W1 = AR_PRIOS[2];  // units (row sequences, up to two pairs each) per chain
 // Trace layout.  AR_TS = 0 (default): [step][lane][4K bytes], a lane's K columns contiguous.
 // AR_TS >= 1: the columns are cut into pieces of ar_pw(K) columns (16 bytes for K % 4 == 0), and
 // piece q of all lanes over AR_TS consecutive steps is one run, [step / AR_TS][piece][lane][step %
@@ -495,6 +506,14 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 
     auto chain_loop = [&](auto WK) {
         constexpr bool IS_W = decltype(WK)::value;
+        // issue priority (s_setprio): the walker has slack (it ends its walks well before the fill
+        // ends the next chain), so its instructions should take the SIMD's idle issue slots only
+        if constexpr (IS_W) {
+            __builtin_amdgcn_s_setprio(AR_PRIO_WALK);
+        } else {
+            if (w == 0) __builtin_amdgcn_s_setprio(AR_PRIO_W0);
+            else __builtin_amdgcn_s_setprio(AR_PRIO_W1);
+        }
 #ifdef AR_PROF
         unsigned long long pf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         unsigned long long tA = AR_NOW();

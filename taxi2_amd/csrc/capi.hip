@@ -1426,6 +1426,9 @@ int ncd_from_slots(taxi2_ctx* ctx, const SlotSrc& ss, const DevSet& X, const Dev
     int32_t* d_cab = (int32_t*)((char*)ctx->d_ncd + b_f + b_s);
     int32_t* d_ca = d_cab + nf;
     int32_t* d_cs = d_ca + nf;
+    // d_ncd (and the caller's d_nslots) are per-context scratch: a call on another stream than the
+    // last user's is ordered behind it (the aligners' shared-buffer event)
+    if (shared_acquire(ctx, st)) return -1;
     hipLaunchKernelGGL(k_ncd_slot_streams, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, ss.sx, ss.sy, ss.slen,
                        ss.cap, ss.nslot, ss.no, ss.d_end, view(X), view(Y), ss.ps, n, d_fused, d_single);
     HIP_TRY(ctx, hipGetLastError());
@@ -1455,7 +1458,7 @@ int ncd_from_slots(taxi2_ctx* ctx, const SlotSrc& ss, const DevSet& X, const Dev
     hipLaunchKernelGGL(k_ncd_slot_finish, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, d_cab, d_ca, d_cs, n,
                        ss.no, out, ostride, ocol);
     HIP_TRY(ctx, hipGetLastError());
-    return 0;
+    return shared_release(ctx, st);
 }
 
 bool has_ncd(const MetricSpec& ms) {
@@ -1483,6 +1486,7 @@ int all_pairs_ncd(taxi2_ctx* ctx, const DevSet& S, int64_t k0, int64_t count, co
     int32_t* d_len = (int32_t*)(d_sy + b_slots);
     double* d_tmp = h_out ? (double*)((char*)d_len + b_len) : nullptr;
     int32_t* d_stmp = b_sc ? (int32_t*)((char*)d_len + b_len + b_out) : nullptr;
+    if (shared_acquire(ctx, st)) return -1;  // d_nslots: per-context scratch, ordered across streams
     for (int64_t c0 = 0; c0 < count; c0 += chunk) {
         const int64_t n = std::min(chunk, count - c0);
         PairSrc ps{PAIRS_TRI, k0 + c0, n, S.n, 0, nullptr, nullptr};
@@ -1501,7 +1505,7 @@ int all_pairs_ncd(taxi2_ctx* ctx, const DevSet& S, int64_t k0, int64_t count, co
             HIP_TRY(ctx, hipStreamSynchronize(st));
         }
     }
-    return 0;
+    return shared_release(ctx, st);
 }
 
 }  // namespace
@@ -1706,6 +1710,9 @@ int taxi2_set_info(taxi2_ctx* ctx, int set_id, int64_t* n, int32_t* max_len, int
     return 0;
 }
 
+static int ncd_pairs_impl(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
+                          const taxi2_scores* sc, int both, double* out, bool try_packed);
+
 int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const taxi2_scores* sc,
                     const int32_t* metrics, int nmetrics, double* out, int32_t* scores_out) {
     if (!ctx) return -1;
@@ -1740,7 +1747,7 @@ int taxi2_all_pairs(taxi2_ctx* ctx, int set, int64_t k0, int64_t count, const ta
                 yb[k] = b;
                 if (++b == s->n) b = ++a + 1;
             }
-            if (taxi2_ncd_pairs(ctx, set, set, xa.data(), yb.data(), n, sc, 1, v.data())) return -1;
+            if (ncd_pairs_impl(ctx, set, set, xa.data(), yb.data(), n, sc, 1, v.data(), false)) return -1;
             for (int64_t k = 0; k < n; ++k)
                 for (int m = 0; m < ms.n; ++m)
                     if (ms.code[m] == TAXI2_METRIC_NCD) {
@@ -2104,8 +2111,11 @@ int taxi2_align_strings(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs,
     return 0;
 }
 
-int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
-                    const taxi2_scores* sc, int both, double* out) {
+// try_packed: aligned pairs first go through the packed aligner's string walkers (one fill each);
+// false when the caller already knows the shape is not the packed aligner's (taxi2_all_pairs' NCD
+// fallback), which then skips the per-chunk attempt and its staging.
+static int ncd_pairs_impl(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
+                          const taxi2_scores* sc, int both, double* out, bool try_packed) {
     if (!ctx) return -1;
     DevSet* X = get_set(ctx, set_x);
     DevSet* Y = get_set(ctx, set_y);
@@ -2118,7 +2128,7 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
     const int no = both ? 2 : 1;
     const int cap = X->max_len + Y->max_len;
     if (!aligned && X->n + (X == Y ? 0 : Y->n) <= count * no) return ncd_raw_cached(ctx, *X, *Y, xs, ys, count, both, out);
-    if (aligned && X->mode == TAXI2_MODE_ALIGN && Y->mode == TAXI2_MODE_ALIGN) {
+    if (try_packed && aligned && X->mode == TAXI2_MODE_ALIGN && Y->mode == TAXI2_MODE_ALIGN) {
         // the packed aligner's walkers write the strings (one fill per pair, both orientations),
         // NCD from those slots (ncd_from_slots); the trace kernels below only for other shapes
         const int scap = std::max(cap, 1);
@@ -2193,6 +2203,11 @@ int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, con
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     return 0;
+}
+
+int taxi2_ncd_pairs(taxi2_ctx* ctx, int set_x, int set_y, const int64_t* xs, const int64_t* ys, int64_t count,
+                    const taxi2_scores* sc, int both, double* out) {
+    return ncd_pairs_impl(ctx, set_x, set_y, xs, ys, count, sc, both, out, true);
 }
 
 int taxi2_ncd_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_sy, const int32_t* d_slen, int64_t cap,
@@ -2415,7 +2430,7 @@ static int format_impl(taxi2_ctx* ctx, int mode, const double* vals, int64_t nro
     HIP_TRY(ctx, hipStreamSynchronize(fst));
     int64_t total = 0;
     for (int64_t b = 0; b < nblk; ++b) {
-        if (rlen[b] >= ((int64_t)1 << 60))
+        if (rlen[b] >= FMT_OVERSIZE)
             return fail(ctx, "a value of row %lld is too large for fixed-point text with %d decimals",
                         (long long)(b / nch), decimals);
         rbase[b] = total;

@@ -147,16 +147,22 @@ __device__ __forceinline__ void fmt_token_at(const FmtArgs& a, int64_t r, int64_
     }
 }
 
+// A token holding a value too large for fixed-point text adds FMT_OVERSIZE to its length, once: a
+// chunk's sum (<= FMT_BLOCK tokens) stays below 2^63 and at or above FMT_OVERSIZE, which the host
+// reports as an error.  Real token lengths stay far below it.
+constexpr int64_t FMT_OVERSIZE = (int64_t)1 << 40;
+
 __device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, int64_t t, int64_t nt) {
     int64_t g, c;
     fmt_token_at(a, r, t, g, c);
     const double* v = a.vals + g * a.vstride;
     int64_t len = 0;
+    bool over = false;
     if (a.mode != 1) {
         len = (a.row_offs[r + 1] - a.row_offs[r]) + 1 + (a.col_offs[c + 1] - a.col_offs[c]) + 1;  // + '\n'
         for (int m = 0; m < a.nm; ++m) {
             len += 1 + (fmt_defined(v[m]) ? fmt_fixed(v[m], a.decimals, nullptr) : a.missing_len);
-            if (fmt_defined(v[m]) && !(__builtin_fabs(v[m]) < a.vlim)) len += (int64_t)1 << 60;
+            if (fmt_defined(v[m]) && !(__builtin_fabs(v[m]) < a.vlim)) over = true;
         }
         if (a.mode == 2)
             len += fmt_span(a.rsuf_offs, 2 * r) + fmt_span(a.csuf_offs, 2 * c) + fmt_span(a.rsuf_offs, 2 * r + 1) +
@@ -164,10 +170,10 @@ __device__ __forceinline__ int64_t fmt_token_len(const FmtArgs& a, int64_t r, in
     } else {
         if (t == 0) len += a.row_offs[r + 1] - a.row_offs[r];
         len += 1 + (fmt_defined(v[0]) ? fmt_fixed(v[0], a.decimals, nullptr) : a.missing_len);
-        if (fmt_defined(v[0]) && !(__builtin_fabs(v[0]) < a.vlim)) len += (int64_t)1 << 60;
+        if (fmt_defined(v[0]) && !(__builtin_fabs(v[0]) < a.vlim)) over = true;
         if (t == nt - 1) len += 1;
     }
-    return len;
+    return over ? len + FMT_OVERSIZE : len;
 }
 
 __device__ __forceinline__ void fmt_token_write(const FmtArgs& a, int64_t r, int64_t t, int64_t nt, char* o) {
