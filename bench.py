@@ -175,6 +175,11 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--secondary", default="allmetrics,config4,task,config5,config5_aligned,prealigned",
                     help="secondary legs after the headline (one GPU only; bench_secondary.py); '' = none")
+    ap.add_argument("--dist-legs", default="config5",
+                    help="legs every rank runs together after the headline when N > 1 (config5: BASELINE "
+                         "configs[4] sharded over the ranks); '' = none")
+    ap.add_argument("--dist-timeout", type=float, default=900.0,
+                    help="seconds the N > 1 legs may take before they are reported as timed out")
     return ap.parse_args()
 
 
@@ -261,6 +266,9 @@ def main() -> None:
         del out, scores
         torch.cuda.empty_cache()
         secondary = bench_secondary.run_all(eng, seqset, N_SEQS, legs)
+    dist_legs = None
+    if world > 1 and args.dist_legs:  # every rank, after the timed region and the CPU baseline
+        dist_legs = run_dist_legs(args, eng, world, rank)
     from taxi2_amd._native import build_info
 
     build = build_info()
@@ -308,6 +316,7 @@ def main() -> None:
             "ceilings": ceilings(value / world, traffic, B, compute),
             "cpu_baseline": cpu,
             "secondary": secondary,
+            "dist_legs": dist_legs,
             "build": build,
             "assumptions": [
                 "Biopython 1.85's tie order among equal-scoring alignments is restated (end state M>Ix>Iy, "
@@ -319,7 +328,39 @@ def main() -> None:
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        if dist_legs and dist_legs.get("timed_out"):
+            # a collective left hanging: the line is out, leave without the group's teardown
+            sys.stdout.flush()
+            os._exit(0)
         dist.destroy_process_group()
+
+
+def run_dist_legs(args, eng, world: int, rank: int) -> dict:
+    """The N > 1 legs (bench_secondary.py leg_config5_dist), on every rank, in a worker thread with a
+    deadline: a collective that never completes is reported as timed out instead of holding the
+    headline line back (the ranks then exit without the process group's teardown)."""
+    import threading
+
+    import bench_secondary
+
+    out: dict = {}
+
+    def work():
+        for name in [x for x in args.dist_legs.split(",") if x]:
+            try:
+                if name == "config5":
+                    out[name] = bench_secondary.leg_config5_dist(eng, world, rank)
+                else:
+                    out[name] = {"error": f"unknown distributed leg {name}"}
+            except Exception as e:  # a failing leg never takes the headline line with it
+                out[name] = {"error": f"{type(e).__name__}: {e}"}
+
+    th = threading.Thread(target=work, daemon=True)
+    th.start()
+    th.join(args.dist_timeout)
+    if th.is_alive():
+        out["timed_out"] = True
+    return out
 
 
 NORTH_STAR_PER_GPU = 1e8 / 8          # BASELINE.json north_star: >= 1e8 aligned pairs/s on 8 x MI355X

@@ -164,6 +164,58 @@ def leg_config5(eng, n: int = 200_000, L: int = 1000) -> dict:
     }
 
 
+def timed_dist_task(start, timings, world: int, rank: int, sync=None, device=None) -> dict:
+    """Time one collective task run on every rank the way bench.py times its headline: barrier and
+    device sync on both sides, the slowest rank's wall time; the task's own phase times (its
+    ``timings()`` dict) are reduced to their maximum over ranks, so ``comm_s`` -- the rank-to-rank
+    state passing and the row-minima gather of the streamed path -- is reported apart from
+    ``compute_s``."""
+    import torch
+    import torch.distributed as dist
+
+    if sync:
+        sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    res = start()
+    if sync:
+        sync()
+    local = time.perf_counter() - t0
+    dist.barrier()
+    ph = dict(timings() or {})
+    keys = ("comm_s", "compute_s", "reduce_s")
+    v = torch.tensor([local] + [float(ph.get(k, 0.0) or 0.0) for k in keys], dtype=torch.float64, device=device)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    out = {"wall_s": float(v[0]), "n_ranks": world}
+    out.update({k + "_max": float(x) for k, x in zip(keys, v[1:].tolist())})
+    out["seconds_taken_rank0"] = getattr(res, "seconds_taken", None) if rank == 0 else None
+    return out
+
+
+def leg_config5_dist(eng, world: int, rank: int, n: int = 200_000, L: int = 1000) -> dict:
+    """BASELINE.json configs[4] on every GPU of the run: VersusAll.start() on 200 000 x 1 000 pre-aligned
+    rows under torch.distributed (one process per GPU).  The streamed path shards the rows by rank
+    (versus_all.py _stream_rows: row blocks computed on each rank's GPU, the subset statistics'
+    state passed rank to rank, the row minima gathered to rank 0 -- RCCL point-to-point and gather
+    over xGMI), p / jc / k2p x100, row minima + 2-genus / ~1 000-species subset statistics.  Strong
+    scaling: the whole job is fixed as the ranks grow."""
+    import torch
+
+    _log(f"config5_dist: rank {rank}/{world}: building {n} x {L} pre-aligned rows")
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as tmp:
+        task, _, _ = build_config5_task(n, L, eng, Path(tmp), 2.0)
+        _log(f"config5_dist: rank {rank}: VersusAll.start()")
+        rec = timed_dist_task(task.start, lambda: task.timings, world, rank, sync=torch.cuda.synchronize,
+                              device=torch.device("cuda", torch.cuda.current_device()))
+    rec.update({
+        "workload": f"config5 on {world} GPUs: VersusAll.start() on {n} x {L} pre-aligned synthetic rows (seed "
+                    f"0x7A14), p/jc/k2p x100, row minima + 2-genus / ~1 000-species subset statistics, rows "
+                    f"sharded by rank, statistics state passed rank to rank, row minima gathered to rank 0",
+        "n_seqs": n, "ordered_pairs": n * n, "ordered_pairs_per_s": n * n / rec["wall_s"], "scaling": "strong",
+    })
+    return rec
+
+
 def leg_config5_aligned(eng, n: int = 12_000, L: int = 1000) -> dict:
     """Config 5's aligned (NW / Gotoh) form on a stated subset ("Run NW on a stated
     tile subset"): VersusAll.start() on N = 12 000 sequences of the config-5 generator (seed 0x7A14,

@@ -46,24 +46,43 @@ def shard_pairs(n: int, world: int) -> list[tuple[int, int]]:
     return out
 
 
-def gather_blocks(local: np.ndarray, counts: list[int], group=None, device=None) -> np.ndarray:
-    """All-gather variable-length leading-dim blocks; returns the concatenation in rank order.
+def gather_blocks(local, counts: list[int], group=None, device=None, dst: int | None = None):
+    """Gather variable-length leading-dim blocks in rank order.
 
-    ``local`` has shape (counts[rank], ...).  Uses torch.distributed (the default group's
-    backend: nccl = RCCL on ROCm GPUs, gloo on CPU)."""
+    ``local`` has shape (counts[rank], ...): a numpy array, or a torch tensor already on the
+    collective's device (no host round trip).  Uses torch.distributed (the default group's backend:
+    nccl = RCCL on ROCm GPUs, gloo on CPU).  RCCL has no variable-size gather, so blocks are padded to
+    the largest one.  dst None: every rank receives the concatenation (all-gather); dst = r: only rank
+    r does (a gather: the other ranks return None and receive nothing)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     pad = max(counts) if counts else 0
-    tail = local.shape[1:]
-    buf = np.zeros((pad,) + tail, dtype=local.dtype)
-    buf[: local.shape[0]] = local
-    t = torch.from_numpy(buf)
-    if device is not None:
-        t = t.to(device)
-    outs = torch.empty((world * pad,) + tuple(tail), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(outs, t, group=group)
+    if isinstance(local, torch.Tensor):
+        t = local if device is None else local.to(device)
+        tail = tuple(t.shape[1:])
+        if t.shape[0] != pad:
+            tp = torch.zeros((pad,) + tail, dtype=t.dtype, device=t.device)
+            tp[: t.shape[0]] = t
+            t = tp
+    else:
+        tail = tuple(local.shape[1:])
+        buf = np.zeros((pad,) + tail, dtype=local.dtype)
+        buf[: local.shape[0]] = local
+        t = torch.from_numpy(buf)
+        if device is not None:
+            t = t.to(device)
+    if dst is None:
+        outs = torch.empty((world * pad,) + tail, dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(outs, t, group=group)
+    else:
+        parts = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+        dist.gather(t, gather_list=parts, dst=dst, group=group)
+        if rank != dst:
+            return None
+        outs = torch.cat(parts, dim=0)
     outs = outs.cpu().numpy().reshape((world, pad) + tail)
     return np.concatenate([outs[r, : counts[r]] for r in range(world)], axis=0)
 

@@ -1124,13 +1124,14 @@ class VersusAll:
                     if rank == 0:
                         sink.recv_state(world - 1, comm)
                     t = tick("comm_s", t)
-                if sink.rmin_k is not None:
+                if sink.rmin_k is not None:  # the row minima to rank 0, which writes them (a gather)
                     lo, hi = r0, r1
                     loc = np.stack([sink.rmin_idx[lo:hi].astype(np.float64), sink.rmin_d[lo:hi]], axis=1)
                     allr = gather_blocks(loc, [b - a for a, b in rows],
-                                         device=comm if backend == "nccl" else None)
-                    sink.rmin_idx[:] = allr[:, 0].astype(np.int64)
-                    sink.rmin_d[:] = allr[:, 1]
+                                         device=comm if backend == "nccl" else None, dst=0)
+                    if rank == 0:
+                        sink.rmin_idx[:] = allr[:, 0].astype(np.int64)
+                        sink.rmin_d[:] = allr[:, 1]
                     tick("comm_s", t)
             if overlap:
                 for rs in reds:

@@ -13,6 +13,7 @@ import sys
 import textwrap
 
 import numpy as np
+import pytest
 
 from tests.conftest import ROOT
 
@@ -116,3 +117,50 @@ def test_shard_range_covers():
         for w in (1, 2, 3, 8):
             b = shard_range(n, w)
             assert b[0][0] == 0 and b[-1][1] == n and all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+
+
+GATHER_WORKER = textwrap.dedent(
+    """
+    import os, sys
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, {root!r})
+    from taxi2_amd.sharding import gather_blocks, shard_range
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    rows = shard_range(23, world)
+    lo, hi = rows[rank]
+    loc = np.stack([np.arange(lo, hi, dtype=np.float64), -np.arange(lo, hi, dtype=np.float64)], axis=1)
+    got = gather_blocks(loc, [b - a for a, b in rows], dst=0)              # numpy, to rank 0 only
+    got_t = gather_blocks(torch.from_numpy(loc), [b - a for a, b in rows], dst=world - 1)  # a tensor, to the last rank
+    np.save(os.environ["OUT"] + f".{{rank}}.npy", np.array([got is None, got_t is None]))
+    if got is not None:
+        np.save(os.environ["OUT"] + ".g0.npy", got)
+    if got_t is not None:
+        np.save(os.environ["OUT"] + ".gl.npy", got_t)
+    dist.destroy_process_group()
+    """
+)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_blocks_to_one_rank_gloo(tmp_path, world):
+    """gather_blocks(dst=r) (the streamed path's row minima): only rank r receives the
+    rank-ordered concatenation; numpy and tensor inputs alike."""
+    script = tmp_path / "gather.py"
+    script.write_text(GATHER_WORKER.format(root=str(ROOT)))
+    out = tmp_path / "g"
+    env = dict(os.environ, OUT=str(out), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    q = np.arange(23, dtype=np.float64)
+    exp = np.stack([q, -q], axis=1)
+    assert np.array_equal(np.load(str(out) + ".g0.npy"), exp)
+    assert np.array_equal(np.load(str(out) + ".gl.npy"), exp)
+    for k in range(world):
+        none0, nonel = np.load(str(out) + f".{k}.npy")
+        assert none0 == (k != 0) and nonel == (k != world - 1)
