@@ -173,6 +173,36 @@ constexpr uint32_t AR_NOBAND = 0x0080u;  // lo 128, width 0: no lane stores
 // same values as before; only the stored best is shifted.
 constexpr int AR_EQ_MATCH = 3, AR_EQ_MISMATCH = 1, AR_CO_I = -7, AR_CO_E = 0;
 
+// The fill's constants for Gotoh scores with ONE extend for internal and end gaps (ie == ee; the
+// host admits such sets through ar_scores_ok): drift dz = ie, substitution s - 2 ie, opens relative
+// to the extend co_i = io - ie, co_e = eo - ee.  Under such scores the column-0 and row-0 boundaries
+// are B(i, 0) = B(0, j) = co_e (i, j >= 1) and B(0, 0) = 0 in drift coordinates; the default scores
+// (co_e = 0) make them one flat 0.  DEF kernels use the constant default set (folded by the compiler).
+struct ArSc {
+    int eqm, eqx, coi, coe;  // match / mismatch substitution in drift coordinates, the two opens
+    int ma, mi, io, ie, eo, ee;
+};
+__host__ __device__ constexpr ArSc ar_sc(int ma, int mi, int io, int ie, int eo, int ee) {
+    return ArSc{ma - 2 * ie, mi - 2 * ie, io - ie, eo - ee, ma, mi, io, ie, eo, ee};
+}
+constexpr ArSc AR_DEFAULT = ar_sc(1, -1, -8, -1, -1, -1);  // align.py:20-27
+static_assert(AR_DEFAULT.eqm == AR_EQ_MATCH && AR_DEFAULT.eqx == AR_EQ_MISMATCH && AR_DEFAULT.coi == AR_CO_I &&
+                  AR_DEFAULT.coe == AR_CO_E,
+              "default constants");
+// Scores k_alignr takes besides the defaults: one extend (the drift), every open no better than its
+// extend (the best-open recurrences), scores within +-12 (the int8 raw trace, alignt2_kernel.hpp),
+// an internal open no better than the end open relative to their extend (co_i <= co_e: the
+// pre-columns then reproduce the column-0 boundary, see the first-row reset), and every stored value
+// of an L-column fill inside the normal f16 range the best state's v_pk_maximum3_f16 needs (BIAS16:
+// drift-coordinate values in [-19 456, 11 263]; the -16 384 sentinel sits below every real value).
+__host__ __device__ inline bool ar_scores_ok(int ma, int mi, int io, int ie, int eo, int ee, int L) {
+    bool small = true;
+    for (const int v : {ma, mi, io, ie, eo, ee}) small = small && v >= -12 && v <= 12;
+    const ArSc S = ar_sc(ma, mi, io, ie, eo, ee);
+    return ie == ee && io <= ie && eo <= ee && small && S.coi <= S.coe &&
+           (long long)L * (S.eqm > 0 ? S.eqm : 0) + 64 <= 11000;
+}
+
 __device__ __forceinline__ uint32_t ar_pk_int(int lo, int hi) { return pk_int(pk2(lo, hi)); }
 
 // 8 bytes at any byte address (one unaligned global store)
@@ -194,16 +224,16 @@ __device__ __forceinline__ void ar_band_lanes(int i, int nA, int nB, int off, in
 }
 
 // the .z / .w words of a record: the row's open (pk_int) and B = 0 shifted by it (a biased pattern)
-__device__ __forceinline__ uint4 ar_record(uint32_t x, uint32_t y, bool last) {
-    const uint32_t o = last ? ar_pk_int(AR_CO_E, AR_CO_E) : ar_pk_int(AR_CO_I, AR_CO_I);
-    return make_uint4(x, y, o, pk2b(0, 0) + o);
+__device__ __forceinline__ uint4 ar_record(const ArSc& S, uint32_t x, uint32_t y, bool last) {
+    const uint32_t o = last ? ar_pk_int(S.coe, S.coe) : ar_pk_int(S.coi, S.coi);
+    return make_uint4(x, y, o, pk2b(S.coe, S.coe) + o);  // column 0: B(i, 0) = co_e (i >= 1)
 }
 
 template <int K, int W>
-__device__ __forceinline__ uint4 ar_row_record(const ArRow* __restrict__ tab, const ArChain& ch, int n, int rows, int g,
+__device__ __forceinline__ uint4 ar_row_record(const ArSc& S, const ArRow* __restrict__ tab, const ArChain& ch, int n, int rows, int g,
                                                int band) {
     constexpr int NT = 64 * W;
-    if (g < 0 || g >= rows) return ar_record(0u, AR_NOBAND, false);
+    if (g < 0 || g >= rows) return ar_record(S, 0u, AR_NOBAND, false);
     int t = 0;
     for (int q = 1; q < n; ++q)
         if (tab[q].r0 <= g) t = q;
@@ -227,14 +257,14 @@ __device__ __forceinline__ uint4 ar_row_record(const ArRow* __restrict__ tab, co
         hi = max(hi, u);
     }
     y |= hi < lo ? AR_NOBAND : ((uint32_t)lo | ((uint32_t)(hi - lo) << 8));
-    return ar_record(x, y, i == r.nA - 1);
+    return ar_record(S, x, y, i == r.nA - 1);
 }
 
 // <= 128 VGPRs: 4 waves per SIMD, so that the 5 workgroups of 3 waves the LDS allows fit a CU (the
 // launch bound alone lets the allocator take more and lose a workgroup per CU)
-template <int K, int W, int OCC>
+template <int K, int W, int OCC, bool DEF>
 __global__ void __launch_bounds__(64 * (W + 1), OCC) __attribute__((amdgpu_num_vgpr(128)))
-k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64_t total, int64_t npairs,
+k_alignr(SetView XS, SetView YS, KScores ksc, const ArSeg* __restrict__ segs, int nseg, int64_t total, int64_t npairs,
          MetricSpec ms, int chunk_req, int out_mode, double* __restrict__ out, int32_t* __restrict__ sout,
          uint8_t* __restrict__ trace, int64_t buf_bytes, int cap_rows, unsigned long long* __restrict__ next,
          int band, int64_t* __restrict__ esc_list, unsigned long long* __restrict__ esc_n, StrOut so,
@@ -242,8 +272,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
     static_assert(K % 2 == 0 && K <= 8 && W <= 2, "row-shared shapes: K <= 8 columns per lane, one or two fill waves");
     constexpr int NT = 64 * W;
     constexpr int XR = a1c_xr(W);
-    constexpr int dz = -1;                          // default scores: ie
-    const KScores sc{1, -1, -8, -1, -1, -1};        // align.py:20-27 defaults
+    // the scores' fill constants: the defaults folded in (DEF), else the launch's one-extend set
+    const ArSc S = DEF ? AR_DEFAULT : ar_sc(ksc.ma, ksc.mi, ksc.io, ksc.ie, ksc.eo, ksc.ee);
+    const int dz = S.ie;  // the drift
+    const KScores sc{S.ma, S.mi, S.io, S.ie, S.eo, S.ee};
     constexpr int NW = 4 * AR_UNITS;                // walks per chain (both orientations of 2 pairs per unit)
     __shared__ uint4 xinfo[XR];
     __shared__ ArRow tab[2][AR_UNITS];
@@ -390,6 +422,10 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
         int i = nA_ + 1, j = nB_ + 1;  // the virtual end cell, in M: its first move picks the end state
         uint32_t xa = 0u, yb = 0u;
         int valid = 0, ts = 0, tv = 0, gap = 0, nmc = 0, nmatch = 0, nio = 0, ncol = 0;
+        int nioe = 0;  // end-gap opens (generic scores only: the default end open scores 0)
+        // the Ix open of the end column and the Iy open of the last row (end gaps), the internal one
+        // elsewhere (uniform: scalar selects)
+        const int coe = S.coe, coi = S.coi;
         uint64_t wx = 0, wy = 0;  // string windows (column, row sequence): bits 0-7 = the last column produced
         bool first = true;        // the virtual end cell (uniform: every walk starts together)
         // Every lane runs the body every step (no per-lane region: its merge copies cost ~20 VALU a
@@ -438,8 +474,8 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             const int d1v = (int)(int8_t)(uint8_t)(nb >> bsh);          // M - Ix of (ni, nj)
             const int d2v = (int)(int8_t)(uint8_t)(nb >> (bsh + 16u));  // M - Iy
             // ---- the predecessor's state (first-path tie order), relative to its Ix
-            const int co = j == nB_ ? 0 : -7;  // Ix open of column j (end gap: eo - ee = 0)
-            const int oy = i == nA_ ? 0 : -7;  // Iy open of row i
+            const int co = j == nB_ ? coe : coi;  // Ix open of column j (end gap: eo - ee)
+            const int oy = i == nA_ ? coe : coi;  // Iy open of row i
             const int aX = isX ? co : 0;
             const int aY = isX ? co : isY ? -oy : 0;
             const int vM = d1v + aX, vY = d1v - d2v + aY;
@@ -450,6 +486,8 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
             // a gap run's open (its last move, walked backward): internal unless on an edge
             const bool en = isX ? (j == nB_ || j == 0) : (i == nA_ || i == 0);
             nio += !isM && nst != st && !en;
+            // (an end gap run reaching the origin is opened there: row 0 / column 0 of the fill)
+            if constexpr (!DEF) nioe += !isM && en && (nst != st || (ni | nj) == 0);
             const bool fin_now = alive && (ni | nj) == 0;
             const bool esc_now = alive && !fin_now && ni >= 1 && nj >= 1 && band > 0 && (uint32_t)(nj - ni - bdl) > bwd;
             if (fin_now || esc_now) {  // park the walk's outcome (no values leave this region)
@@ -459,7 +497,9 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 R.ts = ts;
                 R.tv = tv;
                 R.gap = gap;
-                R.sc2 = 2 * nmatch + nmc - 7 * nio;
+                // the path's score in drift coordinates: s - 2 ie per M column, one open per gap run
+                R.sc2 = DEF ? 2 * nmatch + nmc - 7 * nio
+                            : S.eqm * nmatch + S.eqx * (nmc - nmatch) + coi * nio + coe * nioe;
                 R.ncol = ncol;
                 if (fin_now && so.sx && (ncol & 7)) {  // the columns since the last window store
                     const size_t o8 = sbase + (size_t)(nA_ + nB_ - ncol);
@@ -498,8 +538,12 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                     if (so.slen) so.slen[p * so.nslot + (oslot & (so.nslot - 1))] = R.ncol;
                 }
             }
-            if (fst == AT_ESC)  // queue the pair (once) for the full-trace pass (k_alignt2_queued)
+            if (fst == AT_ESC) {  // queue the pair (once) for the full-trace pass (k_alignt2_queued)
                 if (atomicOr(&escf[pb][t][h], 1) == 0 && esc_list) esc_list[atomicAdd(esc_n, 1ull)] = p;
+                // a launch without that pass (esc_list null: band 0, so only a failed score check
+                // gets here) reports its results invalid through the host-mapped flag
+                if (!esc_list) __hip_atomic_fetch_or(pace_err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
         if (lane < NW) W_.st = AT_DONE;
     };
@@ -671,23 +715,32 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                         int s2[2];
 #pragma unroll
                         for (int hh = 0; hh < 2; ++hh)
-                            s2[hh] = (jr[hh] < 1 ? 0 : (cb[hh] == (uint32_t)"ACGT"[rb] ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
+                            s2[hh] = (jr[hh] < 1 ? 0 : (cb[hh] == (uint32_t)"ACGT"[rb] ? S.eqm : S.eqx)) - S.coi;
                         eqt[rb][k / EP][tid][k % EP] = ar_pk_int(s2[0], s2[1]);
                     }
                 }
             }
-            if (tid < 64) xinfo[tid] = ar_row_record<K, W>(tab[cur], ch, n, rows, tid, band);
-            else if (tid < 128) xinfo[XR - 128 + tid] = ar_record(0u, AR_NOBAND, false);
+            if (tid < 64) xinfo[tid] = ar_row_record<K, W>(S, tab[cur], ch, n, rows, tid, band);
+            else if (tid < 128) xinfo[XR - 128 + tid] = ar_record(S, 0u, AR_NOBAND, false);
             // lane's end-column Ix open (slot K - 1): the end-gap open in the half whose column nB_h
             // is this lane's last slot, the internal open elsewhere
             const int tq0 = w * 64 + lane;
             const int nbv0 = ch.nB[0] + ch.off[0], nbv1 = ch.nB[1] + ch.off[1];
-            const uint32_t cend = ar_pk_int((ch.nB[0] > 0 && tq0 == nbv0 / K - 1) ? AR_CO_E : AR_CO_I,
-                                            (ch.nB[1] > 0 && tq0 == nbv1 / K - 1) ? AR_CO_E : AR_CO_I);
+            const uint32_t cend = ar_pk_int((ch.nB[0] > 0 && tq0 == nbv0 / K - 1) ? S.coe : S.coi,
+                                            (ch.nB[1] > 0 && tq0 == nbv1 / K - 1) ? S.coe : S.coi);
             const int own0 = ch.nB[0] > 0 ? nbv0 / K - 1 : -1, own1 = ch.nB[1] > 0 ? nbv1 / K - 1 : -1;
-            const uint32_t COI = ar_pk_int(AR_CO_I, AR_CO_I);
-            const uint32_t GZ = pk2b(0, 0) + COI;  // B = 0 shifted by the internal open
-            const uint32_t cadj = cend - COI;      // the end column's Ix open over the internal one
+            const uint32_t COI = ar_pk_int(S.coi, S.coi);
+            // row 0 of a unit, shifted by the internal open (G = B + o_i): B(0, j) = co_e on every
+            // column but real column 0 (virtual column off_h), where B(0, 0) = 0; the pre-columns
+            // left of it hold co_e too, so that every pre-column keeps B(i, v) = co_e on the rows
+            // below (M = B(i - 1, v - 1) + 0, Ix and Iy lower as long as co_i <= co_e) and real
+            // column 0 carries the boundary B(i, 0) = co_e.  The default scores make it one flat 0.
+            const uint32_t GZ = pk2b(S.coe, S.coe) + COI;
+            const uint32_t cadj = cend - COI;  // the end column's Ix open over the internal one
+            // (lane 0 only) the slot holding real column 0 of each half (-1: off_h = 0, the
+            // boundary input itself) and the diagonal input of row 1 (B(0, virtual column 0))
+            const int z0 = ch.off[0] - 1, z1 = ch.off[1] - 1;
+            const uint32_t GZ0 = tq0 == 0 ? pk2b(ch.off[0] > 0 ? S.coe : 0, ch.off[1] > 0 ? S.coe : 0) + COI : GZ;
             uint32_t stG[K], stX[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -794,13 +847,23 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                 }
                 uint32_t* const eq = I.eq;
                 if (pre) {  // a unit's first or last row, or a byte other than A/C/G/T
-                    if (rec.y & AR_FIRST) {  // row 0 of the new pair: B = 0, Ix = -inf, diagonal B(0, j0 - 1) = 0
+                    if (rec.y & AR_FIRST) {  // row 0 of the new pair: B = co_e (0 at column 0), Ix = -inf
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
                             stG[k] = GZ;
                             stX[k] = NEG16X2;
                         }
-                        carry = GZ;
+                        carry = GZ0;  // the diagonal B(0, j0 - 1)
+                        if constexpr (!DEF) {
+                            if (tq == 0 && S.coe != 0) {  // the lane holding real column 0 (rare)
+                                const uint32_t g0 = pk2b(0, 0) + COI;
+#pragma unroll
+                                for (int k = 0; k < K; ++k) {
+                                    if (k == z0) stG[k] = (stG[k] & 0xFFFF0000u) | (g0 & 0xFFFFu);
+                                    if (k == z1) stG[k] = (stG[k] & 0xFFFFu) | (g0 & 0xFFFF0000u);
+                                }
+                            }
+                        }
                     }
                     if (rec.y & AR_OTHER) {  // byte compares against both halves' columns
                         const uint32_t rb = (rec.y >> 16) & 0xFFu;
@@ -810,7 +873,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 #pragma unroll
                             for (int hh = 0; hh < 2; ++hh) {
                                 const uint32_t cb = (colb[hh][k / 4] >> (8 * (k % 4))) & 0xFFu;
-                                s2[hh] = (((premask >> (8 * hh + k)) & 1u) ? 0 : (cb == rb ? AR_EQ_MATCH : AR_EQ_MISMATCH)) - AR_CO_I;
+                                s2[hh] = (((premask >> (8 * hh + k)) & 1u) ? 0 : (cb == rb ? S.eqm : S.eqx)) - S.coi;
                             }
                             eq[k] = ar_pk_int(s2[0], s2[1]);
                             __builtin_amdgcn_sched_barrier(0);  // one column at a time: few live values
@@ -925,7 +988,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
                                 break;
                             }
                         }
-                        if (stalled && lane == 0) __hip_atomic_store(pace_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (stalled && lane == 0) __hip_atomic_fetch_or(pace_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
 #ifdef AR_PROF
                     const unsigned long long t1 = AR_NOW();
@@ -954,7 +1017,7 @@ k_alignr(SetView XS, SetView YS, const ArSeg* __restrict__ segs, int nseg, int64
 #endif
                     if (w == 0 && (s1 & (INTERVAL - 1)) == 0) {  // the next 64 rows' records
                         const int gpre = s1 + lane;
-                        xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(tab[cur], ch, n, rows, gpre, band);
+                        xinfo[gpre & (XR - 1)] = ar_row_record<K, W>(S, tab[cur], ch, n, rows, gpre, band);
                     }
                     // publish (the ring / record writes above complete first: release)
                     // (a stalled wave publishes "done": its partner never waits on it again)

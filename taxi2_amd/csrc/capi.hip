@@ -166,8 +166,12 @@ int shared_release(taxi2_ctx* ctx, hipStream_t st) {
 // ctx->h_pace: its results are invalid.  Checked after the blocking entry points' synchronisation
 // and before the next row-shared launch (the *_dev calls' asynchronous launches report there).
 int pace_check(taxi2_ctx* ctx) {
-    if (ctx->h_pace && __atomic_load_n(ctx->h_pace, __ATOMIC_ACQUIRE)) {
+    const unsigned int e = ctx->h_pace ? __atomic_load_n(ctx->h_pace, __ATOMIC_ACQUIRE) : 0u;
+    if (e) {
         __atomic_store_n(ctx->h_pace, 0u, __ATOMIC_RELEASE);
+        if (e & 2u)  // (alignr_kernel.hpp: a launch with no queued pass, esc_list null)
+            return fail(ctx, "k_alignr: a walk failed its score check in a launch without a full-trace pass; "
+                             "the launch's results are invalid");
         return fail(ctx, "k_alignr: a fill wave's pacing wait exceeded its bound (AR_SPIN_CAP); the launch was "
                          "abandoned and its results are invalid");
     }
@@ -640,22 +644,24 @@ int launch_alignt_pairs(taxi2_ctx* ctx, const VariantT& v, const DevSet& X, cons
 }
 
 // ---------------------------------------------------------------- row-shared packed aligner
-// (alignr_kernel.hpp): default scores, triangle and rectangle launches up to 1 024 columns and rows.
+// (alignr_kernel.hpp): the default scores (constants folded in) and one-extend user sets
+// (ar_scores_ok), triangle and rectangle launches up to 1 024 columns and rows.
 struct VariantR {
     int K, W, occ;
+    bool def;
     const void* fn;
-    void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, const ArSeg*, int, int64_t, int64_t, MetricSpec, int,
+    void (*launch)(dim3, dim3, hipStream_t, SetView, SetView, KScores, const ArSeg*, int, int64_t, int64_t, MetricSpec, int,
                    int, double*, int32_t*, uint8_t*, int64_t, int, unsigned long long*, int, int64_t*,
                    unsigned long long*, StrOut, unsigned int*);
 };
 
-template <int K, int W, int OCC>
-void launch_alignr(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, const ArSeg* segs, int nseg, int64_t units,
-                   int64_t npairs, MetricSpec ms, int chunk, int om, double* out, int32_t* so, uint8_t* tr, int64_t bb,
-                   int cap, unsigned long long* nx, int band, int64_t* el, unsigned long long* en, StrOut str,
+template <int K, int W, int OCC, bool DEF>
+void launch_alignr(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, KScores k, const ArSeg* segs, int nseg,
+                   int64_t units, int64_t npairs, MetricSpec ms, int chunk, int om, double* out, int32_t* so, uint8_t* tr,
+                   int64_t bb, int cap, unsigned long long* nx, int band, int64_t* el, unsigned long long* en, StrOut str,
                    unsigned int* perr) {
-    hipLaunchKernelGGL((k_alignr<K, W, OCC>), g, b, 0, st, x, y, segs, nseg, units, npairs, ms, chunk, om, out, so, tr, bb,
-                       cap, nx, band, el, en, str, perr);
+    hipLaunchKernelGGL((k_alignr<K, W, OCC, DEF>), g, b, 0, st, x, y, k, segs, nseg, units, npairs, ms, chunk, om, out, so,
+                       tr, bb, cap, nx, band, el, en, str, perr);
 }
 
 // waves per SIMD the row-shared shapes are compiled for: LDS (~23.5 KB per workgroup of three waves)
@@ -663,8 +669,12 @@ void launch_alignr(dim3 g, dim3 b, hipStream_t st, SetView x, SetView y, const A
 #ifndef AR_OCC
 #define AR_OCC 5
 #endif
-#define T2_VARIANTR(K, W) VariantR{K, W, AR_OCC, (const void*)&k_alignr<K, W, AR_OCC>, &launch_alignr<K, W, AR_OCC>}
-const VariantR kAlignR[] = {T2_VARIANTR(4, 1), T2_VARIANTR(8, 1), T2_VARIANTR(6, 2), T2_VARIANTR(8, 2)};
+#define T2_VARIANTR(K, W, D) \
+    VariantR{K, W, AR_OCC, D, (const void*)&k_alignr<K, W, AR_OCC, D>, &launch_alignr<K, W, AR_OCC, D>}
+const VariantR kAlignR[] = {T2_VARIANTR(4, 1, true), T2_VARIANTR(8, 1, true), T2_VARIANTR(6, 2, true),
+                            T2_VARIANTR(8, 2, true)};
+const VariantR kAlignRG[] = {T2_VARIANTR(4, 1, false), T2_VARIANTR(8, 1, false), T2_VARIANTR(6, 2, false),
+                             T2_VARIANTR(8, 2, false)};
 
 static int64_t tri_row_host(int64_t g, int64_t N);
 
@@ -753,19 +763,26 @@ void build_segments(std::vector<RowIv>& rows, std::vector<ArSeg>& segs, int64_t&
 }
 
 const VariantR* pick_variantr(const KScores& k, const DevSet& X, const DevSet& Y, const PairSrc& ps) {
-    if (!is_default(k) || test_env("TAXI2_NO_ALIGNR") || test_env("TAXI2_NO_PACKED") || ps.sel) return nullptr;
+    if (test_env("TAXI2_NO_ALIGNR") || test_env("TAXI2_NO_PACKED") || ps.sel) return nullptr;
     if (ps.mode != PAIRS_TRI && ps.mode != PAIRS_RECT) return nullptr;
     if (X.max_len > 1024 || Y.max_len > 1024) return nullptr;  // the f16-maximum3 value range (BIAS16)
     // the walker addresses sequence bytes by 32-bit offsets from the sets' bases
     if (X.nbytes >= ((int64_t)1 << 32) || Y.nbytes >= ((int64_t)1 << 32)) return nullptr;
-    for (const auto& v : kAlignR)
-        if (64 * v.K * v.W >= X.max_len) return &v;
+    const bool def = is_default(k);
+    // user sets: one extend and best opens (the queued pass's kAlignT2R recurrences, bopen_ok), and
+    // their fill values in the f16 range at this length (ar_scores_ok)
+    if (!def && !(bopen_ok(k) && ar_scores_ok(k.ma, k.mi, k.io, k.ie, k.eo, k.ee, std::max(X.max_len, Y.max_len)) &&
+                  !test_env("TAXI2_NO_ALIGNR_GEN")))
+        return nullptr;
+    const VariantR* tab = def ? kAlignR : kAlignRG;
+    for (int i = 0; i < 4; ++i)
+        if (64 * tab[i].K * tab[i].W >= X.max_len) return &tab[i];
     return nullptr;
 }
 
 int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, const DevSet& Y, const PairSrc& ps,
                         const KScores& k, const MetricSpec& ms, int out_mode, double* d_out, int32_t* d_scores,
-                        hipStream_t st, StrOut str = StrOut{}) {
+                        hipStream_t st, StrOut str = StrOut{}, bool queue = true) {
     if (pace_check(ctx)) return -1;  // an earlier asynchronous launch failed
     // ---- segments of the launch's pairs (host), staged through a pinned buffer
     std::vector<RowIv> rows;
@@ -835,18 +852,27 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     // trace band: 2.5 sqrt(L) (80 at 1 000 bp: the widest measured excursion is 67; escapes requeue
     // exactly).  Narrower bands cut the trace writes (337 KB per pair at 80, 275 at 64) but the
     // requeued pairs' full-trace pass costs more than the writes save
-    int band = std::max(32, (int)std::ceil(2.5 * std::sqrt((double)max_len)));
+    // User one-extend sets take more paths off the diagonal at that width (1 000 bp, config 3: 5.4 %
+    // of generic1's pairs and 13.8 % of (1, -2, -4, -1, -2, -1)'s requeued at band 80): 3 sqrt(L) for
+    // them, 3.5 sqrt(L) when a mismatch scores no better than two gap columns (s - 2 ie <= 0 in drift
+    // coordinates: a pair of gap runs then replaces a run of mismatches for the two opens alone).
+    // Measured optima (tools/bench_scores.py, profiles/r6/scores/): 80 / 96 / 112.
+    const ArSc asc = ar_sc(k.ma, k.mi, k.io, k.ie, k.eo, k.ee);
+    const double bf = v.def ? 2.5 : asc.eqx > 0 ? 3.0 : 3.5;
+    int band = std::max(32, (int)std::ceil(bf * std::sqrt((double)max_len)));
     if (4 * band >= max_len) band = 0;
     if (const char* e = test_env("TAXI2_AT_BAND")) band = std::max(0, atoi(e));
-    // the queued pass (k_alignt2_queued over the launch's PairSrc, sign-digit full trace)
-    const VariantT* vq = pick_variantt2(k, max_len);
-    if (!vq) return fail(ctx, "no packed variant for the queued pass at length %d", max_len);
+    // the queued pass (k_alignt2_queued over the launch's PairSrc, sign-digit full trace); scores
+    // outside its 16-bit range (queue = false): no band, nothing to requeue
+    const VariantT* vq = queue ? pick_variantt2(k, max_len) : nullptr;
+    if (queue && !vq) return fail(ctx, "no packed variant for the queued pass at length %d", max_len);
+    if (!vq) band = 0;
     int per_cu_q = 0;
-    HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_q, vq->fn, 64 * (vq->W + 1), 0));
+    if (vq) HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_q, vq->fn, 64 * (vq->W + 1), 0));
     const int64_t grid_q = std::max<int64_t>(1, std::min<int64_t>(ps.count, (int64_t)ctx->num_cus * std::max(1, per_cu_q)));
     const int chunk_q = 2;  // one pair per stream: the queue is usually empty or a handful of pairs
     const int cap_rows_q = max_len;
-    const size_t bb_q = at_buf_bytes(cap_rows_q, 2 * vq->K, vq->W);
+    const size_t bb_q = vq ? at_buf_bytes(cap_rows_q, 2 * vq->K, vq->W) : 0;
 
     if (shared_acquire(ctx, st)) return -1;
     if (ensure(ctx, &ctx->d_trace, &ctx->d_trace_bytes, std::max((size_t)grid * 2 * bb, (size_t)grid_q * 2 * bb_q)))
@@ -860,14 +886,14 @@ int launch_alignr_pairs(taxi2_ctx* ctx, const VariantR& v, const DevSet& X, cons
     unsigned long long* esc_n = (unsigned long long*)((char*)ctx->d_work + 24);
     int64_t* esc_list = (int64_t*)((char*)ctx->d_work + 64);
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_work, 0, 64, st));
-    v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), (const ArSeg*)ctx->d_seg, (int)segs.size(),
+    v.launch(dim3((unsigned)grid), dim3(64 * (v.W + 1)), st, view(X), view(Y), k, (const ArSeg*)ctx->d_seg, (int)segs.size(),
              units, ps.count, ms, chunk, out_mode, d_out, d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb, cap_rows, next,
-             band, esc_list, esc_n, str, ctx->h_pace);
+             band, vq ? esc_list : nullptr, esc_n, str, ctx->h_pace);
     HIP_TRY(ctx, hipGetLastError());
     PairSrc p2 = ps;
     p2.sel = esc_list;
     p2.dcount = esc_n;
-    vq->launch(dim3((unsigned)grid_q), dim3(64 * (vq->W + 1)), st, view(X), view(Y), p2, k, ms, chunk_q, out_mode, d_out,
+    if (vq) vq->launch(dim3((unsigned)grid_q), dim3(64 * (vq->W + 1)), st, view(X), view(Y), p2, k, ms, chunk_q, out_mode, d_out,
                d_scores, (uint8_t*)ctx->d_trace, (int64_t)bb_q, cap_rows_q, 4096, next2, BandArgs{0, nullptr, nullptr}, str);
     HIP_TRY(ctx, hipGetLastError());
     if (test_env("TAXI2_AT_BAND_STATS")) {
@@ -990,11 +1016,12 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (!is_linear(k) && !test_env("TAXI2_NO_ALIGNT")) {
         // packed 16-bit fill when every difference fits int16 (TAXI2_NO_PACKED=1: 32-bit fill)
         const bool packed = at_fits16(k, max_len) && !test_env("TAXI2_NO_PACKED");
-        if (packed)
-            if (const VariantR* vr = pick_variantr(k, X, Y, ps)) {
-                if (ps.count <= 0) return 0;
-                return launch_alignr_pairs(ctx, *vr, X, Y, ps, k, ms, out_mode, d_out, d_scores, st);
-            }
+        // the row-shared aligner has its own value range (ar_scores_ok); when the packed queued pass's
+        // (at_fits16) is exceeded it stores the full trace and requeues nothing
+        if (const VariantR* vr = pick_variantr(k, X, Y, ps)) {
+            if (ps.count <= 0) return 0;
+            return launch_alignr_pairs(ctx, *vr, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, StrOut{}, packed);
+        }
         const VariantT* vt = packed ? pick_variantt2(k, max_len) : pick_variantt(k, max_len);
         if (vt) {
             if (ps.count <= 0) return 0;

@@ -1,5 +1,5 @@
 """GPU parity of the packed aligners' trace band (the row-shared k_alignr, alignr_kernel.hpp, for the
-default scores up to 1 024 columns; k_alignt2, alignt2_kernel.hpp a2_band_blocks, for the other
+default and one-extend scores up to 1 024 columns; k_alignt2, alignt2_kernel.hpp a2_band_blocks, for the other
 score sets and shapes; both requeue escapes to k_alignt2_queued's full-trace pass):
 the fill stores only the diagonal strip j - i in [min(0, nB - nA) - band, max(0, nB - nA) + band]
 of each pair's trace, a walk that would leave it queues the pair, and a second launch redoes the
@@ -47,7 +47,7 @@ def _queued(err: str) -> int:
 
 
 @pytest.mark.parametrize("band", ["8", "40", "default"])
-@pytest.mark.parametrize("scores", ["default", "generic"])
+@pytest.mark.parametrize("scores", ["default", "generic", "generic1"])
 def test_band_triangle(engine, oracle_c, capfd, band, scores):
     from taxi2_amd._native import tri_pairs
 

@@ -20,6 +20,7 @@
 #   peak             tools/valu_peak (SIMD cycles per wave64 instruction)
 #   d2h              tools/d2h_probe (device -> host text bandwidth: memcpy, 4 streams, kernel stores)
 #   tool:SCRIPT      python tools/SCRIPT.py (bench tools), e.g. tool:bench_long
+#   tooltrace:SCRIPT rocprofv3 --kernel-trace --stats of that tool
 #   sec:LEG          one bench_secondary.py leg alone (task, config5, config4, allmetrics)
 #   with:V=X,...:STEP  any step with those environment settings (outputs under the step's own names)
 #   secenv:NAME:LEG:V=X,...  that leg with those environment settings -> secenv_NAME.json
@@ -120,6 +121,9 @@ run_step() {
         timeout -k 10 120 "$R/tools/d2h_probe" > "$OUT/d2h_probe.txt" 2>&1 ;;
     tool:*)
         (cd "$R" && timeout -k 10 900 python3 -u "tools/${s#tool:}.py" > "$OUT/${s#tool:}.json" 2> "$OUT/${s#tool:}.err") ;;
+    tooltrace:*)  # rocprofv3 --kernel-trace --stats of python tools/SCRIPT.py
+        (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tooltrace_${s#tooltrace:}" -o run -- \
+            python3 "$R/tools/${s#tooltrace:}.py" > "$OUT/tooltrace_${s#tooltrace:}.json" 2> "$OUT/tooltrace_${s#tooltrace:}.err") ;;
     sec:*)
         # (sec:A+B+C: those legs one after another in one process, as bench.py runs them)
         (cd "$R" && timeout -k 10 600 python3 -u bench_secondary.py $(echo "${s#sec:}" | tr '+' ' ') > "$OUT/sec_${s#sec:}.json" 2> "$OUT/sec_${s#sec:}.err") ;;
