@@ -426,6 +426,12 @@ k_alignr(SetView XS, SetView YS, KScores ksc, const ArSeg* __restrict__ segs, in
         // the Ix open of the end column and the Iy open of the last row (end gaps), the internal one
         // elsewhere (uniform: scalar selects)
         const int coe = S.coe, coi = S.coi;
+        // linear gaps (io = ie, eo = ee: both opens 0 over the extend) take the reference's
+        // Needleman-Wunsch traceback (align.py:151-157 through Biopython's linear-gap algorithm;
+        // oracle/restatement.py _nw): at each cell the first of H, V, D (swapped: V, H, D) at the
+        // cell's maximum.  With zero opens the fill's Ix(i, j) = B(i - 1, j) and Iy(i, j) = B(i, j - 1)
+        // (B >= Ix, Iy), i.e. the NW candidates v and h, and D1 / D2 are d - v and d - h.
+        const bool lin = !DEF && coi == 0 && coe == 0;
         uint64_t wx = 0, wy = 0;  // string windows (column, row sequence): bits 0-7 = the last column produced
         bool first = true;        // the virtual end cell (uniform: every walk starts together)
         // Every lane runs the body every step (no per-lane region: its merge copies cost ~20 VALU a
@@ -482,6 +488,10 @@ k_alignr(SetView XS, SetView YS, KScores ksc, const ArSeg* __restrict__ segs, in
             const int vm = max(max(vM, vY), 0);
             const int alt = prio ? AT_IX + (vY == vm) : AT_IY - (vm == 0);  // Ix = 1, Iy = 2
             int nst = vM == vm ? AT_M : alt;
+            if (!DEF && lin) {  // linear gaps: the single-matrix move of (ni, nj), gaps before the diagonal
+                const int vv = -d1v, vh = -d2v, vb = max(max(vv, vh), 0);  // v - d, h - d, best - d
+                nst = prio ? (vv == vb ? AT_IX : vh == vb ? AT_IY : AT_M) : (vh == vb ? AT_IY : vv == vb ? AT_IX : AT_M);
+            }
             nst = ni == 0 ? AT_IY : nj == 0 ? AT_IX : nst;
             // a gap run's open (its last move, walked backward): internal unless on an edge
             const bool en = isX ? (j == nB_ || j == 0) : (i == nA_ || i == 0);

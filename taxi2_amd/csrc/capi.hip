@@ -1013,6 +1013,13 @@ int launch_align_pairs(taxi2_ctx* ctx, const DevSet& X, const DevSet& Y, const P
     if (mag * (2LL * max_len + 2) >= (1LL << 26))
         return fail(ctx, "score magnitudes too large for 32-bit DP at length %d", max_len);
     const int xcap = std::max(max_len, 1);
+    // linear gaps with one extend: the row-shared aligner, its walker in the single-matrix tie order;
+    // the full trace (no band: the queued pass, k_alignt2_queued, walks in the Gotoh order)
+    if (is_linear(k) && !test_env("TAXI2_NO_ALIGNT"))
+        if (const VariantR* vr = pick_variantr(k, X, Y, ps)) {
+            if (ps.count <= 0) return 0;
+            return launch_alignr_pairs(ctx, *vr, X, Y, ps, k, ms, out_mode, d_out, d_scores, st, StrOut{}, false);
+        }
     if (!is_linear(k) && !test_env("TAXI2_NO_ALIGNT")) {
         // packed 16-bit fill when every difference fits int16 (TAXI2_NO_PACKED=1: 32-bit fill)
         const bool packed = at_fits16(k, max_len) && !test_env("TAXI2_NO_PACKED");

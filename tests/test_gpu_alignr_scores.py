@@ -3,7 +3,8 @@
 Round 6 runs k_alignr for every score set with ONE extend for internal and end gaps whose opens are
 no better than the extend (the best-open recurrences, capi.hip bopen_ok), an internal open no better
 than the end open relative to the extend, and fill values inside the f16 range at the launch's
-length (alignr_kernel.hpp ar_scores_ok); other sets keep k_alignt2.  Each set here: alignment
+length (alignr_kernel.hpp ar_scores_ok); other sets keep k_alignt2.  Linear gaps (opens = extends)
+with one extend run it too, its walker in the reference's single-matrix tie order (full trace).  Each set here: alignment
 scores and metrics against the C oracle bit for bit (jc / k2p within 1e-12), the launch's kernel
 named by its band statistics line, the walked strings equal to the trace kernels', and -- at sizes
 the oracle would take minutes for -- the same launch through k_alignt2 (TAXI2_NO_ALIGNR_GEN=1).
@@ -34,6 +35,11 @@ SETS = {
     "ties": (1, 0, -2, -1, -1, -1),          # mismatch = 0, opens one below the extend: tie-heavy
     "big": (10, -10, -10, -6, -10, -6),      # eqm = 22: k_alignr up to 497 columns only
     "end_open_worse": (2, -1, -3, -3, -12, -3),  # co_i = 0 > co_e = -9: k_alignt2
+    # linear gaps with one extend: k_alignr with the single-matrix (Needleman-Wunsch) tie order
+    "linear1": (1, -1, -2, -2, -2, -2),
+    "linear_ties": (1, 0, -1, -1, -1, -1),
+    "linear2": (2, -3, -3, -3, -3, -3),
+    "linear_two_extends": (1, -1, -2, -2, -1, -1),  # ie != ee: k_align
 }
 
 
@@ -47,13 +53,13 @@ def _fits16(sc, length: int) -> bool:
 
 
 def alignr_eligible(sc, length: int) -> bool:
-    """capi.hip pick_variantr's choice restated: no linear gaps, bopen_ok (ie == ee, opens <=
+    """capi.hip pick_variantr's choice restated: no linear gaps with two extends, bopen_ok (ie == ee, opens <=
     extends) and alignr_kernel.hpp ar_scores_ok.  (Past the packed queued pass's range, _fits16,
     k_alignr stores the full trace and requeues nothing.)"""
     ma, mi, io, ie, eo, ee = sc
     if sc == (1, -1, -8, -1, -1, -1):
         return True
-    if io == ie and eo == ee:  # linear gaps: k_align (capi.hip is_linear)
+    if io == ie and eo == ee and ie != ee:  # linear gaps, two extends: k_align (capi.hip is_linear)
         return False
     small = all(-12 <= v <= 12 for v in sc)
     eqm = ma - 2 * ie
@@ -141,7 +147,7 @@ def test_alignr_scores_full_trace_without_queue(engine, oracle_c, capfd, length)
     st.free()
 
 
-@pytest.mark.parametrize("name", ["generic1", "equal_opens", "ties"])
+@pytest.mark.parametrize("name", ["generic1", "equal_opens", "ties", "linear1", "linear_ties"])
 def test_alignr_scores_rectangle(engine, oracle_c, name):
     sc = SETS[name]
     q = _tie_heavy(7, 600, 0x330) + ["", "C"]
@@ -156,7 +162,7 @@ def test_alignr_scores_rectangle(engine, oracle_c, name):
     rs.free()
 
 
-@pytest.mark.parametrize("name", ["generic1", "free_ends"])
+@pytest.mark.parametrize("name", ["generic1", "free_ends", "linear1"])
 @pytest.mark.parametrize("band", ["6", "default"])
 def test_alignr_scores_narrow_band(engine, oracle_c, name, band):
     """Escapes from a narrow trace band requeue to the full-trace pass under user scores too."""
