@@ -50,7 +50,7 @@ int main() {
         hipEventSynchronize(e1);
         printf("4 streams       : %.1f GB/s\n", bytes / ms_since(e0, e1) / 1e6);
     }
-    for (int grid : {256, 1024, 4096}) {
+    for (int grid : {8, 16, 32, 64, 128, 256, 1024, 4096}) {
         hipEventRecord(e0, s[0]);
         hipLaunchKernelGGL(k_copy, dim3(grid), dim3(256), 0, s[0], (const uint4*)d, (uint4*)h, bytes / 16);
         hipEventRecord(e1, s[0]);
