@@ -270,6 +270,27 @@ int taxi2_pack_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_s
                          int nslot, int slot, const int64_t* d_end, const int64_t* d_off, int64_t count, uint8_t* d_dx,
                          uint8_t* d_dy, void* stream);
 
+/* A stream of the context's device whose kernels run only on compute units
+ * [cu_first, cu_first + cu_count) (hipExtStreamCreateWithCUMask; logical CU numbers, which the
+ * driver stripes over the XCDs).  Two such streams over disjoint ranges keep a persistent fill
+ * launch and the text kernels of the task pipeline on separate CUs (versus_all.py:746-769: the
+ * aligned_pairs.txt writer beside the alignments) instead of sharing every CU's issue slots.
+ * *out_stream receives the hipStream_t; destroy it with taxi2_stream_destroy. */
+int taxi2_stream_create_cus(taxi2_ctx* ctx, int cu_first, int cu_count, void** out_stream);
+int taxi2_stream_destroy(taxi2_ctx* ctx, void* stream);
+/* Number of compute units of the context's device. */
+int taxi2_num_cus(taxi2_ctx* ctx);
+/* How the pair-text entry points (taxi2_format_pairs_dev / _ptr_dev) move the text into a pinned
+ * host buffer: 0 = the text kernel stores straight into it (default), 1 = the text kernel writes
+ * device memory and one DMA copy moves it (no CUs), 2 = the same with a 16-byte copy kernel.  The
+ * text bytes are identical in every mode. */
+int taxi2_set_text_copy(taxi2_ctx* ctx, int mode);
+/* d_src[0, nbytes) (device) -> h_dst (pinned host memory), asynchronous on `stream`: a copy kernel of
+ * 16-byte stores (the rate of kernel stores over the host link, beside a running fill), or the DMA
+ * engine when either side is not 16-byte aligned.  The task pipeline's text transfer
+ * (versus_all.py:746-750, aligned_pairs.txt). */
+int taxi2_copy_text_dev(taxi2_ctx* ctx, const uint8_t* d_src, uint8_t* h_dst, int64_t nbytes, void* stream);
+
 /* NCD of aligned-string slots already on the device -- taxi2_tri_strings_dev (nslot 2) or
  * taxi2_rect_strings_dev (nslot 1) output: pair k's alignment of orientation o is the last
  * d_slen[k * nslot + o] bytes before byte d_end[k] of slot k * nslot + o (cap bytes each).

@@ -46,6 +46,11 @@ EXPORTS = (
     "taxi2_format_pairs_ptr_dev",
     "taxi2_format_pairs_ptr_async",
     "taxi2_pack_slots_dev",
+    "taxi2_stream_create_cus",
+    "taxi2_stream_destroy",
+    "taxi2_num_cus",
+    "taxi2_set_text_copy",
+    "taxi2_copy_text_dev",
     "taxi2_list_pairs",
     "taxi2_closest",
     "taxi2_align_strings",
@@ -152,6 +157,11 @@ _SIGNATURES = {
     "taxi2_format_pairs_ptr_dev": (_INT, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _INT, _P, _I64,
                                           ctypes.POINTER(_I64), _P]),
     "taxi2_pack_slots_dev": (_INT, [_P, _P, _P, _P, _I64, _INT, _INT, _P, _P, _I64, _P, _P, _P]),
+    "taxi2_stream_create_cus": (_INT, [_P, _INT, _INT, ctypes.POINTER(_P)]),
+    "taxi2_stream_destroy": (_INT, [_P, _P]),
+    "taxi2_num_cus": (_INT, [_P]),
+    "taxi2_set_text_copy": (_INT, [_P, _INT]),
+    "taxi2_copy_text_dev": (_INT, [_P, _P, _P, _I64, _P]),
     "taxi2_list_pairs": (_INT, [_P, _INT, _INT, _P, _P, _I64, ctypes.POINTER(CScores), _P, _INT, _P, _P]),
     "taxi2_closest": (_INT, [_P, _INT, _INT, _I64, _I64, ctypes.POINTER(CScores), _I32, ctypes.c_double,
                              _P, _INT, _P, _P, _P, _P]),
@@ -580,6 +590,37 @@ class Engine:
                     ctypes.c_void_p(dx_ptr), ctypes.c_void_p(dy_ptr), ctypes.c_void_p(stream)),
                 "taxi2_pack_slots_dev",
             )
+
+    def num_cus(self) -> int:
+        """Compute units of the engine's device (taxi2_num_cus)."""
+        return int(self._lib.taxi2_num_cus(self._ctx))
+
+    def cu_stream(self, cu_first: int, cu_count: int) -> int:
+        """A raw hipStream_t whose kernels run only on CUs [cu_first, cu_first + cu_count)
+        (taxi2_stream_create_cus); wrap it with torch.cuda.ExternalStream, release it with
+        destroy_stream once its work is done."""
+        out = _P()
+        with self._lock:
+            self._check(self._lib.taxi2_stream_create_cus(self._ctx, int(cu_first), int(cu_count), ctypes.byref(out)),
+                        "taxi2_stream_create_cus")
+        return int(out.value)
+
+    def set_text_copy(self, mode: int) -> None:
+        """Pair-text transfer into pinned memory (taxi2_set_text_copy): 0 kernel stores, 1 device
+        buffer + DMA, 2 device buffer + 16-byte copy kernel; the bytes are the same."""
+        with self._lock:
+            self._check(self._lib.taxi2_set_text_copy(self._ctx, int(mode)), "taxi2_set_text_copy")
+
+    def copy_text_dev(self, src_ptr: int, dst_ptr: int, nbytes: int, stream: int) -> None:
+        """Device bytes -> pinned host bytes on ``stream`` (taxi2_copy_text_dev, asynchronous)."""
+        with self._lock:
+            self._check(self._lib.taxi2_copy_text_dev(self._ctx, ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr),
+                                                      int(nbytes), ctypes.c_void_p(stream)), "taxi2_copy_text_dev")
+
+    def destroy_stream(self, stream: int) -> None:
+        """Synchronise and destroy a stream from cu_stream (taxi2_stream_destroy)."""
+        with self._lock:
+            self._check(self._lib.taxi2_stream_destroy(self._ctx, ctypes.c_void_p(stream)), "taxi2_stream_destroy")
 
     def format_pairs_ptr_dev(self, nrows: int, ncols: int, px_ptr: int, py_ptr: int, slen_ptr: int, row_ids, col_ids,
                              *, first: bool, stream: int | None = None) -> memoryview:

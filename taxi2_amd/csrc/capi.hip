@@ -73,6 +73,7 @@ struct taxi2_ctx {
     int num_cus = 0;
     size_t total_mem = 0;  // device memory (bytes)
     int reserve_cus = 0;  // packed aligner launches leave this many CUs' worth of workgroups free
+    int text_copy = 0;    // pair text into pinned host memory: 0 kernel stores, 1 HBM + DMA, 2 HBM + copy kernel
     hipStream_t stream = nullptr;
     std::string err;
     std::vector<DevSet> sets;
@@ -2528,12 +2529,23 @@ int format_pairs_impl(taxi2_ctx* ctx, int64_t nrows, int64_t ncols, PairFmtArgs 
     if (total > out_cap) return 1;  // caller retries with a buffer of *out_len bytes
     if (!out) return fail(ctx, "null output buffer");
     char* mapped = host_mapped(out);
-    if (!mapped && ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 1)) return -1;
+    // text_copy 1 / 2: the text kernel writes HBM (its byte stores at every pair's unaligned ends
+    // stay on the device) and one linear copy moves it: the DMA engine (no CUs), or a copy kernel
+    // of 16-byte stores from a 16-aligned destination (only the last partial word by bytes)
+    const int mode = mapped ? (ctx->text_copy == 2 && ((uintptr_t)mapped & 15u) ? 1 : ctx->text_copy) : 1;
+    if (mode && ensure(ctx, &ctx->d_out, &ctx->d_out_bytes, (size_t)total + 16)) return -1;
     HIP_TRY(ctx, hipMemcpyAsync(d_rbase, rbase.data(), nblk * 8, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_pairs_text, dim3((unsigned)nblk), dim3(FMT_BLOCK), 0, st, a, (int)nch, d_rbase,
-                       mapped ? mapped : (char*)ctx->d_out);
+                       mode ? (char*)ctx->d_out : mapped);
     HIP_TRY(ctx, hipGetLastError());
-    if (!mapped) HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, st));
+    if (mode == 1) {
+        HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_out, total, hipMemcpyDeviceToHost, st));
+    } else if (mode == 2) {
+        const int64_t n16 = total >> 4;
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 1024));
+        hipLaunchKernelGGL(k_copy_text, dim3((unsigned)blocks), dim3(256), 0, st, (const char*)ctx->d_out, mapped, total);
+        HIP_TRY(ctx, hipGetLastError());
+    }
     HIP_TRY(ctx, hipStreamSynchronize(st));
     return 0;
 }
@@ -2590,6 +2602,59 @@ int taxi2_pack_slots_dev(taxi2_ctx* ctx, const uint8_t* d_sx, const uint8_t* d_s
     hipLaunchKernelGGL(k_pack_slots, dim3((unsigned)blocks), dim3(256), 0, st, d_sx, d_sy, d_slen, cap, nslot, slot, d_end,
                        d_off, count, d_dx, d_dy);
     HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+int taxi2_stream_create_cus(taxi2_ctx* ctx, int cu_first, int cu_count, void** out_stream) {
+    if (!ctx) return -1;
+    if (!out_stream) return fail(ctx, "null output stream");
+    *out_stream = nullptr;
+    if (cu_first < 0 || cu_count < 1 || cu_first + cu_count > ctx->num_cus)
+        return fail(ctx, "CU range [%d, %d) outside the device's %d CUs", cu_first, cu_first + cu_count, ctx->num_cus);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<uint32_t> mask((ctx->num_cus + 31) / 32, 0u);
+    for (int c = cu_first; c < cu_first + cu_count; ++c) mask[c >> 5] |= 1u << (c & 31);
+    hipStream_t s = nullptr;
+    HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    *out_stream = (void*)s;
+    return 0;
+}
+
+int taxi2_stream_destroy(taxi2_ctx* ctx, void* stream) {
+    if (!ctx) return -1;
+    if (!stream) return 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(ctx, hipStreamDestroy((hipStream_t)stream));
+    return 0;
+}
+
+int taxi2_num_cus(taxi2_ctx* ctx) { return ctx ? ctx->num_cus : -1; }
+
+int taxi2_copy_text_dev(taxi2_ctx* ctx, const uint8_t* d_src, uint8_t* h_dst, int64_t nbytes, void* stream) {
+    if (!ctx) return -1;
+    if (nbytes < 0) return fail(ctx, "negative size");
+    if (nbytes == 0) return 0;
+    if (!d_src || !h_dst) return fail(ctx, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    char* mapped = host_mapped(h_dst);
+    if (!mapped) return fail(ctx, "taxi2_copy_text_dev: the destination is not pinned host memory");
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    const int64_t n16 = nbytes >> 4;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 1024));
+    if (((uintptr_t)mapped & 15u) || ((uintptr_t)d_src & 15u)) {  // the 16-byte copy needs both aligned
+        HIP_TRY(ctx, hipMemcpyAsync(h_dst, d_src, (size_t)nbytes, hipMemcpyDeviceToHost, st));
+        return 0;
+    }
+    hipLaunchKernelGGL(k_copy_text, dim3((unsigned)blocks), dim3(256), 0, st, (const char*)d_src, mapped, nbytes);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+int taxi2_set_text_copy(taxi2_ctx* ctx, int mode) {
+    if (!ctx) return -1;
+    if (mode < 0 || mode > 2) return fail(ctx, "text copy mode %d (0 kernel stores, 1 DMA, 2 copy kernel)", mode);
+    ctx->text_copy = mode;
     return 0;
 }
 

@@ -498,6 +498,18 @@ k_pairs_text(PairFmtArgs a, int nch, const int64_t* __restrict__ chunk_base, cha
     }
 }
 
+// Device text -> pinned host text: 16-byte loads and stores over the whole buffer (dst 16-aligned;
+// the link rate of kernel stores needs whole 16-byte writes, tools/d2h_probe), the last total % 16
+// bytes one per lane.
+__global__ void __launch_bounds__(256) k_copy_text(const char* __restrict__ src, char* __restrict__ dst, int64_t total) {
+    const int64_t n16 = total >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+        d4[i] = s4[i];
+    if (blockIdx.x == 0 && threadIdx.x < (total & 15)) dst[16 * n16 + threadIdx.x] = src[16 * n16 + threadIdx.x];
+}
+
 // Compaction of one orientation's aligned strings out of the walkers' slots (StrOut): pair k's
 // string is the last slen[k * nslot + slot] bytes before byte end[k] of its slot, copied to
 // dst + off[k].  One wave per pair, lanes striding over the bytes (coalesced loads and stores).

@@ -151,6 +151,16 @@ class VersusAll:
         # CUs' worth of workgroup slots the one-fill aligned_pairs path leaves free beside each
         # block's fill, for the previous block's text kernel (host-link bound: it needs few CUs)
         self.params.engine.text_reserve_cus = 32
+        # text_cu_mask: the fill and the text on disjoint CU ranges (CU-masked streams);
+        # text_copy: how the pair text reaches pinned host memory (0 kernel stores, 1 device buffer +
+        # DMA, 2 device buffer + 16-byte copy kernel; taxi2_set_text_copy)
+        self.params.engine.text_cu_mask = False
+        self.params.engine.text_copy = 0
+        # text_pipeline "fused": each block's compaction and text queued on the fill stream behind
+        # its fill (whole chip, ~1 ms per GB), the text moved to the host beside the next fills by
+        # the DMA engine (text_copy 1) or a copy kernel (2), no CUs reserved; "streams": the text
+        # kernels on a second stream beside the fills, in text_reserve_cus CUs (round 5)
+        self.params.engine.text_pipeline = "fused"
         self.params.engine.stream = None
         self.params.engine.dense_limit = 4 << 30
         self.params.engine.block_bytes = 256 << 20
@@ -304,6 +314,55 @@ class VersusAll:
         return D
 
     def _tri_with_pairs(self, seqs, eng, st, D, cidx, clabels, scores, fh) -> bool:
+        """_tri_with_pairs_on with its two streams.  With text_reserve_cus = R > 0 the fill stream
+        runs on CUs [R, num_cus) and the text stream on CUs [0, R) (taxi2_stream_create_cus): the
+        fill's persistent launch leaves R CUs' worth of workgroup slots free, and without a CU mask
+        the dispatcher spreads both kernels' workgroups over every CU, so the text kernel's VALU
+        work can take issue slots from the fill waves on all of them (params.engine.text_cu_mask,
+        TAXI2_TEXT_MASK=1; profiles/r6/task/)."""
+        import torch
+
+        dev = torch.device("cuda", eng.device)
+        # CUs' worth of workgroup slots the fill leaves free for the previous block's text kernel
+        pipeline = os.environ.get("TAXI2_TEXT_PIPELINE", self.params.engine.text_pipeline)
+        if pipeline not in ("fused", "streams"):
+            raise ValueError(f"params.engine.text_pipeline: 'fused' or 'streams', not {pipeline!r}")
+        reserve = int(os.environ.get("TAXI2_TEXT_RESERVE_CUS", self.params.engine.text_reserve_cus))
+        copy_mode = int(os.environ.get("TAXI2_TEXT_COPY", self.params.engine.text_copy))
+        if pipeline == "fused":  # the fill takes every CU; nothing runs beside it but the host copies
+            reserve = 0
+            copy_mode = copy_mode or 1
+        ncu = eng.num_cus()
+        raw = []
+        mask = os.environ.get("TAXI2_TEXT_MASK", "1" if self.params.engine.text_cu_mask else "") not in ("", "0")
+        eng.set_text_copy(copy_mode if pipeline == "streams" else 0)
+        if 0 < reserve < ncu and mask:
+            # fill, text, and the block writers' formatters (on the text CUs, their own queue)
+            raw = [eng.cu_stream(reserve, ncu - reserve), eng.cu_stream(0, reserve), eng.cu_stream(0, reserve)]
+            stream, tstream, wstream = (torch.cuda.ExternalStream(h, device=dev) for h in raw)
+        else:
+            wstream = None
+            stream = torch.cuda.Stream(dev)
+            # high priority: a queue of its own beside the fill's (HIP multiplexes streams onto
+            # GPU_MAX_HW_QUEUES hardware queues, and two streams sharing one run their kernels in
+            # order), and the dispatcher hands freed slots to the text first
+            tstream = torch.cuda.Stream(dev, priority=0 if os.environ.get("TAXI2_TEXT_PRIO") == "0" else -1)
+        try:
+            # the fused pipeline's host copies: a stream of their own (the DMA engine, or the copy
+            # kernel, beside the queued fills)
+            cstream = torch.cuda.Stream(dev)
+            return self._tri_with_pairs_on(seqs, eng, st, D, cidx, clabels, scores, fh, stream, tstream, wstream,
+                                           cstream, reserve, pipeline, copy_mode)
+        finally:
+            eng.set_text_copy(0)
+            if raw:
+                for s_ in (stream, tstream, wstream):
+                    s_.synchronize()
+                for h in raw:
+                    eng.destroy_stream(h)
+
+    def _tri_with_pairs_on(self, seqs, eng, st, D, cidx, clabels, scores, fh, stream, tstream, wstream, cstream,
+                           reserve, pipeline, copy_mode) -> bool:
         """aligned_pairs.txt and the counter metrics from ONE fill per unordered pair: the triangle
         in row blocks (taxi2_tri_strings_dev: the walkers walk both orientations, as the metric
         kernel does), the (a, b) strings formatted with row a's block, the (b, a) strings compacted
@@ -340,7 +399,6 @@ class VersusAll:
         # a triangle block fills each pair once for both orientations: twice launch_pairs of them
         # per launch (fewer launch tails and per-block host steps; the slots still fit slot_budget)
         target = max(1, min(2 * launch, slot_budget // per_pair) if launch else slot_budget // per_pair)
-        stream = torch.cuda.Stream(dev)
         # the counter metrics land in a device copy of D (scattered on the GPU) unless that copy
         # would be large.  Rows [x0, x1) are complete once their block is scattered (the (r, c < r)
         # values come from earlier blocks): they go to a pinned staging buffer behind the block's
@@ -363,6 +421,24 @@ class VersusAll:
             blocks.append((x0, x1, cnt))
             x0 = x1
         rows_max = max(b[1] - b[0] for b in blocks)
+        fused = pipeline == "fused"
+        if fused:
+            # kept (b, a) storage bound per row a: sum over b > a of la + lb columns
+            suf = np.concatenate([np.cumsum(lens_h[::-1])[::-1], [0]])
+            keep_bound = (n - 1 - np.arange(n)) * lens_h + suf[1:]
+            ids_d = torch.as_tensor(ids[0].copy(), device=dev)
+            ioffs_d = torch.as_tensor(ids[1], device=dev)
+            nch = -(-n // 256)
+            tb_max = max(int(row_text_bound[b[0]:b[1]].sum()) for b in blocks) + 16
+            # PIPE_DEPTH + 1 text buffers: block k + PIPE_DEPTH + 1 is launched after post(k) has
+            # moved block k's text out
+            tslots = [dict(text=torch.empty(tb_max, dtype=torch.uint8, device=dev),
+                           total=torch.zeros(2, dtype=torch.int64, device=dev),
+                           scratch=torch.empty(2 * rows_max * nch, dtype=torch.int64, device=dev))
+                      for _ in range(PIPE_DEPTH + 1)]
+            b_index = [0]
+            htot = torch.zeros(2, dtype=torch.int64, pin_memory=True)
+            pins = []
         stage = [None, None, None]  # pinned buffer, its event, the rows (x0, x1) it holds
         if Dd is not None:
             stage[0] = torch.empty((rows_max, n, Mc), dtype=torch.float64, pin_memory=True)
@@ -390,10 +466,6 @@ class VersusAll:
         # block k's event.  Tensors of a block are
         # record_stream()'d on tstream before they are dropped, so the caching allocator never hands
         # their memory to the next block while the text still reads it.
-        # high priority: a queue of its own beside the fill's (HIP multiplexes streams onto
-        # GPU_MAX_HW_QUEUES hardware queues, and two streams sharing one run their kernels in
-        # order), and the dispatcher hands freed slots to the text first
-        tstream = torch.cuda.Stream(dev, priority=0 if os.environ.get("TAXI2_TEXT_PRIO") == "0" else -1)
         with torch.cuda.stream(stream):
             lens = torch.as_tensor(lens_h, device=dev)
             # self alignments (x, x) for the diagonal pairs' text
@@ -447,6 +519,7 @@ class VersusAll:
 
             sink = _BlockWriters(self, seqs, Engine(eng.device), files=True, walk=False, pairs=False)
             sink.rmin_k = None  # (row minima: the streamed path's extra, not the dense path's)
+            sink._wstream = wstream  # None: the writers make their own
             sink.diag = self._diag_info(seqs, eng, st, True, scores, [str(m) for m in self.params.distances.metrics])
             writers = ThreadPoolExecutor(1, thread_name_prefix="taxi2-writers")
             scale = 100.0 if self.params.format.percentage_multiply else 1.0
@@ -456,10 +529,9 @@ class VersusAll:
                 Abuf = [torch.empty((rows_max, n, Mc), dtype=torch.float64, device=dev) for _ in range(3)]
             nblk = [0]
 
-        # CUs' worth of workgroup slots the fill leaves free, so that the previous block's text kernel
-        # (bound by the host link it writes through) runs beside it instead of after it
-        # (measured at N = 5 000: 0 -> 4.9 s, 16 -> 4.2 s, 32 -> 3.6 s, 48 -> 3.6 s, profiles/r5/task_reserve/)
-        reserve = int(os.environ.get("TAXI2_TEXT_RESERVE_CUS", self.params.engine.text_reserve_cus))
+        # `reserve`: CUs' worth of workgroup slots the fill leaves free, so that the previous block's
+        # text kernel runs beside it instead of after it (round 5, unmasked streams, N = 5 000:
+        # 0 -> 4.9 s, 16 -> 4.2 s, 32 -> 3.6 s, 48 -> 3.6 s, profiles/r5/task_reserve/)
         fill_ev = []  # (start, end) events of every block's fill: the fills' GPU time for task.timings
 
         def launch(x0: int, x1: int, cnt: int):
@@ -490,7 +562,87 @@ class VersusAll:
                     Dd[rb, ra] = d[:, 1, :]
                 ev = torch.cuda.Event()
                 ev.record(stream)
-            return dict(x0=x0, x1=x1, k0=k0, cnt=cnt, d=d, sx=sx, sy=sy, sl=sl, ra=ra, rb=rb, ev=ev)
+                blk = dict(x0=x0, x1=x1, k0=k0, cnt=cnt, d=d, sx=sx, sy=sy, sl=sl, ra=ra, rb=rb, ev=ev)
+                if fused:
+                    text_on_fill_stream(blk)
+            return blk
+
+        def text_on_fill_stream(b) -> None:
+            """Fused pipeline: block b's compaction of its kept (b, a) strings and its whole
+            aligned_pairs.txt text (taxi2_format_pairs_ptr_async: lengths, offsets and text on the
+            device, no host synchronisation) queued on the fill stream right behind its fill, so they
+            run on the whole chip between two fills (~1 ms of text kernel per GB) instead of waiting
+            for CU slots beside a persistent fill; the text lands in one of NT device buffers and
+            post() moves it to the host beside the next fills (DMA engine or copy kernel)."""
+            x0, x1, k0, cnt = b["x0"], b["x1"], b["k0"], b["cnt"]
+            end = L1 = off = None
+            if cnt:
+                sx, sy, sl, ra, rb = b["sx"], b["sy"], b["sl"], b["ra"], b["rb"]
+                end = (lens[ra] + lens[rb]).to(torch.int64)
+                L1 = sl[:, 1].to(torch.int64)
+                off = torch.cumsum(L1, 0) - L1
+                # kept storage by the host bound (an alignment has at most la + lb columns): no
+                # read-back of the exact total behind the fill
+                nb = int(keep_bound[x0:x1].sum())
+                kxy = carve(2 * max(1, nb), cnt, k0 + cnt)
+                kx, ky = kxy[:max(1, nb)], kxy[max(1, nb):]
+                eng.pack_slots_dev(sx.data_ptr(), sy.data_ptr(), sl.data_ptr(), cap, 2, 1, end.data_ptr(),
+                                   off.data_ptr(), cnt, kx.data_ptr(), ky.data_ptr(), stream.cuda_stream)
+                kpx[k0:k0 + cnt] = kx.data_ptr() + off
+                kpy[k0:k0 + cnt] = ky.data_ptr() + off
+                klen[k0:k0 + cnt] = sl[:, 1]
+                kept_b[0] += 2 * nb
+                px, py, ln = pointers(x0, x1, k0, cnt, sx, sy, sl, end)
+            else:
+                px, py, ln = pointers(x0, x1, k0, 0)
+            slot = tslots[b_index[0] % len(tslots)]
+            b_index[0] += 1
+            eng.format_pairs_ptr_async(x1 - x0, n, px.data_ptr(), py.data_ptr(), ln.data_ptr(), ids_d.data_ptr(),
+                                       ioffs_d.data_ptr() + 8 * x0, ids_d.data_ptr(), ioffs_d.data_ptr(),
+                                       first=x0 == 0, text_ptr=slot["text"].data_ptr(), cap=slot["text"].numel(),
+                                       total_ptr=slot["total"].data_ptr(), scratch_ptr=slot["scratch"].data_ptr(),
+                                       stream=stream.cuda_stream)
+            tev = torch.cuda.Event()
+            tev.record(stream)
+            b.update(tslot=slot, tev=tev, keep=(end, L1, off, px, py, ln))
+
+        def ensure_pins() -> None:
+            if not pins:
+                psz = min(max(TEXT_CALL_BYTES, 1 << 20), int(row_text_bound.sum()) + 16)
+                pins.extend(torch.empty(psz, dtype=torch.uint8, pin_memory=True) for _ in range(2))
+
+        def text_to_host(b) -> None:
+            """Block b's text from its device buffer to the file: its length read back on the copy
+            stream once the text kernel is done, then <= TEXT_CALL_BYTES pieces through two pinned
+            buffers (piece j's transfer runs while piece j - 1 is written)."""
+            slot = b["tslot"]
+            with torch.cuda.stream(cstream):
+                cstream.wait_event(b["tev"])
+                htot.copy_(slot["total"], non_blocking=True)
+                cstream.synchronize()
+                total_b, fit = int(htot[0]), int(htot[1])
+                if not fit:
+                    raise NativeError(f"aligned_pairs text of rows {b['x0']}-{b['x1']} outgrew its bound")
+                if not pins:  # (a keep-budget switch before the pipeline's setup)
+                    ensure_pins()
+                prev = None
+                piece = pins[0].numel()
+                for j, o in enumerate(range(0, total_b, piece)):
+                    nbj = min(piece, total_b - o)
+                    buf = pins[j % 2]
+                    if copy_mode == 2:
+                        eng.copy_text_dev(slot["text"].data_ptr() + o, buf.data_ptr(), nbj, cstream.cuda_stream)
+                    else:
+                        buf[:nbj].copy_(slot["text"][o:o + nbj], non_blocking=True)
+                    evj = torch.cuda.Event()
+                    evj.record(cstream)
+                    if prev is not None:
+                        prev[0].synchronize()
+                        fh.write(memoryview(prev[1].numpy()[:prev[2]]))
+                    prev = (evj, buf, nbj)
+                if prev is not None:
+                    prev[0].synchronize()
+                    fh.write(memoryview(prev[1].numpy()[:prev[2]]))
 
         prof = {} if os.environ.get("TAXI2_TASK_PROFILE") else None
 
@@ -530,7 +682,20 @@ class VersusAll:
                     tl[0] = t
 
             with torch.cuda.stream(tstream):
-                if cnt:
+                if fused:
+                    if cnt:
+                        tstream.wait_event(b["ev"])
+                        if Dd is None:
+                            b["d"].record_stream(tstream)
+                            dd = b["d"].cpu().numpy()
+                            a_h, b_h = b["ra"].cpu().numpy(), b["rb"].cpu().numpy()
+                            for q, kk in enumerate(cidx):
+                                D[a_h, b_h, kk] = dd[:, 0, q]
+                                D[b_h, a_h, kk] = dd[:, 1, q]
+                    mark("wait")
+                    text_to_host(b)
+                    mark("text")
+                elif cnt:
                     tstream.wait_event(b["ev"])
                     for key in ("d", "sx", "sy", "sl", "ra", "rb"):
                         b[key].record_stream(tstream)
@@ -556,14 +721,15 @@ class VersusAll:
                     kpy[k0:k0 + cnt] = ky.data_ptr() + off
                     klen[k0:k0 + cnt] = sl[:, 1]
                     kept_b[0] += 2 * tot
-                mark("pack")
-                px, py, ln = pointers(x0, x1, k0, cnt, sx, sy, sl, end) if cnt else pointers(x0, x1, k0, 0)
-                mark("pointers")
+                if not fused:
+                    mark("pack")
+                    px, py, ln = pointers(x0, x1, k0, cnt, sx, sy, sl, end) if cnt else pointers(x0, x1, k0, 0)
+                    mark("pointers")
                 # the text in row runs of at most TEXT_CALL_BYTES (an upper bound from the lengths):
                 # the pinned buffer the kernel writes into stays ~1 GB, allocated once -- a block's
                 # whole text (~4 GB at N = 5 000) took ~1 s to pin, twice as the buffer grew
                 r0 = x0
-                while r0 < x1:
+                while r0 < x1 and not fused:
                     r1 = r0 + 1
                     tot_b = row_text_bound[r0]
                     while r1 < x1 and tot_b + row_text_bound[r1] <= TEXT_CALL_BYTES:
@@ -574,7 +740,8 @@ class VersusAll:
                                                       ln.data_ptr() + 4 * o, (ids[0], ids[1][r0:r1 + 1]), ids,
                                                       first=r0 == 0, stream=tstream.cuda_stream))
                     r0 = r1
-                mark("text")
+                if not fused:
+                    mark("text")
                 rows_in()  # the previous block's staged rows into D
                 rows_out(x0, x1)
                 mark("rows")
@@ -624,12 +791,16 @@ class VersusAll:
                 # a second chunk later)
                 first = False
                 tp = [perf_counter()]
-                eng._pinned_view(min(TEXT_CALL_BYTES, int(row_text_bound.sum())))
+                if fused:  # two pinned pieces for text_to_host (the arena: carve() on block 0)
+                    ensure_pins()
+                else:
+                    eng._pinned_view(min(TEXT_CALL_BYTES, int(row_text_bound.sum())))
                 tp.append(perf_counter())
                 ls = np.sort(lens_h)
                 est = int(2.08 * float(np.dot(ls, np.arange(n, dtype=np.float64)))) + (1 << 20)
                 with torch.cuda.stream(tstream):
-                    arena[0] = torch.empty(max(1, min(est, keep_limit)), dtype=torch.uint8, device=dev)
+                    if not fused:
+                        arena[0] = torch.empty(max(1, min(est, keep_limit)), dtype=torch.uint8, device=dev)
                     tp.append(perf_counter())
                     # the first use of each torch kernel of post() loads its code object (~0.2 s in
                     # all): a one-row dummy block here, while the GPU aligns
@@ -637,8 +808,9 @@ class VersusAll:
                         (1, 2), dtype=torch.int32, device=dev)
                     pointers(0, 1, 0, 1, z8, z8, z32, torch.zeros(1, dtype=torch.int64, device=dev))
                 tp.append(perf_counter())
-                arena[1] = 0
-                kept.append(arena[0])
+                if not fused:
+                    arena[1] = 0
+                    kept.append(arena[0])
                 if prof is not None:
                     print("taxi2 task setup: pinned %.1f arena %.1f warm %.1f ms" % tuple(
                         1e3 * (tp[i + 1] - tp[i]) for i in range(3)), file=sys.stderr)

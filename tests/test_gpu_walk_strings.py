@@ -122,16 +122,27 @@ def test_task_pairs_from_walks_equal_round2_path(tmp_path, engine, variant, stre
         assert (tmp_path / "walk" / f).read_bytes() == (tmp_path / "r2" / f).read_bytes(), f
 
 
+@pytest.mark.parametrize("pipeline", ["fused_dma", "fused_kernel", "streams", "streams_mask"])
 @pytest.mark.parametrize("mode", ["one_block", "small_blocks", "switch", "split_text"])
 @pytest.mark.parametrize("variant", ["default", "generic"])
-def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant, monkeypatch):
+def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant, pipeline, monkeypatch):
     """Dense aligned_pairs.txt from ONE fill per unordered pair (taxi2_tri_strings_dev: both
     orientations walked, the (b, a) strings kept in HBM until row b, text through per-pair pointers)
     == the rect path that aligns every ordered pair once (TAXI2_PAIRS_RECT=1), every output file
     byte for byte: one block, many small blocks (the pipeline two blocks deep, the writers formatting
     each block from HBM), a keep budget that runs out mid-way (the remaining rows switch to the rect
-    path), and a block's text split over many formatter calls (a one-row bound per call)."""
+    path), and a block's text split over many formatter calls (a one-row bound per call).  Every
+    text pipeline (params.engine.text_pipeline): the text queued on the fill stream and moved by the
+    DMA engine or the copy kernel, and the second-stream text beside the fills (plain or CU-masked
+    streams)."""
     from taxi2_amd.tasks import versus_all as VA
+
+    env = {"fused_dma": {"TAXI2_TEXT_PIPELINE": "fused", "TAXI2_TEXT_COPY": "1"},
+           "fused_kernel": {"TAXI2_TEXT_PIPELINE": "fused", "TAXI2_TEXT_COPY": "2"},
+           "streams": {"TAXI2_TEXT_PIPELINE": "streams", "TAXI2_TEXT_COPY": "0"},
+           "streams_mask": {"TAXI2_TEXT_PIPELINE": "streams", "TAXI2_TEXT_COPY": "2", "TAXI2_TEXT_MASK": "1"}}
+    for k, v in env[pipeline].items():
+        monkeypatch.setenv(k, v)
 
     if mode == "split_text":
         monkeypatch.setattr(VA, "TEXT_CALL_BYTES", 1)
