@@ -158,7 +158,8 @@ class VersusAll:
         self.params.engine.text_copy = 0
         # text_pipeline "fused": each block's compaction and text queued on the fill stream behind
         # its fill (whole chip, ~1 ms per GB), the text moved to the host beside the next fills by
-        # the DMA engine (text_copy 1) or a copy kernel (2), no CUs reserved; "streams": the text
+        # a copy kernel (text_copy 2, the default there: no LDS, so it co-runs with a persistent
+        # fill) or the DMA engine (1), no CUs reserved; "streams": the text
         # kernels on a second stream beside the fills, in text_reserve_cus CUs (round 5)
         self.params.engine.text_pipeline = "fused"
         self.params.engine.stream = None
@@ -331,7 +332,7 @@ class VersusAll:
         copy_mode = int(os.environ.get("TAXI2_TEXT_COPY", self.params.engine.text_copy))
         if pipeline == "fused":  # the fill takes every CU; nothing runs beside it but the host copies
             reserve = 0
-            copy_mode = copy_mode or 1
+            copy_mode = copy_mode or 2
         ncu = eng.num_cus()
         raw = []
         mask = os.environ.get("TAXI2_TEXT_MASK", "1" if self.params.engine.text_cu_mask else "") not in ("", "0")
