@@ -609,7 +609,8 @@ class VersusAll:
 
         def ensure_pins() -> None:
             if not pins:
-                psz = min(max(TEXT_CALL_BYTES, 1 << 20), int(row_text_bound.sum()) + 16)
+                # (a multiple of 16: every piece's source stays 16-aligned for the copy kernel)
+                psz = (min(max(TEXT_CALL_BYTES, 1 << 20), int(row_text_bound.sum()) + 16) + 15) // 16 * 16
                 pins.extend(torch.empty(psz, dtype=torch.uint8, pin_memory=True) for _ in range(2))
 
         def text_to_host(b) -> None:
