@@ -781,6 +781,9 @@ class VersusAll:
         for x0, x1, cnt in blocks:
             try:
                 blk = launch(x0, x1, cnt) if cnt else dict(x0=x0, x1=x1, k0=0, cnt=0)
+                if fused and not cnt:  # a block of the last row alone: its text still needs queueing
+                    with torch.cuda.stream(stream):
+                        text_on_fill_stream(blk)
             except NativeError as e:
                 if x0 == 0 and "walker strings need" in str(e):
                     return False

@@ -123,7 +123,7 @@ def test_task_pairs_from_walks_equal_round2_path(tmp_path, engine, variant, stre
 
 
 @pytest.mark.parametrize("pipeline", ["fused_dma", "fused_kernel", "streams", "streams_mask"])
-@pytest.mark.parametrize("mode", ["one_block", "small_blocks", "switch", "split_text"])
+@pytest.mark.parametrize("mode", ["one_block", "small_blocks", "switch", "split_text", "tail_row"])
 @pytest.mark.parametrize("variant", ["default", "generic"])
 def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant, pipeline, monkeypatch):
     """Dense aligned_pairs.txt from ONE fill per unordered pair (taxi2_tri_strings_dev: both
@@ -166,7 +166,9 @@ def test_task_pairs_one_fill_equals_rect_path(tmp_path, engine, mode, variant, p
                 t.params.pairs.scores = dict(Scores(match_score=2, mismatch_score=-3, internal_open_gap_score=-5,
                                                     internal_extend_gap_score=-2, end_open_gap_score=-1,
                                                     end_extend_gap_score=-1))
-            if mode != "one_block":
+            if mode == "tail_row":  # blocks ... (28, 34), (34, 35): the last row alone, no pairs of its own
+                t.params.engine.launch_pairs = 60
+            elif mode != "one_block":
                 t.params.engine.launch_pairs = 97  # a few rows per block
             if mode == "switch":
                 t.params.engine.keep_bytes = 40_000  # runs out after the first blocks
