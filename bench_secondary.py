@@ -139,7 +139,9 @@ def leg_task(eng, n: int = 5000) -> dict:
         "compute_basis": "fill_gpu_s (HIP events around each block's fill)" if ph.get("fill_gpu_s") else "compute_s",
         "text_reserve_cus": int(os.environ.get("TAXI2_TEXT_RESERVE_CUS", t.params.engine.text_reserve_cus)),
         "text_pipeline": os.environ.get("TAXI2_TEXT_PIPELINE", t.params.engine.text_pipeline),
-        "text_copy": int(os.environ.get("TAXI2_TEXT_COPY", t.params.engine.text_copy)),
+        # (the fused pipeline's transfer: 0 means its default, the copy kernel)
+        "text_copy": int(os.environ.get("TAXI2_TEXT_COPY", t.params.engine.text_copy)) or (
+            2 if os.environ.get("TAXI2_TEXT_PIPELINE", t.params.engine.text_pipeline) == "fused" else 0),
         "text_cu_mask": os.environ.get("TAXI2_TEXT_MASK", "1" if t.params.engine.text_cu_mask else "") not in ("", "0"),
         "phases_s": ph, "pairs_from_walks": bool(t.pairs_walked), "files": files,
     }
